@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): node GFLOPS of the range-partitioned,
+load-balanced bf16 SGEMM 8192³ across N MI355X (one process per GPU), plus the
+Mandelbrot 4096² event-pipeline number and the load-balancer convergence
+count ("load-balance iters") as extra fields.
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
+
+A step is one ``compute()`` of the whole 8192×8192×8192 GEMM through the
+framework: the balancer splits the 1024 (or 2048) output tiles across the
+ranks, every rank runs the hand-written CDNA4 MFMA kernel on its slice, the
+per-device times are exchanged and the next split is computed.  Inputs are
+device-resident after the first call and C stays in device memory
+(BASELINE.md "device-resident"); the host-resident variant (A/B uploaded and
+C slices downloaded each call) is reported separately.  Data: synthetic
+uniform [-1, 1) bf16.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+METRIC = "GFLOPS (node) SGEMM-8k + mandelbrot-4k at 1/2/4/8 MI355X; load-balance iters"
+
+
+def _sync():
+    import torch
+
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def _barrier(ctx):
+    if ctx.is_distributed:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def _max_over_ranks(ctx, v: float) -> float:
+    if not ctx.is_distributed:
+        return v
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", torch.cuda.current_device()) if (
+        dist.get_backend() == "nccl") else torch.device("cpu")
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _sum_over_ranks(ctx, v: float) -> float:
+    if not ctx.is_distributed:
+        return v
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", torch.cuda.current_device()) if (
+        dist.get_backend() == "nccl") else torch.device("cpu")
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def timed(ctx, fn, steps: int, warmup: int) -> float:
+    for _ in range(warmup):
+        fn()
+    _barrier(ctx)
+    _sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    _sync()
+    _barrier(ctx)
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    return _max_over_ranks(ctx, ms)
+
+
+def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
+    from cekirdekler_amd.ops.gemm import GemmBf16
+    from cekirdekler_amd.ops.library import library
+    from cekirdekler_amd.parallel.distributed import DistributedCruncher
+
+    if tile is None:
+        tile = "256x256" if (size // 256) ** 2 // ctx.world >= 256 else "256x128"
+    cr = DistributedCruncher("", ctx=ctx, prebuilt=library("sgemm_bf16"))
+    g = GemmBf16(size, size, size, cruncher=cr, tile=tile)
+    ms = timed(ctx, lambda: g.run(compute_id=1, resident=True), steps, warmup)
+    host_steps = max(2, min(steps, 5))
+    ms_host = timed(ctx, lambda: g.run(compute_id=2, resident=False), host_steps, 1)
+    ranges = cr.ranges(1)
+    return {"ms": ms, "gflops": g.flops / (ms * 1e-3) / 1e9, "tile": tile,
+            "host_resident_ms": ms_host, "host_resident_gflops": g.flops / (ms_host * 1e-3) / 1e9,
+            "ranges": ranges}
+
+
+def bench_mandelbrot(ctx, steps, warmup):
+    try:
+        from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
+        from cekirdekler_amd.parallel.distributed import DistributedCruncher
+        from cekirdekler_amd.ops.library import library
+    except Exception as e:  # pragma: no cover
+        return {"error": f"unavailable: {e}"}
+    cr = DistributedCruncher("", ctx=ctx, prebuilt=library("mandelbrot"))
+    m = MandelbrotRenderer(4096, 4096, max_iter=256, cruncher=cr)
+    ms = timed(ctx, lambda: m.render(compute_id=3, pipeline=True), max(3, steps // 2), warmup)
+    flops = _sum_over_ranks(ctx, m.flops())
+    return {"ms": ms, "gflops": flops / (ms * 1e-3) / 1e9, "flop_per_iter": 8}
+
+
+def bench_lb_iters():
+    """Computes until every device share is within 5% of steady state, on two
+    logical devices of this GPU with an injected 2:1 slowdown (the reference
+    law converges as 0.7^k)."""
+    import cekirdekler_amd as ck
+
+    plats = ck.ClPlatforms.all()
+    gpus = plats.gpus()
+    devs = (gpus[0] + gpus[0]) if len(gpus) else (plats.cpus(True) + plats.cpus(True))
+    src = "__global__ void k(float* x){ long long i = get_global_id(0); x[i] = x[i] * 1.0001f + 1.0f; }"
+    cr = ck.ClNumberCruncher(devs, src)
+    cr.set_time_scale(1, 2.0)
+    n = 1 << 22
+    x = ck.ClArray(n, np.float32)
+    x.read = False
+    x.write = False
+    shares = []
+    for _ in range(40):
+        x.compute(cr, 7, "k", n, 256)
+        r = cr.ranges(7)
+        shares.append(r[0] / sum(r))
+    steady = shares[-1]
+    it = next(i for i in range(len(shares)) if all(abs(s - steady) <= 0.05 * steady for s in shares[i:]))
+    cr.dispose()
+    return {"iters": it + 1, "steady_share_dev0": steady}
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--size", type=int, default=8192)
+    ap.add_argument("--tile", default=None)
+    ap.add_argument("--skip-mandelbrot", action="store_true")
+    args = ap.parse_args(argv)
+
+    from cekirdekler_amd.parallel.distributed import init_distributed
+
+    ctx = init_distributed()
+    sg = bench_sgemm(ctx, args.steps, args.warmup, args.size, args.tile)
+    mb = {} if args.skip_mandelbrot else bench_mandelbrot(ctx, args.steps, args.warmup)
+    lb = bench_lb_iters() if ctx.rank == 0 else {}
+    if ctx.rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(sg["gflops"], 1),
+            "unit": "GFLOPS",
+            "n_gpus": ctx.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(sg["ms"], 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic",
+            "config": {"model": f"SGEMM {args.size}x{args.size}x{args.size} bf16 (fp32 acc/out), "
+                                f"range-partitioned + load-balanced, tile {sg['tile']}",
+                       "global_batch": 1, "seq_len": args.size,
+                       "parallelism": f"range-partition dp{ctx.world}"},
+            "extra": {
+                "sgemm_device_resident_gflops": round(sg["gflops"], 1),
+                "sgemm_host_resident_gflops": round(sg["host_resident_gflops"], 1),
+                "sgemm_host_resident_ms": round(sg["host_resident_ms"], 3),
+                "sgemm_ranges": sg["ranges"],
+                "mandelbrot_4k": mb,
+                "load_balance_iters": lb,
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if ctx.is_distributed:
+        import torch.distributed as dist
+
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

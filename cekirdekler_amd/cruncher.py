@@ -1,0 +1,448 @@
+"""``ClNumberCruncher`` — the entry API (reference ClNumberCruncher.cs:56-415)
+and ``Cores`` usage-type-2 API (reference Cores.cs:37-1982).
+
+A cruncher JIT-compiles one HIP C++ (or OpenCL-C dialect) kernel string for
+every selected device (hiprtc → gfx950 code object per GPU, host compiler for
+the CPU device), owns a native ``Cores`` scheduler, and executes
+``ClArray``/``ClParameterGroup.compute(...)`` calls: the global range is split
+across devices by the iterative load balancer per compute id.
+"""
+from __future__ import annotations
+
+import enum
+import re
+from typing import List, Optional, Sequence
+
+from ._native import cek, kernel_dir
+from .arrays import ClArray, ClParameterGroup, _register_cores, as_clarray
+from .hardware import ClDevices, ClPlatforms
+
+PIPELINE_EVENT = True    # Cores.PIPELINE_EVENT (Cores.cs:416-423)
+PIPELINE_DRIVER = False  # Cores.PIPELINE_DRIVER
+
+_SPLIT = re.compile(r"[ ,;\-\n@]+")
+
+
+class AcceleratorType(enum.IntFlag):
+    """Device classes (reference ``AcceleratorType``, ClNumberCruncher.cs:32-49)."""
+    CPU = 1
+    GPU = 2
+    ACC = 4
+
+
+class ClComputeError(ValueError):
+    """A compute() call was rejected by validation (work-size/array-size)."""
+
+
+def split_kernel_names(kernels) -> List[str]:
+    if isinstance(kernels, (list, tuple)):
+        return [k for k in kernels if k]
+    return [k for k in _SPLIT.split(kernels.strip()) if k]
+
+
+def select_devices(types, num_gpus: int = -1, cpu_cores: int = -1, stream: bool = True) -> ClDevices:
+    """Device discovery from an AcceleratorType (reference Cores ctor,
+    Cores.cs:156-273: CPUs partitioned to N-1 cores, GPUs capped by
+    numberOfGPUsToUse)."""
+    if isinstance(types, str):
+        t = 0
+        low = types.lower()
+        t |= AcceleratorType.CPU if "cpu" in low else 0
+        t |= AcceleratorType.GPU if "gpu" in low else 0
+        t |= AcceleratorType.ACC if "acc" in low else 0
+        types = AcceleratorType(t)
+    plats = ClPlatforms.all()
+    devs = ClDevices([])
+    if types & AcceleratorType.CPU:
+        devs = devs + plats.cpus(True, stream, cpu_cores)
+    if types & AcceleratorType.GPU:
+        g = plats.gpus(False)
+        if num_gpus is not None and num_gpus > 0:
+            g = g[:num_gpus]
+        devs = devs + g
+    return devs
+
+
+class ClNumberCruncher:
+    """Compiles a kernel string for a device set and runs computes on it.
+
+    ``ClNumberCruncher(AcceleratorType.GPU, src)`` or
+    ``ClNumberCruncher(ClPlatforms.all().gpus(), src)``.  ``prebuilt`` adds
+    AOT code objects (``[(path, [names])]``) — the library kernels of
+    :mod:`cekirdekler_amd.ops` use this.
+    """
+
+    def __init__(self, devices, kernel_source: str = "", cpu_cores: int = -1, num_gpus: int = -1,
+                 stream: bool = True, no_pipelining: bool = False, queue_concurrency: int = 16,
+                 prebuilt: Optional[Sequence] = None, options: Optional[Sequence[str]] = None,
+                 smooth: bool = True):
+        if isinstance(devices, (AcceleratorType, int, str)):
+            devices = select_devices(devices, num_gpus, cpu_cores, stream)
+        if not isinstance(devices, ClDevices):
+            devices = ClDevices(list(devices))
+        self.devices = devices
+        self.kernel_source = kernel_source or ""
+        if "enqueue_kernel" in self.kernel_source:
+            raise NotImplementedError(
+                "device-side enqueue (OpenCL 2.0 enqueue_kernel) has no HIP equivalent; "
+                "launch follow-up kernels from the host (compute() with several kernel names)")
+        cfg = cek.CoresConfig()
+        cfg.queue_concurrency = int(queue_concurrency)
+        cfg.no_pipelining = bool(no_pipelining)
+        cfg.smooth = bool(smooth)
+        cfg.options = list(options or [])
+        cfg.prebuilt = [p if isinstance(p, str) else f"{p[0]}|{','.join(p[1])}" for p in (prebuilt or [])]
+        self.repeat_count = 1
+        self.repeat_kernel_name = ""
+        self.performance_feed = False
+        self.number_of_errors_happened = 0
+        self._cores = None
+        if len(devices) == 0:
+            self._error_code, self._error_message = 1, "no device selected"
+            return
+        self._cores = cek.Cores([d.native_info() for d in devices], self.kernel_source, cfg)
+        self._error_code = self._cores.error_code
+        self._error_message = self._cores.error_message
+        if self._error_code:
+            self.number_of_errors_happened += 1
+        _register_cores(self)
+
+    # ------------------------------------------------------------ status
+    def error_code(self) -> int:
+        return self._error_code
+
+    def error_message(self) -> str:
+        return self._error_message
+
+    errorCode = error_code
+    errorMessage = error_message
+
+    @property
+    def cores(self):
+        if self._cores is None:
+            raise RuntimeError("cruncher has no native core (disposed or failed)")
+        return self._cores
+
+    @property
+    def kernel_names(self) -> List[str]:
+        return [k.name for k in self._cores.kernels] if self._cores else []
+
+    def device_names(self) -> List[str]:
+        return [self._cores.device(i).name for i in range(self._cores.num_devices)]
+
+    deviceNames = device_names
+
+    @property
+    def number_of_devices(self) -> int:
+        return self._cores.num_global_devices if self._cores else 0
+
+    # ------------------------------------------------------------ modes
+    def _prop(name):  # noqa: N805
+        def get(self):
+            return getattr(self._cores, name) if self._cores else False
+
+        def set_(self, v):
+            if self._cores:
+                setattr(self._cores, name, bool(v))
+        return property(get, set_)
+
+    no_compute_mode = _prop("no_compute")
+    fine_grained_queue_control = _prop("fine_grained")
+    enqueue_mode_async_enable = _prop("async_enqueue")
+    enqueue_mode = _prop("enqueue_mode")
+    smooth_load_balancer = _prop("smooth")
+    noComputeMode = no_compute_mode
+    fineGrainedQueueControl = fine_grained_queue_control
+    enqueueModeAsyncEnable = enqueue_mode_async_enable
+    enqueueMode = enqueue_mode
+    smoothLoadBalancer = smooth_load_balancer
+    del _prop
+
+    @property
+    def repeatCount(self) -> int:  # noqa: N802
+        return self.repeat_count
+
+    @repeatCount.setter
+    def repeatCount(self, v: int) -> None:  # noqa: N802
+        self.repeat_count = int(v)
+
+    @property
+    def repeatKernelName(self) -> str:  # noqa: N802
+        return self.repeat_kernel_name
+
+    @repeatKernelName.setter
+    def repeatKernelName(self, v: str) -> None:  # noqa: N802
+        self.repeat_kernel_name = v or ""
+
+    @property
+    def performanceFeed(self) -> bool:  # noqa: N802
+        return self.performance_feed
+
+    @performanceFeed.setter
+    def performanceFeed(self, v: bool) -> None:  # noqa: N802
+        self.performance_feed = bool(v)
+
+    def flush_last_used_command_queue(self) -> None:
+        """HIP submits at enqueue time; kept for API parity (clFlush)."""
+
+    flushLastUsedCommandQueue = flush_last_used_command_queue
+
+    def sync(self) -> None:
+        """Wait for every queued operation on every device."""
+        if self._cores:
+            self._cores.finish()
+
+    def count_markers_reached(self) -> int:
+        return int(self._cores.markers_reached()) if self._cores else 0
+
+    def count_markers_remaining(self) -> int:
+        return int(self._cores.markers_issued() - self._cores.markers_reached()) if self._cores else 0
+
+    countMarkersReached = count_markers_reached
+    countMarkersRemaining = count_markers_remaining
+
+    # ------------------------------------------------------------ balancer state
+    def ranges(self, compute_id: int) -> List[int]:
+        return list(self._cores.ranges(compute_id))
+
+    def references(self, compute_id: int) -> List[int]:
+        return list(self._cores.references(compute_id))
+
+    def benchmarks(self, compute_id: int) -> List[float]:
+        return list(self._cores.benchmarks(compute_id))
+
+    def normalized_compute_powers_of_devices(self, compute_id: Optional[int] = None):
+        c = self._cores
+        cid = c.last_compute_id if compute_id is None else compute_id
+        if not c or not c.has_state(cid):
+            return None
+        b, r = c.benchmarks(cid), c.ranges(cid)
+        tot = sum(b) + 0.01 * len(b)
+        thr = [(tot / (bi + 0.01)) * (ri + 1) for bi, ri in zip(b, r)]
+        s = sum(thr) or 1.0
+        return [x / s for x in thr]
+
+    def normalized_global_ranges_of_devices(self, compute_id: int):
+        c = self._cores
+        if not c or not c.has_state(compute_id):
+            return None
+        r = c.ranges(compute_id)
+        s = float(sum(r)) or 1.0
+        return [x / s for x in r]
+
+    normalizedComputePowersOfDevices = normalized_compute_powers_of_devices
+    normalizedGlobalRangesOfDevices = normalized_global_ranges_of_devices
+
+    def performance_report(self, compute_id: int = 0) -> str:
+        """Console table of load distribution and per-device times
+        (reference Cores.performanceReport, Cores.cs:994-1063)."""
+        c = self._cores
+        if compute_id == 0:
+            ids = c.compute_ids()
+            if not ids:
+                s = "Needs one more compute to profile. Load balancer needs multiple iterations to be useful."
+                print(s)
+                return s
+            compute_id = ids[0]
+        if not c.has_state(compute_id):
+            s = "Error: Global range array is not ready."
+            print(s)
+            return s
+        r = c.ranges(compute_id)
+        b = c.benchmarks(compute_id)
+        tot = float(sum(r)) or 1.0
+        pct = "----- Load Distributions: " + "".join(f" [{100.0 * x / tot:.1f}%] -" for x in r)
+        pct += "-" * max(0, 50 - len(pct))
+        lines = ["", "", f"Compute-ID: {compute_id}  {pct}" + "-" * 48]
+        base = c.global_base
+        for i in range(len(r)):
+            if 0 <= i - base < c.num_devices:
+                d = c.device(i - base)
+                kind = "gddr" if (d.dedicated_memory and not d.streaming) else "stream"
+                name = d.name.strip()
+            else:
+                kind, name = "remote", f"rank-device {i}"
+            head = f"Device {i}({kind}): {name}"
+            head = head[:50].ljust(50)
+            lines.append(f"{head} ||| time: {b[i]:,.2f}ms, workitems: {r[i]:,}")
+        lines.append("-" * 113)
+        s = "\n".join(lines) + "\n"
+        print(s)
+        return s
+
+    performanceReport = performance_report
+
+    def last_compute_performance_report(self) -> str:
+        return self.performance_report(self._cores.last_compute_id)
+
+    lastComputePerformanceReport = last_compute_performance_report
+
+    def last_record(self) -> dict:
+        """Structured record of the last compute (observability)."""
+        r = self._cores.last_record()
+        return {"compute_id": r.compute_id, "wall_ms": r.wall_ms, "ranges": list(r.ranges),
+                "references": list(r.references), "device_ms": list(r.device_ms),
+                "h2d_bytes": r.h2d_bytes, "d2h_bytes": r.d2h_bytes, "pipelined": r.pipelined}
+
+    # ------------------------------------------------------------ compute
+    def _validate(self, group: ClParameterGroup, names, G, L, pipeline, blobs) -> None:
+        D = self.number_of_devices
+        if self._error_code:
+            raise ClComputeError("Number-cruncher device compile error:\n" + self._error_message)
+        if G % L != 0:
+            raise ClComputeError(
+                f"Work-size error: global range({G}) is not an integer multiple of local range({L}).")
+        if pipeline and G % (L * blobs) != 0:
+            raise ClComputeError(
+                f"Work-size error: global range({G}) is not an integer multiple of "
+                f"(local range)*(number of pipeline blobs)=({L * blobs}).")
+        need = L * D * (blobs if pipeline else 1)
+        if G < need:
+            raise ClComputeError(
+                f"Work-size error: global work size({G}) must be equal to or greater than "
+                f"(number of selected devices)*(local worksize){'*(blobs)' if pipeline else ''}=({need})")
+        if not names:
+            raise ClComputeError("no kernel name given")
+        for a in group.arrays:
+            if a._partial or (a._write and not a._write_all):
+                if a.N < G * a.elements_per_work_item:
+                    raise ClComputeError(
+                        f"Array-size error: (global range)*(number of array elements per work item)="
+                        f"({G * a.elements_per_work_item}) must be equal to or less than array length ({a.N}).")
+
+    def _compute_group(self, group: ClParameterGroup, compute_id: int, kernels, global_range: int,
+                       local_range: int = 256, global_offset: int = 0, pipeline: bool = False,
+                       pipeline_type: bool = PIPELINE_EVENT, pipeline_blobs: int = 4) -> None:
+        names = split_kernel_names(kernels)
+        G, L = int(global_range), int(local_range)
+        try:
+            self._validate(group, names, G, L, pipeline, int(pipeline_blobs))
+        except ClComputeError:
+            self.number_of_errors_happened += 1
+            raise
+        call = cek.ComputeCall()
+        call.kernels = names
+        call.repeats = max(1, int(self.repeat_count))
+        call.repeat_kernel = self.repeat_kernel_name if self.repeat_count > 1 else ""
+        call.arrays = [a._spec() for a in group.arrays]
+        call.global_range = G
+        call.local_range = L
+        call.global_offset = int(global_offset)
+        call.compute_id = int(compute_id)
+        call.pipeline = bool(pipeline)
+        call.pipeline_event = bool(pipeline_type)
+        call.blobs = int(pipeline_blobs)
+        self._cores.compute(call)
+        if self.performance_feed:
+            self.performance_report(compute_id)
+
+    def compute(self, arrays, compute_id: int, kernels, global_range: int, local_range: int = 256,
+                global_offset: int = 0, pipeline: bool = False, pipeline_type: bool = PIPELINE_EVENT,
+                pipeline_blobs: int = 4) -> None:
+        """Functional form: ``cr.compute([a, b, c], 1, "k", G, L)``."""
+        group = arrays if isinstance(arrays, ClParameterGroup) else ClParameterGroup(arrays)
+        self._compute_group(group, compute_id, kernels, global_range, local_range, global_offset,
+                            pipeline, pipeline_type, pipeline_blobs)
+
+    # ------------------------------------------------------------ device data access
+    def upload(self, array: ClArray, device: int = 0) -> None:
+        self._cores.upload(device, as_clarray(array)._spec())
+
+    def download(self, array: ClArray, device: int = 0) -> None:
+        self._cores.download(device, as_clarray(array)._spec())
+
+    def device_pointer(self, array: ClArray, device: int = 0) -> int:
+        return int(self._cores.device_pointer(device, as_clarray(array)._spec()))
+
+    def _release_array(self, uid: int) -> None:
+        if self._cores is not None:
+            self._cores.release_array(uid)
+
+    def set_time_scale(self, device: int, scale: float) -> None:
+        """Test/bench hook: multiply a device's measured time (injected
+        heterogeneity for load-balancer convergence measurements)."""
+        self._cores.set_time_scale(device, float(scale))
+
+    # ------------------------------------------------------------ lifecycle
+    def dispose(self) -> None:
+        if self._cores is not None:
+            try:
+                self._cores.finish()
+            except Exception:
+                pass
+            self._cores = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.dispose()
+
+    def __repr__(self) -> str:
+        return f"<ClNumberCruncher devices={self.device_names() if self._cores else []} kernels={self.kernel_names}>"
+
+
+class Cores:
+    """Reference "usage type 2" API: ``Cores(types, src, names, ...)`` then
+    ``compute(names, repeats, syncKernel, arrays, readWrite, epw, G, id, ...)``
+    with the readWrite token strings ``partial read write all ro wo zc``
+    (ClArray.cs:611-629, Cores.cs:471)."""
+
+    def __init__(self, device_types, kernel_source: str, kernel_names=None, default_queue: bool = False,
+                 local_range: int = 256, num_gpus: int = -1, stream: bool = True, max_cpu: int = -1,
+                 no_pipelining: bool = False, devices: Optional[ClDevices] = None):
+        devs = devices if devices is not None else select_devices(device_types, num_gpus, max_cpu, stream)
+        self.local_range = local_range
+        self.cruncher = ClNumberCruncher(devs, kernel_source, no_pipelining=no_pipelining)
+        self.kernel_names = kernel_names or self.cruncher.kernel_names
+
+    @property
+    def number_of_devices(self) -> int:
+        return self.cruncher.number_of_devices
+
+    numberOfDevices = number_of_devices
+
+    def compute(self, kernel_names, repeats: int, repeat_kernel: str, arrays, read_writes: Sequence[str],
+                elements_per_item: Sequence[int], global_range: int, compute_id: int,
+                global_offset: int = 0, pipeline: bool = False, blobs: int = 4,
+                pipeline_type: bool = PIPELINE_EVENT, local_range: Optional[int] = None) -> None:
+        group = ClParameterGroup()
+        for arr, rw, e in zip(arrays, read_writes, elements_per_item):
+            a = as_clarray(arr)
+            toks = set(rw.split())
+            a._partial = "partial" in toks
+            a._read = "read" in toks
+            a._write = "write" in toks
+            a._write_all = "all" in toks
+            a._ro = "ro" in toks
+            a._wo = "wo" in toks
+            a.zero_copy = "zc" in toks
+            a.elements_per_work_item = int(e)
+            group.arrays.append(a)
+        self.cruncher.repeat_count = repeats
+        self.cruncher.repeat_kernel_name = repeat_kernel or ""
+        self.cruncher._compute_group(group, compute_id, kernel_names, global_range,
+                                     local_range or self.local_range, global_offset, pipeline,
+                                     pipeline_type, blobs)
+
+    def performance_report(self, compute_id: int = 0) -> str:
+        return self.cruncher.performance_report(compute_id)
+
+    performanceReport = performance_report
+
+    def benchmarks(self, compute_id: int):
+        return self.cruncher.benchmarks(compute_id)
+
+    def global_ranges(self, compute_id: int):
+        return self.cruncher.ranges(compute_id)
+
+    def global_references(self, compute_id: int):
+        return self.cruncher.references(compute_id)
+
+    def device_names(self):
+        return self.cruncher.device_names()
+
+    deviceNames = device_names
+
+    def dispose(self) -> None:
+        self.cruncher.dispose()

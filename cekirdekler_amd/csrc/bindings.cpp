@@ -1,0 +1,250 @@
+// pybind11 module `_cek`: the single Python↔C++ boundary of the runtime.
+// Every compute() crosses it once and releases the GIL for the fan-out.
+#include <pybind11/functional.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "balancer.h"
+#include "cores.h"
+#include "device.h"
+#include "dist.h"
+#include "jit.h"
+#include "memory.h"
+
+namespace py = pybind11;
+using namespace cek;
+
+namespace {
+
+class PyExchanger : public Exchanger {
+ public:
+  using Exchanger::Exchanger;
+  std::vector<double> allgather(const std::vector<double>& local) override {
+    PYBIND11_OVERRIDE_PURE(std::vector<double>, Exchanger, allgather, local);
+  }
+  int rank() const override { PYBIND11_OVERRIDE_PURE(int, Exchanger, rank, ); }
+  int world() const override { PYBIND11_OVERRIDE_PURE(int, Exchanger, world, ); }
+};
+
+uint64_t py_host_alloc(uint64_t bytes, uint64_t align) {
+  bool pinned = false;
+  return reinterpret_cast<uint64_t>(host_alloc(bytes, align, &pinned));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_cek, m) {
+  m.doc() = "cekirdekler_amd native runtime (HIP/gfx950)";
+
+  py::register_exception<Error>(m, "CekError", PyExc_RuntimeError);
+
+  py::enum_<DevType>(m, "DevType")
+      .value("CPU", kCPU)
+      .value("GPU", kGPU)
+      .value("ACC", kACC)
+      .export_values();
+
+  py::class_<DeviceInfo>(m, "DeviceInfo")
+      .def(py::init<>())
+      .def_readwrite("type", &DeviceInfo::type)
+      .def_readwrite("ordinal", &DeviceInfo::ordinal)
+      .def_readwrite("name", &DeviceInfo::name)
+      .def_readwrite("arch", &DeviceInfo::arch)
+      .def_readwrite("vendor", &DeviceInfo::vendor)
+      .def_readwrite("platform", &DeviceInfo::platform)
+      .def_readwrite("compute_units", &DeviceInfo::compute_units)
+      .def_readwrite("mem_bytes", &DeviceInfo::mem_bytes)
+      .def_readwrite("dedicated_memory", &DeviceInfo::dedicated_memory)
+      .def_readwrite("streaming", &DeviceInfo::streaming)
+      .def_readwrite("cpu_threads", &DeviceInfo::cpu_threads)
+      .def_readwrite("pci_bus", &DeviceInfo::pci_bus)
+      .def_readwrite("pci_device", &DeviceInfo::pci_device)
+      .def_readwrite("clock_khz", &DeviceInfo::clock_khz)
+      .def_readwrite("lds_per_block", &DeviceInfo::lds_per_block)
+      .def("describe", &DeviceInfo::describe)
+      .def("__repr__", [](const DeviceInfo& d) { return "<DeviceInfo " + d.describe() + ">"; });
+
+  m.def("gpu_count", &gpu_count);
+  m.def("enumerate_devices", &enumerate_devices);
+  m.def("gpu_info", &gpu_info);
+  m.def("cpu_info", &cpu_info, py::arg("threads") = -1);
+  m.def("enable_peer_access", &enable_peer_access);
+
+  py::class_<KernelSig>(m, "KernelSig")
+      .def_readonly("name", &KernelSig::name)
+      .def_readonly("arity", &KernelSig::arity)
+      .def("__repr__", [](const KernelSig& k) { return "<Kernel " + k.name + "/" + std::to_string(k.arity) + ">"; });
+  m.def("parse_kernels", &parse_kernels);
+  m.def("is_opencl_dialect", &is_opencl_dialect);
+  m.def("gpu_rewrite", &gpu_rewrite);
+  m.def("cpu_rewrite", &cpu_rewrite);
+  m.def("cache_dir", &cache_dir);
+  m.def("hash_hex", &hash_hex);
+  m.def("compile_gpu", [](const std::string& src, const std::vector<std::string>& opts, const std::string& arch) {
+    std::string code, log;
+    bool ok = compile_gpu(gpu_rewrite(src), opts, arch, code, log);
+    return py::make_tuple(ok, py::bytes(code), log);
+  }, py::arg("src"), py::arg("options") = std::vector<std::string>{}, py::arg("arch") = "gfx950");
+
+  m.def("host_alloc", &py_host_alloc, py::arg("bytes"), py::arg("align") = 4096);
+  m.def("host_free", [](uint64_t p) { host_free(reinterpret_cast<void*>(p)); });
+  m.def("host_is_pinned", [](uint64_t p) { return host_is_pinned(reinterpret_cast<void*>(p)); });
+  m.def("host_register", [](uint64_t p, uint64_t n) { return host_register(reinterpret_cast<void*>(p), n); });
+  m.def("host_unregister", [](uint64_t p) { host_unregister(reinterpret_cast<void*>(p)); });
+  m.def("copy_memory", [](uint64_t d, uint64_t s, uint64_t n) {
+    py::gil_scoped_release r;
+    copy_memory(reinterpret_cast<void*>(d), reinterpret_cast<const void*>(s), n);
+  });
+
+  m.def("load_balance", [](std::vector<double> bench, bool smooth, std::vector<std::vector<double>> history,
+                           long long total, std::vector<long long> ranges, long long step) {
+    load_balance(bench, smooth, history, total, ranges, step);
+    return py::make_tuple(ranges, history);
+  });
+  m.def("initial_split", [](int devices, bool smooth, std::vector<std::vector<double>> history,
+                            long long total, long long step) {
+    std::vector<long long> ranges;
+    initial_split(devices, smooth, history, total, ranges, step);
+    return py::make_tuple(ranges, history);
+  });
+  m.attr("HISTORY_DEPTH") = kHistoryDepth;
+
+  py::class_<ArraySpec>(m, "ArraySpec")
+      .def(py::init<>())
+      .def(py::init([](uint64_t uid, uint64_t host, uint64_t bytes, int elem_size, bool read, bool partial,
+                       bool write, bool write_all, bool ro, bool wo, bool zc, int epw) {
+             ArraySpec a;
+             a.uid = uid;
+             a.host = reinterpret_cast<void*>(host);
+             a.bytes = bytes;
+             a.elem_size = elem_size;
+             a.read = read;
+             a.partial = partial;
+             a.write = write;
+             a.write_all = write_all;
+             a.ro = ro;
+             a.wo = wo;
+             a.zc = zc;
+             a.epw = epw;
+             return a;
+           }),
+           py::arg("uid"), py::arg("host"), py::arg("bytes"), py::arg("elem_size"), py::arg("read") = true,
+           py::arg("partial") = false, py::arg("write") = true, py::arg("write_all") = false,
+           py::arg("ro") = false, py::arg("wo") = false, py::arg("zc") = false, py::arg("epw") = 1)
+      .def_readwrite("uid", &ArraySpec::uid)
+      .def_property("host", [](const ArraySpec& a) { return reinterpret_cast<uint64_t>(a.host); },
+                    [](ArraySpec& a, uint64_t p) { a.host = reinterpret_cast<void*>(p); })
+      .def_readwrite("bytes", &ArraySpec::bytes)
+      .def_readwrite("elem_size", &ArraySpec::elem_size)
+      .def_readwrite("read", &ArraySpec::read)
+      .def_readwrite("partial", &ArraySpec::partial)
+      .def_readwrite("write", &ArraySpec::write)
+      .def_readwrite("write_all", &ArraySpec::write_all)
+      .def_readwrite("ro", &ArraySpec::ro)
+      .def_readwrite("wo", &ArraySpec::wo)
+      .def_readwrite("zc", &ArraySpec::zc)
+      .def_readwrite("epw", &ArraySpec::epw);
+
+  py::class_<ComputeCall>(m, "ComputeCall")
+      .def(py::init<>())
+      .def_readwrite("kernels", &ComputeCall::kernels)
+      .def_readwrite("repeats", &ComputeCall::repeats)
+      .def_readwrite("repeat_kernel", &ComputeCall::repeat_kernel)
+      .def_readwrite("arrays", &ComputeCall::arrays)
+      .def_readwrite("global_range", &ComputeCall::global_range)
+      .def_readwrite("local_range", &ComputeCall::local_range)
+      .def_readwrite("global_offset", &ComputeCall::global_offset)
+      .def_readwrite("compute_id", &ComputeCall::compute_id)
+      .def_readwrite("pipeline", &ComputeCall::pipeline)
+      .def_readwrite("pipeline_event", &ComputeCall::pipeline_event)
+      .def_readwrite("blobs", &ComputeCall::blobs);
+
+  py::class_<CoresConfig>(m, "CoresConfig")
+      .def(py::init<>())
+      .def_readwrite("queue_concurrency", &CoresConfig::queue_concurrency)
+      .def_readwrite("no_pipelining", &CoresConfig::no_pipelining)
+      .def_readwrite("smooth", &CoresConfig::smooth)
+      .def_readwrite("options", &CoresConfig::options)
+      .def_readwrite("prebuilt", &CoresConfig::prebuilt);
+
+  py::class_<ComputeRecord>(m, "ComputeRecord")
+      .def_readonly("compute_id", &ComputeRecord::compute_id)
+      .def_readonly("wall_ms", &ComputeRecord::wall_ms)
+      .def_readonly("ranges", &ComputeRecord::ranges)
+      .def_readonly("references", &ComputeRecord::references)
+      .def_readonly("device_ms", &ComputeRecord::device_ms)
+      .def_readonly("h2d_bytes", &ComputeRecord::h2d_bytes)
+      .def_readonly("d2h_bytes", &ComputeRecord::d2h_bytes)
+      .def_readonly("pipelined", &ComputeRecord::pipelined);
+
+  py::class_<Exchanger, PyExchanger, std::shared_ptr<Exchanger>>(m, "Exchanger")
+      .def(py::init<>())
+      .def("allgather", &Exchanger::allgather)
+      .def("rank", &Exchanger::rank)
+      .def("world", &Exchanger::world);
+
+  py::class_<ShmExchanger, Exchanger, std::shared_ptr<ShmExchanger>>(m, "ShmExchanger")
+      .def(py::init<const std::string&, int, int, int, double>(), py::arg("name"), py::arg("rank"),
+           py::arg("world"), py::arg("max_values") = 64, py::arg("timeout_s") = 300.0)
+      .def("allgather", &ShmExchanger::allgather, py::call_guard<py::gil_scoped_release>())
+      .def("unlink", &ShmExchanger::unlink);
+
+  py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
+      .def_static("unique_id", []() { return py::bytes(Comm::unique_id()); })
+      .def(py::init([](py::bytes uid, int rank, int world, int device) {
+             return std::make_shared<Comm>(std::string(uid), rank, world, device);
+           }), py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("world", &Comm::world)
+      .def("broadcast", [](Comm& c, uint64_t p, uint64_t bytes, int root, uint64_t stream) {
+        c.broadcast(reinterpret_cast<void*>(p), bytes, root, reinterpret_cast<hipStream_t>(stream));
+      }, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce_sum_f32", [](Comm& c, uint64_t p, uint64_t n, uint64_t stream) {
+        c.allreduce_sum_f32(reinterpret_cast<void*>(p), n, reinterpret_cast<hipStream_t>(stream));
+      }, py::call_guard<py::gil_scoped_release>());
+
+  py::class_<Cores, std::shared_ptr<Cores>>(m, "Cores")
+      .def(py::init<const std::vector<DeviceInfo>&, const std::string&, const CoresConfig&>(),
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("error_code", &Cores::error_code)
+      .def_property_readonly("error_message", &Cores::error_message)
+      .def_property_readonly("kernels", &Cores::kernels)
+      .def_property_readonly("num_devices", &Cores::num_devices)
+      .def_property_readonly("num_global_devices", &Cores::num_global_devices)
+      .def_property_readonly("global_base", &Cores::global_base)
+      .def_property_readonly("build_ms", &Cores::build_ms)
+      .def("device", &Cores::device)
+      .def("compute", &Cores::compute, py::call_guard<py::gil_scoped_release>())
+      .def_property("enqueue_mode", &Cores::enqueue_mode,
+                    [](Cores& c, bool on) {
+                      py::gil_scoped_release r;
+                      c.set_enqueue_mode(on);
+                    })
+      .def_readwrite("async_enqueue", &Cores::async_enqueue)
+      .def_readwrite("no_compute", &Cores::no_compute)
+      .def_readwrite("fine_grained", &Cores::fine_grained)
+      .def_readwrite("smooth", &Cores::smooth)
+      .def_readwrite("dist_gather_writes", &Cores::dist_gather_writes)
+      .def_readwrite("dist_broadcast_reads", &Cores::dist_broadcast_reads)
+      .def("set_time_scale", &Cores::set_time_scale)
+      .def("set_dynamic_lds", &Cores::set_dynamic_lds)
+      .def("has_state", &Cores::has_state)
+      .def("ranges", &Cores::ranges)
+      .def("references", &Cores::references)
+      .def("benchmarks", &Cores::benchmarks)
+      .def("history", &Cores::history)
+      .def("set_state", &Cores::set_state)
+      .def("compute_ids", &Cores::compute_ids)
+      .def_property_readonly("last_compute_id", &Cores::last_compute_id)
+      .def("last_record", &Cores::last_record)
+      .def("markers_reached", &Cores::markers_reached)
+      .def("markers_issued", &Cores::markers_issued)
+      .def("finish", &Cores::finish, py::call_guard<py::gil_scoped_release>())
+      .def("release_array", &Cores::release_array)
+      .def("device_bytes", &Cores::device_bytes)
+      .def("device_pointer", &Cores::device_pointer)
+      .def("upload", &Cores::upload, py::call_guard<py::gil_scoped_release>())
+      .def("download", &Cores::download, py::call_guard<py::gil_scoped_release>())
+      .def("copy_between", &Cores::copy_between, py::call_guard<py::gil_scoped_release>())
+      .def("set_distributed", &Cores::set_distributed);
+}

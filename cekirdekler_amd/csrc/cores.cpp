@@ -1,0 +1,525 @@
+#include "cores.h"
+
+#include <algorithm>
+#include <map>
+#include <numeric>
+#include <sstream>
+
+#include "trace.h"
+
+namespace cek {
+
+Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
+             const CoresConfig& cfg)
+    : cfg_(cfg) {
+  smooth = cfg.smooth;
+  double t0 = now_ms();
+  // One code object per architecture, one module per device.
+  std::ostringstream errs;
+  for (size_t i = 0; i < devices.size(); ++i) {
+    const auto& d = devices[i];
+    std::shared_ptr<Program> prog;
+    try {
+      prog = Program::build(d, source, cfg.options, d.type == kGPU ? cfg.prebuilt : std::vector<std::string>{});
+    } catch (const std::exception& e) {
+      errs << "device " << i << " (" << d.name << "): " << e.what() << "\n";
+      error_code_ = 1;
+      continue;
+    }
+    if (!prog->ok()) {
+      errs << "device " << i << " (" << d.name << ") build failed:\n" << prog->log() << "\n";
+      error_code_ = 1;
+      continue;
+    }
+    workers_.emplace_back(new Worker(d, prog, cfg.queue_concurrency, cfg.no_pipelining));
+  }
+  error_ = errs.str();
+  if (workers_.empty() && error_code_ == 0) {
+    error_code_ = 1;
+    error_ = "no device selected";
+  }
+  global_devices_ = static_cast<int>(workers_.size());
+  time_scale_.assign(workers_.size(), 1.0);
+  build_ms_ = now_ms() - t0;
+}
+
+Cores::~Cores() {
+  try {
+    finish();
+  } catch (...) {
+  }
+  workers_.clear();
+}
+
+std::vector<KernelSig> Cores::kernels() const {
+  if (workers_.empty()) return {};
+  return workers_[0]->program().kernels();
+}
+
+void Cores::set_time_scale(int device, double scale) {
+  if (device < 0 || device >= static_cast<int>(time_scale_.size())) throw Error("bad device index");
+  time_scale_[device] = scale;
+}
+
+void Cores::set_dynamic_lds(unsigned bytes) {
+  for (auto& w : workers_) w->set_dynamic_lds(bytes);
+}
+
+void Cores::set_distributed(std::shared_ptr<Exchanger> ex, std::shared_ptr<Comm> comm,
+                            int global_devices, int global_base) {
+  ex_ = std::move(ex);
+  comm_ = std::move(comm);
+  global_devices_ = global_devices;
+  global_base_ = global_base;
+  state_.clear();
+}
+
+void Cores::set_enqueue_mode(bool on) {
+  if (on && !enqueue_mode_) {
+    enqueue_t0_ = now_ms();
+  } else if (!on && enqueue_mode_) {
+    finish();
+    double el = now_ms() - enqueue_t0_;
+    auto it = state_.find(last_id_);
+    if (it != state_.end()) {
+      for (int w = 0; w < num_devices(); ++w) {
+        size_t g = static_cast<size_t>(global_base_ + w);
+        if (g < it->second.bench.size()) it->second.bench[g] = el * time_scale_[w];
+      }
+    }
+  }
+  enqueue_mode_ = on;
+}
+
+std::vector<long long> Cores::ranges(int id) const {
+  auto it = state_.find(id);
+  return it == state_.end() ? std::vector<long long>{} : it->second.ranges;
+}
+std::vector<long long> Cores::references(int id) const {
+  auto it = state_.find(id);
+  return it == state_.end() ? std::vector<long long>{} : it->second.references;
+}
+std::vector<double> Cores::benchmarks(int id) const {
+  auto it = state_.find(id);
+  return it == state_.end() ? std::vector<double>{} : it->second.bench;
+}
+std::vector<std::vector<double>> Cores::history(int id) const {
+  auto it = state_.find(id);
+  return it == state_.end() ? std::vector<std::vector<double>>{} : it->second.history;
+}
+std::vector<int> Cores::compute_ids() const {
+  std::vector<int> out;
+  for (auto& kv : state_) out.push_back(kv.first);
+  return out;
+}
+
+void Cores::set_state(int id, const std::vector<long long>& ranges,
+                      const std::vector<std::vector<double>>& history, const std::vector<double>& bench) {
+  auto& st = state_[id];
+  st.ranges = ranges;
+  st.history = history;
+  st.bench = bench;
+  st.global_range = std::accumulate(ranges.begin(), ranges.end(), 0LL);
+  st.references.assign(ranges.size(), 0);
+  long long acc = st.global_offset;
+  for (size_t i = 0; i < ranges.size(); ++i) {
+    st.references[i] = acc;
+    acc += ranges[i];
+  }
+}
+
+long long Cores::markers_reached() {
+  long long r = 0;
+  for (auto& w : workers_) r += w->markers_reached();
+  return r;
+}
+
+long long Cores::markers_issued() {
+  long long r = 0;
+  for (auto& w : workers_) r += w->markers_issued();
+  return r;
+}
+
+void Cores::finish() {
+  for (auto& w : workers_) {
+    w->wait();
+    w->sync_all();
+  }
+}
+
+void Cores::release_array(uint64_t uid) {
+  for (auto& w : workers_) w->release(uid);
+}
+
+uint64_t Cores::device_pointer(int i, const ArraySpec& a) {
+  Worker& w = *workers_.at(i);
+  w.set_device();
+  return reinterpret_cast<uint64_t>(w.buffer(a));
+}
+
+void Cores::upload(int i, const ArraySpec& a) {
+  Worker& w = *workers_.at(i);
+  w.set_device();
+  hipStream_t s = w.main_stream();
+  w.h2d(s, a, 0, a.bytes / a.elem_size);
+  if (w.gpu()) CEK_HIP(hipStreamSynchronize(s));
+}
+
+void Cores::download(int i, const ArraySpec& a) {
+  Worker& w = *workers_.at(i);
+  w.set_device();
+  hipStream_t s = w.main_stream();
+  w.d2h(s, a, 0, a.bytes / a.elem_size);
+  if (w.gpu()) CEK_HIP(hipStreamSynchronize(s));
+}
+
+void Cores::copy_between(int src_dev, const ArraySpec& src, int dst_dev, const ArraySpec& dst,
+                         uint64_t bytes) {
+  Worker& ws = *workers_.at(src_dev);
+  Worker& wd = *workers_.at(dst_dev);
+  if (bytes > src.bytes || bytes > dst.bytes) throw Error("copy_between: size exceeds array");
+  if (!ws.gpu() && !wd.gpu()) {
+    std::memcpy(dst.host, src.host, bytes);
+    return;
+  }
+  if (ws.gpu() && wd.gpu()) {
+    ws.set_device();
+    void* sp = ws.buffer(src);
+    wd.set_device();
+    void* dp = wd.buffer(dst);
+    ws.set_device();
+    hipStream_t s = ws.main_stream();
+    if (ws.dev().ordinal == wd.dev().ordinal)
+      CEK_HIP(hipMemcpyAsync(dp, sp, bytes, hipMemcpyDeviceToDevice, s));
+    else
+      CEK_HIP(hipMemcpyPeerAsync(dp, wd.dev().ordinal, sp, ws.dev().ordinal, bytes, s));
+    CEK_HIP(hipStreamSynchronize(s));
+    return;
+  }
+  if (ws.gpu()) {  // GPU → CPU device (host memory)
+    ws.set_device();
+    hipStream_t s = ws.main_stream();
+    CEK_HIP(hipMemcpyAsync(dst.host, ws.buffer(src), bytes, hipMemcpyDeviceToHost, s));
+    CEK_HIP(hipStreamSynchronize(s));
+  } else {  // CPU → GPU
+    wd.set_device();
+    hipStream_t s = wd.main_stream();
+    CEK_HIP(hipMemcpyAsync(wd.buffer(dst), src.host, bytes, hipMemcpyHostToDevice, s));
+    CEK_HIP(hipStreamSynchronize(s));
+  }
+}
+
+// ------------------------------------------------------------- compute --
+
+void Cores::launch_kernels(Worker& wk, hipStream_t s, const ComputeCall& c, long long ref,
+                           long long range) {
+  if (no_compute) return;
+  int reps = std::max(1, c.repeats);
+  for (int r = 0; r < reps; ++r) {
+    for (auto& k : c.kernels)
+      wk.launch(s, k, c.arrays, ref, range, static_cast<int>(c.local_range), c.global_range);
+    if (!c.repeat_kernel.empty())
+      wk.launch(s, c.repeat_kernel, c.arrays, 0, c.local_range, static_cast<int>(c.local_range),
+                c.local_range);
+  }
+}
+
+void Cores::full_reads(Worker& wk, hipStream_t s, const ComputeCall& c, uint64_t* h2d) {
+  const bool dist = comm_ && dist_broadcast_reads;
+  for (auto& a : c.arrays) {
+    if (a.zc || a.partial || !a.read) continue;
+    if (dist) {
+      if (global_base_ == 0) {
+        wk.h2d(s, a, 0, a.bytes / a.elem_size);
+        *h2d += a.bytes;
+      }
+      comm_->broadcast(wk.buffer(a), a.bytes, 0, s);
+    } else {
+      wk.h2d(s, a, 0, a.bytes / a.elem_size);
+      *h2d += a.bytes;
+    }
+  }
+}
+
+void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref, long long range,
+                       uint64_t* h2d, uint64_t* d2h) {
+  hipStream_t s = nullptr;
+  if (wk.gpu())
+    s = (enqueue_mode_ && async_enqueue) ? wk.compute_stream(wk.next_compute_queue()) : wk.main_stream();
+  // phase 1: host → device (partial slice wins over full read)
+  for (auto& a : c.arrays) {
+    if (a.zc) continue;
+    if (a.partial) {
+      wk.h2d(s, a, static_cast<uint64_t>(ref) * a.epw, static_cast<uint64_t>(range) * a.epw);
+      *h2d += static_cast<uint64_t>(range) * a.epw * a.elem_size;
+    }
+  }
+  full_reads(wk, s, c, h2d);
+  // phase 2: kernels
+  launch_kernels(wk, s, c, ref, range);
+  // optional device-side all-gather of written slices (distributed keep-resident)
+  const bool gather = comm_ && dist_gather_writes;
+  if (gather) {
+    auto& st = state_[c.compute_id];
+    for (auto& a : c.arrays) {
+      if (a.zc || !(a.write || a.wo) || a.write_all) continue;
+      std::vector<uint64_t> offs(global_devices_), sizes(global_devices_);
+      for (int g = 0; g < global_devices_; ++g) {
+        offs[g] = static_cast<uint64_t>(st.references[g]) * a.epw * a.elem_size;
+        sizes[g] = static_cast<uint64_t>(st.ranges[g]) * a.epw * a.elem_size;
+        if (offs[g] + sizes[g] > a.bytes) sizes[g] = offs[g] < a.bytes ? a.bytes - offs[g] : 0;
+      }
+      comm_->allgatherv(wk.buffer(a), offs, sizes, s);
+    }
+  }
+  // phase 3: device → host
+  for (size_t i = 0; i < c.arrays.size(); ++i) {
+    const auto& a = c.arrays[i];
+    if (a.zc || !a.write) continue;
+    if (a.write_all) {
+      if (static_cast<int>(i % global_devices_) == gidx) {
+        wk.d2h(s, a, 0, a.bytes / a.elem_size);
+        *d2h += a.bytes;
+      }
+    } else if (gather) {
+      wk.d2h(s, a, 0, a.bytes / a.elem_size);
+      *d2h += a.bytes;
+    } else {
+      wk.d2h(s, a, static_cast<uint64_t>(ref) * a.epw, static_cast<uint64_t>(range) * a.epw);
+      *d2h += static_cast<uint64_t>(range) * a.epw * a.elem_size;
+    }
+  }
+  if (fine_grained) wk.add_marker(s);
+  if (!enqueue_mode_ && wk.gpu()) CEK_HIP(hipStreamSynchronize(s));
+}
+
+void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long long ref,
+                               long long range, uint64_t* h2d, uint64_t* d2h) {
+  const long long B = std::max(1, c.blobs);
+  const long long chunk = range / B;
+  const int halves = (B % 2 == 0) ? 2 : 1;
+  const long long per_half = B / halves;
+  hipStream_t m = wk.main_stream();
+  full_reads(wk, m, c, h2d);
+  int slot = 0;
+  hipEvent_t ev_full = nullptr;
+  if (wk.gpu()) {
+    ev_full = wk.event(slot++);
+    CEK_HIP(hipEventRecord(ev_full, m));
+    for (int h = 0; h < halves; ++h) CEK_HIP(hipStreamWaitEvent(wk.pipe_stream(h, 1), ev_full, 0));
+  }
+  // Interleave the two half-pipelines' chunks so both read streams start early.
+  for (long long k = 0; k < per_half; ++k) {
+    for (int h = 0; h < halves; ++h) {
+      hipStream_t rs = wk.pipe_stream(h, 0), ks = wk.pipe_stream(h, 1), ws = wk.pipe_stream(h, 2);
+      long long off = ref + h * (range / halves) + k * chunk;
+      for (auto& a : c.arrays) {
+        if (a.zc || !a.partial) continue;
+        wk.h2d(rs, a, static_cast<uint64_t>(off) * a.epw, static_cast<uint64_t>(chunk) * a.epw);
+        *h2d += static_cast<uint64_t>(chunk) * a.epw * a.elem_size;
+      }
+      if (wk.gpu()) {
+        hipEvent_t er = wk.event(slot++);
+        CEK_HIP(hipEventRecord(er, rs));
+        CEK_HIP(hipStreamWaitEvent(ks, er, 0));
+      }
+      launch_kernels(wk, ks, c, off, chunk);
+      if (wk.gpu()) {
+        hipEvent_t ek = wk.event(slot++);
+        CEK_HIP(hipEventRecord(ek, ks));
+        CEK_HIP(hipStreamWaitEvent(ws, ek, 0));
+      }
+      for (auto& a : c.arrays) {
+        if (a.zc || !a.write || a.write_all) continue;
+        wk.d2h(ws, a, static_cast<uint64_t>(off) * a.epw, static_cast<uint64_t>(chunk) * a.epw);
+        *d2h += static_cast<uint64_t>(chunk) * a.epw * a.elem_size;
+      }
+    }
+  }
+  // write-all owners download after every chunk's kernels
+  bool any_all = false;
+  for (auto& a : c.arrays) any_all |= (a.write && a.write_all && !a.zc);
+  if (wk.gpu()) {
+    for (int h = 0; h < halves; ++h) {
+      hipEvent_t e = wk.event(slot++);
+      CEK_HIP(hipEventRecord(e, wk.pipe_stream(h, 1)));
+      CEK_HIP(hipStreamWaitEvent(m, e, 0));
+      hipEvent_t e2 = wk.event(slot++);
+      CEK_HIP(hipEventRecord(e2, wk.pipe_stream(h, 2)));
+      CEK_HIP(hipStreamWaitEvent(m, e2, 0));
+    }
+  }
+  if (any_all) {
+    for (size_t i = 0; i < c.arrays.size(); ++i) {
+      const auto& a = c.arrays[i];
+      if (a.write && a.write_all && !a.zc && static_cast<int>(i % global_devices_) == gidx) {
+        wk.d2h(m, a, 0, a.bytes / a.elem_size);
+        *d2h += a.bytes;
+      }
+    }
+  }
+  if (fine_grained) wk.add_marker(m);
+  if (wk.gpu()) CEK_HIP(hipStreamSynchronize(m));
+}
+
+void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long long ref,
+                                long long range, uint64_t* h2d, uint64_t* d2h) {
+  const long long B = std::max(1, c.blobs);
+  const long long chunk = range / B;
+  hipStream_t m = wk.main_stream();
+  full_reads(wk, m, c, h2d);
+  int slot = 0;
+  hipEvent_t ev_full = nullptr;
+  if (wk.gpu()) {
+    ev_full = wk.event(slot++);
+    CEK_HIP(hipEventRecord(ev_full, m));
+  }
+  const int nq = wk.queue_concurrency();
+  std::vector<char> used(16, 0);
+  for (long long k = 0; k < B; ++k) {
+    int qi = static_cast<int>(k % nq);
+    hipStream_t s = wk.compute_stream(qi);
+    if (wk.gpu() && !used[qi]) CEK_HIP(hipStreamWaitEvent(s, ev_full, 0));
+    used[qi] = 1;
+    long long off = ref + k * chunk;
+    for (auto& a : c.arrays) {
+      if (a.zc || !a.partial) continue;
+      wk.h2d(s, a, static_cast<uint64_t>(off) * a.epw, static_cast<uint64_t>(chunk) * a.epw);
+      *h2d += static_cast<uint64_t>(chunk) * a.epw * a.elem_size;
+    }
+    launch_kernels(wk, s, c, off, chunk);
+    for (auto& a : c.arrays) {
+      if (a.zc || !a.write || a.write_all) continue;
+      wk.d2h(s, a, static_cast<uint64_t>(off) * a.epw, static_cast<uint64_t>(chunk) * a.epw);
+      *d2h += static_cast<uint64_t>(chunk) * a.epw * a.elem_size;
+    }
+  }
+  if (wk.gpu()) {
+    for (int q = 0; q < 16; ++q) {
+      if (!used[q]) continue;
+      hipEvent_t e = wk.event(slot++);
+      CEK_HIP(hipEventRecord(e, wk.compute_stream(q)));
+      CEK_HIP(hipStreamWaitEvent(m, e, 0));
+    }
+  }
+  for (size_t i = 0; i < c.arrays.size(); ++i) {
+    const auto& a = c.arrays[i];
+    if (a.write && a.write_all && !a.zc && static_cast<int>(i % global_devices_) == gidx) {
+      wk.d2h(m, a, 0, a.bytes / a.elem_size);
+      *d2h += a.bytes;
+    }
+  }
+  if (fine_grained) wk.add_marker(m);
+  if (wk.gpu()) CEK_HIP(hipStreamSynchronize(m));
+}
+
+void Cores::run_device(int w, const ComputeCall& c, long long ref, long long range, bool pipelined,
+                       double* out_ms, uint64_t* h2d, uint64_t* d2h) {
+  Worker& wk = *workers_[w];
+  const int gidx = global_base_ + w;
+  TraceRange tr("cek.device" + std::to_string(gidx) + ".id" + std::to_string(c.compute_id));
+  double t0 = now_ms();
+  if (range > 0) {
+    wk.set_device();
+    if (!pipelined)
+      run_3phase(wk, gidx, c, ref, range, h2d, d2h);
+    else if (c.pipeline_event)
+      run_event_pipeline(wk, gidx, c, ref, range, h2d, d2h);
+    else
+      run_driver_pipeline(wk, gidx, c, ref, range, h2d, d2h);
+  } else if (comm_ && (dist_gather_writes || dist_broadcast_reads)) {
+    // still take part in the collectives
+    run_3phase(wk, gidx, c, ref, 0, h2d, d2h);
+  }
+  *out_ms = (now_ms() - t0) * time_scale_[w];
+}
+
+void Cores::compute(const ComputeCall& c) {
+  if (error_code_ != 0) throw Error("cannot compute, initialisation failed: " + error_);
+  const long long G = c.global_range, L = c.local_range;
+  if (G <= 0) throw Error("global range must be positive");
+  if (L <= 0 || L > 1024) throw Error("local range must be in [1, 1024]");
+  if (G % L != 0) throw Error("global range must be a multiple of local range");
+  for (auto& k : c.kernels)
+    if (!workers_[0]->program().has(k)) throw Error("unknown kernel: " + k);
+  if (!c.repeat_kernel.empty() && !workers_[0]->program().has(c.repeat_kernel))
+    throw Error("unknown repeat kernel: " + c.repeat_kernel);
+  const int D = global_devices_;
+  const int nloc = num_devices();
+  const long long B = std::max(1, c.blobs);
+  const bool pipe_req = c.pipeline && !cfg_.no_pipelining;
+  TraceRange tr("cek.compute.id" + std::to_string(c.compute_id));
+  double wall0 = now_ms();
+
+  auto it = state_.find(c.compute_id);
+  bool fresh = it == state_.end() || it->second.global_range != G ||
+               it->second.local_range != L ||
+               static_cast<int>(it->second.ranges.size()) != D;
+  BalancerState& st = state_[c.compute_id];
+  if (fresh) {
+    st = BalancerState();
+    st.history.assign(kHistoryDepth, std::vector<double>(D, 0.0));
+    st.bench.assign(D, 0.0);
+    st.global_range = G;
+    st.local_range = L;
+  }
+  st.global_offset = c.global_offset;
+  const bool first = fresh || std::all_of(st.ranges.begin(), st.ranges.end(), [](long long r) { return r == 0; });
+  if (!(enqueue_mode_ && !first)) {
+    if (first) {
+      // Cores.cs:569-596
+      std::vector<long long> eq(D, G / D);
+      eq[0] += G - (G / D) * D;
+      bool b1 = std::all_of(eq.begin(), eq.end(), [&](long long r) { return r >= B * L; });
+      long long step = (b1 && pipe_req && G >= B * L) ? B * L : L;
+      initial_split(D, smooth, st.history, G, st.ranges, step);
+    } else {
+      bool b1 = std::all_of(st.ranges.begin(), st.ranges.end(), [&](long long r) { return r >= B * L; });
+      long long step = (b1 && pipe_req && G >= B * L) ? B * L : L;
+      load_balance(st.bench, smooth, st.history, G, st.ranges, step);
+    }
+  }
+  st.references.assign(D, 0);
+  long long acc = c.global_offset;
+  for (int i = 0; i < D; ++i) {
+    st.references[i] = acc;
+    acc += st.ranges[i];
+  }
+  // Pipelining eligibility (Cores.cs:624-652), decided per call for all devices.
+  bool pipelined = pipe_req && c.repeats <= 1 && !enqueue_mode_;
+  for (int i = 0; i < D && pipelined; ++i)
+    if (st.ranges[i] % (B * L) != 0 || st.ranges[i] < B * L) pipelined = false;
+  if (comm_ && (dist_gather_writes || dist_broadcast_reads)) pipelined = false;
+
+  std::vector<double> ms(nloc, 0.0);
+  std::vector<uint64_t> h2d(nloc, 0), d2h(nloc, 0);
+  if (nloc == 1) {
+    run_device(0, c, st.references[global_base_], st.ranges[global_base_], pipelined, &ms[0], &h2d[0], &d2h[0]);
+  } else {
+    for (int w = 0; w < nloc; ++w) {
+      int g = global_base_ + w;
+      long long ref = st.references[g], rng = st.ranges[g];
+      workers_[w]->post([=, &c, &ms, &h2d, &d2h] {
+        run_device(w, c, ref, rng, pipelined, &ms[w], &h2d[w], &d2h[w]);
+      });
+    }
+    for (auto& w : workers_) w->wait();
+  }
+  last_id_ = c.compute_id;
+  if (!enqueue_mode_) {
+    std::vector<double> all = ms;
+    if (ex_) all = ex_->allgather(ms);
+    if (static_cast<int>(all.size()) == D) st.bench = all;
+  }
+  ++st.calls;
+  last_record_.compute_id = c.compute_id;
+  last_record_.wall_ms = now_ms() - wall0;
+  last_record_.ranges = st.ranges;
+  last_record_.references = st.references;
+  last_record_.device_ms = st.bench;
+  last_record_.h2d_bytes = std::accumulate(h2d.begin(), h2d.end(), 0ull);
+  last_record_.d2h_bytes = std::accumulate(d2h.begin(), d2h.end(), 0ull);
+  last_record_.pipelined = pipelined;
+}
+
+}  // namespace cek

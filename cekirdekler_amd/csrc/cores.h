@@ -1,0 +1,149 @@
+// Multi-device scheduler — the MI355X-native counterpart of the reference's
+// `Cores` (Cores.cs:37-1982): one worker per device, per-compute-id range
+// tables driven by the iterative load balancer, and three execution shapes
+// per device:
+//   * 3-phase (H2D → kernels → D2H) on one in-order stream
+//     (Cores.cs:745-835, Worker.cs:821-840/:1033-1114/:1343-1361),
+//   * event-driven pipeline: the device's range cut into `blobs` chunks that
+//     stream through two half-pipelines, each {read, compute, write} HIP
+//     streams joined by hipEvents (Cores.cs:1197-1367, Worker.cs:1411-1567),
+//   * driver pipeline: chunk k on round-robin stream k mod 16
+//     (Cores.cs:1368-1958).
+// plus enqueue mode / async enqueue / no-compute / fine-grained markers /
+// repeat + sync kernel (ClNumberCruncher.cs:66-187, Cores.cs:72-126,
+// :449, :796-809).  Fan-out runs on persistent worker threads with the GIL
+// released, one Python→C++ crossing per compute().
+//
+// Distributed mode (one process per GPU): the balancer runs on the global
+// device list; each rank executes its own device's range and the per-device
+// times are exchanged through an Exchanger, so every rank derives the
+// identical next split.  Optional RCCL data plane: broadcast `read` arrays
+// from rank 0 and all-gather written slices into every replica.
+#pragma once
+#include <map>
+
+#include "balancer.h"
+#include "dist.h"
+#include "worker.h"
+
+namespace cek {
+
+struct ComputeCall {
+  std::vector<std::string> kernels;
+  int repeats = 1;
+  std::string repeat_kernel;
+  std::vector<ArraySpec> arrays;
+  long long global_range = 0;
+  long long local_range = 256;
+  long long global_offset = 0;
+  int compute_id = 1;
+  bool pipeline = false;
+  bool pipeline_event = true;  // PIPELINE_EVENT=true, PIPELINE_DRIVER=false
+  int blobs = 4;
+};
+
+struct CoresConfig {
+  int queue_concurrency = 16;
+  bool no_pipelining = false;
+  bool smooth = true;
+  std::vector<std::string> options;
+  std::vector<std::string> prebuilt;  // "path|name1,name2"
+};
+
+struct ComputeRecord {  // structured per-call record (observability)
+  int compute_id = 0;
+  double wall_ms = 0;
+  std::vector<long long> ranges, references;
+  std::vector<double> device_ms;
+  uint64_t h2d_bytes = 0, d2h_bytes = 0;
+  bool pipelined = false;
+};
+
+class Cores {
+ public:
+  Cores(const std::vector<DeviceInfo>& devices, const std::string& source, const CoresConfig& cfg);
+  ~Cores();
+
+  int error_code() const { return error_code_; }
+  const std::string& error_message() const { return error_; }
+  std::vector<KernelSig> kernels() const;
+  int num_devices() const { return static_cast<int>(workers_.size()); }
+  int num_global_devices() const { return global_devices_; }
+  const DeviceInfo& device(int i) const { return workers_.at(i)->dev(); }
+  double build_ms() const { return build_ms_; }
+
+  void compute(const ComputeCall& call);
+
+  // ---- modes ----
+  bool enqueue_mode() const { return enqueue_mode_; }
+  void set_enqueue_mode(bool on);
+  bool async_enqueue = false;
+  bool no_compute = false;
+  bool fine_grained = false;
+  bool smooth = true;
+  void set_time_scale(int device, double scale);  // injected heterogeneity (tests/bench)
+  void set_dynamic_lds(unsigned bytes);
+
+  // ---- state ----
+  bool has_state(int id) const { return state_.count(id) > 0; }
+  std::vector<long long> ranges(int id) const;
+  std::vector<long long> references(int id) const;
+  std::vector<double> benchmarks(int id) const;
+  std::vector<std::vector<double>> history(int id) const;
+  void set_state(int id, const std::vector<long long>& ranges,
+                 const std::vector<std::vector<double>>& history, const std::vector<double>& bench);
+  std::vector<int> compute_ids() const;
+  int last_compute_id() const { return last_id_; }
+  ComputeRecord last_record() const { return last_record_; }
+
+  long long markers_reached();
+  long long markers_issued();
+  void finish();  // synchronise every stream of every device
+  void release_array(uint64_t uid);
+  uint64_t device_bytes(int i) const { return workers_.at(i)->bytes_allocated(); }
+  // Raw device pointer of a cached replica (allocates if needed).
+  uint64_t device_pointer(int i, const ArraySpec& a);
+  void upload(int i, const ArraySpec& a);    // whole array H2D (sync)
+  void download(int i, const ArraySpec& a);  // whole array D2H (sync)
+  void copy_between(int src_dev, const ArraySpec& src, int dst_dev, const ArraySpec& dst,
+                    uint64_t bytes);  // device→device (peer/xGMI) copy, sync
+
+  // ---- distributed ----
+  void set_distributed(std::shared_ptr<Exchanger> ex, std::shared_ptr<Comm> comm,
+                       int global_devices, int global_base);
+  bool dist_gather_writes = false;
+  bool dist_broadcast_reads = false;
+  int global_base() const { return global_base_; }
+
+ private:
+  void run_device(int w, const ComputeCall& c, long long ref, long long range, bool pipelined,
+                  double* out_ms, uint64_t* h2d, uint64_t* d2h);
+  void run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref, long long range,
+                  uint64_t* h2d, uint64_t* d2h);
+  void run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long long ref,
+                          long long range, uint64_t* h2d, uint64_t* d2h);
+  void run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long long ref,
+                           long long range, uint64_t* h2d, uint64_t* d2h);
+  void launch_kernels(Worker& wk, hipStream_t s, const ComputeCall& c, long long ref,
+                      long long range);
+  void full_reads(Worker& wk, hipStream_t s, const ComputeCall& c, uint64_t* h2d);
+
+  std::vector<std::unique_ptr<Worker>> workers_;
+  std::map<int, BalancerState> state_;
+  std::vector<double> time_scale_;
+  std::string error_;
+  int error_code_ = 0;
+  double build_ms_ = 0;
+  bool enqueue_mode_ = false;
+  double enqueue_t0_ = 0;
+  int last_id_ = 0;
+  ComputeRecord last_record_;
+  CoresConfig cfg_;
+
+  std::shared_ptr<Exchanger> ex_;
+  std::shared_ptr<Comm> comm_;
+  int global_devices_ = 0;
+  int global_base_ = 0;
+};
+
+}  // namespace cek

@@ -1,0 +1,44 @@
+// Device discovery: the MI355X-native replacement for the reference's
+// platform/device wrappers (ClPlatform.cs:28-116, ClDevice.cs:26-161) and
+// their native calls (platformList, createDevice, createDeviceAsPartition,
+// deviceGDDR, deviceComputeUnits, deviceMemSize).
+//
+// There is one "ROCm HIP" platform (every visible GPU) and one "Host CPU"
+// platform (a single CPU device driven by a native thread pool; the
+// reference's CPU fission to N-1 cores, ClDevice.cs:85-95, becomes the pool
+// size).
+#pragma once
+#include "common.h"
+
+namespace cek {
+
+struct DeviceInfo {
+  int type = kCPU;        // DevType
+  int ordinal = -1;       // HIP ordinal, -1 for the CPU device
+  std::string name;
+  std::string arch;       // gcnArchName (gfx950...)
+  std::string vendor;
+  std::string platform;
+  int compute_units = 0;
+  uint64_t mem_bytes = 0;
+  bool dedicated_memory = false;  // reference "GDDR" flag (!HOST_UNIFIED_MEMORY)
+  bool streaming = false;         // prefer zero-copy (reference "stream" flag)
+  int cpu_threads = 0;            // CPU device pool size
+  int pci_bus = -1;
+  int pci_device = -1;
+  int clock_khz = 0;
+  uint64_t lds_per_block = 0;
+  std::string describe() const;
+};
+
+// Number of HIP GPUs (0 when no runtime / no device; never throws).
+int gpu_count();
+// All devices: GPUs first (HIP ordinal order) then the CPU device.
+std::vector<DeviceInfo> enumerate_devices();
+DeviceInfo gpu_info(int ordinal);
+DeviceInfo cpu_info(int threads = -1);
+
+// Peer access matrix between GPUs (xGMI); enables access where possible.
+std::vector<std::vector<int>> enable_peer_access();
+
+}  // namespace cek

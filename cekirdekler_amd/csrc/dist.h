@@ -1,0 +1,68 @@
+// Multi-process (one process per MI355X) support.
+//
+// The reference drives every device from one process (Cores.cs:156-344) and
+// balances them with per-device timings it holds in memory.  On MI355X the
+// idiomatic layout is one process per GPU, so the balancer's input — every
+// device's time for the previous call of a compute id — is exchanged across
+// ranks:
+//   * ShmExchanger: node-local control plane in POSIX shared memory
+//     (double-buffered slots + per-rank epoch words; ~µs per exchange),
+//   * Comm: RCCL communicator (xGMI) used for the data plane — broadcast of
+//     `read` arrays and all-gather(v) of written slices so device replicas
+//     stay coherent without a host bounce.
+#pragma once
+#include "common.h"
+
+namespace cek {
+
+class Exchanger {
+ public:
+  virtual ~Exchanger() = default;
+  // Gather `n` doubles from every rank; returns world*n values, rank-major.
+  virtual std::vector<double> allgather(const std::vector<double>& local) = 0;
+  virtual void barrier() { allgather(std::vector<double>(1, 0.0)); }
+  virtual int rank() const = 0;
+  virtual int world() const = 0;
+};
+
+class ShmExchanger : public Exchanger {
+ public:
+  // Rank 0 creates the segment, the others attach (retrying up to timeout).
+  ShmExchanger(const std::string& name, int rank, int world, int max_values = 64,
+               double timeout_s = 300.0);
+  ~ShmExchanger() override;
+  std::vector<double> allgather(const std::vector<double>& local) override;
+  void unlink();  // remove the name (segment lives until every rank unmaps)
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+
+ private:
+  std::string name_;
+  int rank_, world_, maxv_;
+  double timeout_s_;
+  void* base_ = nullptr;
+  size_t size_ = 0;
+  uint64_t epoch_ = 0;
+};
+
+class Comm {
+ public:
+  static std::string unique_id();  // bytes of an ncclUniqueId
+  Comm(const std::string& uid, int rank, int world, int device);
+  ~Comm();
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  // In-place broadcast of `bytes` at dptr from root.
+  void broadcast(void* dptr, uint64_t bytes, int root, hipStream_t s);
+  // In-place all-gather-v: rank r owns [offsets[r], offsets[r]+sizes[r]) bytes.
+  void allgatherv(void* dptr, const std::vector<uint64_t>& offsets,
+                  const std::vector<uint64_t>& sizes, hipStream_t s);
+  void allreduce_sum_f32(void* dptr, uint64_t count, hipStream_t s);
+  void allreduce_sum_f64(void* dptr, uint64_t count, hipStream_t s);
+
+ private:
+  void* comm_ = nullptr;  // ncclComm_t
+  int rank_, world_, device_;
+};
+
+}  // namespace cek

@@ -1,0 +1,579 @@
+#include "jit.h"
+
+#include <dlfcn.h>
+#include <hip/hiprtc.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <regex>
+#include <set>
+#include <sstream>
+
+namespace cek {
+
+// ---------------------------------------------------------------- helpers --
+
+std::string hash_hex(const std::string& s) {
+  uint64_t h1 = 1469598103934665603ull, h2 = 0x9e3779b97f4a7c15ull;
+  for (unsigned char c : s) {
+    h1 = (h1 ^ c) * 1099511628211ull;
+    h2 = (h2 ^ c) * 0x100000001b3ull + 0x632be59bd9b4e019ull;
+  }
+  char buf[40];
+  snprintf(buf, sizeof(buf), "%016llx%016llx", (unsigned long long)h1, (unsigned long long)h2);
+  return buf;
+}
+
+static void mkdirs(const std::string& path) {
+  std::string cur;
+  std::stringstream ss(path);
+  std::string part;
+  if (!path.empty() && path[0] == '/') cur = "/";
+  while (std::getline(ss, part, '/')) {
+    if (part.empty()) continue;
+    cur += part + "/";
+    mkdir(cur.c_str(), 0755);
+  }
+}
+
+std::string cache_dir() {
+  const char* e = getenv("CEK_CACHE_DIR");
+  std::string d;
+  if (e && *e) {
+    d = e;
+  } else {
+    const char* home = getenv("HOME");
+    d = std::string(home && *home ? home : "/tmp") + "/.cache/cekirdekler_amd";
+  }
+  mkdirs(d);
+  return d;
+}
+
+static bool read_file(const std::string& p, std::string& out) {
+  std::ifstream f(p, std::ios::binary);
+  if (!f) return false;
+  std::ostringstream os;
+  os << f.rdbuf();
+  out = os.str();
+  return true;
+}
+
+static void write_file_atomic(const std::string& p, const std::string& data) {
+  std::string tmp = p + ".tmp." + std::to_string(getpid());
+  {
+    std::ofstream f(tmp, std::ios::binary);
+    f.write(data.data(), static_cast<std::streamsize>(data.size()));
+  }
+  rename(tmp.c_str(), p.c_str());
+}
+
+// Replace comments with spaces (keeps offsets stable); string literals kept.
+static std::string strip_comments(const std::string& s) {
+  std::string o = s;
+  size_t i = 0, n = s.size();
+  while (i < n) {
+    if (s[i] == '"' || s[i] == '\'') {
+      char q = s[i++];
+      while (i < n && s[i] != q) {
+        if (s[i] == '\\') ++i;
+        ++i;
+      }
+      ++i;
+    } else if (i + 1 < n && s[i] == '/' && s[i + 1] == '/') {
+      while (i < n && s[i] != '\n') o[i++] = ' ';
+    } else if (i + 1 < n && s[i] == '/' && s[i + 1] == '*') {
+      o[i] = o[i + 1] = ' ';
+      i += 2;
+      while (i + 1 < n && !(s[i] == '*' && s[i + 1] == '/')) {
+        if (s[i] != '\n') o[i] = ' ';
+        ++i;
+      }
+      if (i + 1 < n) o[i] = o[i + 1] = ' ';
+      i += 2;
+    } else {
+      ++i;
+    }
+  }
+  return o;
+}
+
+bool is_opencl_dialect(const std::string& src) {
+  static const std::regex re(R"((^|[^\w])(__kernel|kernel)\s+void\s)");
+  return std::regex_search(strip_comments(src), re);
+}
+
+static std::string regex_replace_all(const std::string& s, const std::string& pat,
+                                     const std::string& rep) {
+  return std::regex_replace(s, std::regex(pat), rep);
+}
+
+// OpenCL-C → HIP C++ (best effort; the reference's kernels are OpenCL C).
+static std::string translate_opencl(const std::string& src) {
+  std::string s = strip_comments(src);
+  s = regex_replace_all(s, R"((^|[^\w])(__kernel|kernel)(\s+void\s))", "$1__global__$3");
+  s = regex_replace_all(s, R"((^|[^\w])__global(?![\w]))", "$1");
+  s = regex_replace_all(s, R"((^|[^\w])global(\s+[\w]))", "$1$2");
+  s = regex_replace_all(s, R"((^|[^\w])(__local|local)(\s+))", "$1__shared__$3");
+  s = regex_replace_all(s, R"((^|[^\w])(__constant|constant)(\s+))", "$1const$3");
+  s = regex_replace_all(s, R"((^|[^\w])(__private|private)(\s+))", "$1$3");
+  s = regex_replace_all(s, R"(barrier\s*\([^)]*\))", "__syncthreads()");
+  s = regex_replace_all(s, R"(mem_fence\s*\([^)]*\))", "__threadfence()");
+  return "#define CEK_OPENCL_DIALECT 1\n" + s;
+}
+
+static size_t match_paren(const std::string& s, size_t open) {
+  int depth = 0;
+  for (size_t i = open; i < s.size(); ++i) {
+    if (s[i] == '(') ++depth;
+    else if (s[i] == ')') {
+      if (--depth == 0) return i;
+    }
+  }
+  return std::string::npos;
+}
+
+static int count_params(const std::string& inside) {
+  std::string t;
+  for (char c : inside)
+    if (!isspace(static_cast<unsigned char>(c))) t += c;
+  if (t.empty() || t == "void") return 0;
+  int depth = 0, n = 1;
+  for (char c : inside) {
+    if (c == '(' || c == '<' || c == '[') ++depth;
+    else if (c == ')' || c == '>' || c == ']') --depth;
+    else if (c == ',' && depth == 0) ++n;
+  }
+  return n;
+}
+
+struct KernelSite {
+  size_t global_pos;   // position of "__global__"
+  bool has_extern_c;
+  size_t open, close;  // parameter parens
+  KernelSig sig;
+};
+
+static std::vector<KernelSite> find_sites(const std::string& s) {
+  static const std::regex re(
+      R"((extern\s+"C"\s+)?__global__\s+(__launch_bounds__\s*\([^)]*\)\s*)?void\s+(__launch_bounds__\s*\([^)]*\)\s*)?([A-Za-z_]\w*)\s*\()");
+  std::vector<KernelSite> out;
+  for (auto it = std::sregex_iterator(s.begin(), s.end(), re); it != std::sregex_iterator(); ++it) {
+    const auto& m = *it;
+    // Skip template kernels (cannot be extern "C").
+    size_t start = static_cast<size_t>(m.position(0));
+    size_t back = start;
+    while (back > 0 && isspace(static_cast<unsigned char>(s[back - 1]))) --back;
+    if (back > 0 && s[back - 1] == '>') continue;
+    KernelSite k;
+    k.has_extern_c = m[1].matched;
+    k.global_pos = k.has_extern_c ? static_cast<size_t>(m.position(1)) : start;
+    k.open = start + static_cast<size_t>(m.length(0)) - 1;
+    k.close = match_paren(s, k.open);
+    if (k.close == std::string::npos) continue;
+    k.sig.name = m[4].str();
+    k.sig.arity = count_params(s.substr(k.open + 1, k.close - k.open - 1));
+    out.push_back(k);
+  }
+  return out;
+}
+
+std::vector<KernelSig> parse_kernels(const std::string& src) {
+  std::string s = is_opencl_dialect(src) ? translate_opencl(src) : strip_comments(src);
+  std::vector<KernelSig> out;
+  std::set<std::string> seen;
+  for (auto& k : find_sites(s)) {
+    if (seen.insert(k.sig.name).second) out.push_back(k.sig);
+  }
+  return out;
+}
+
+// ------------------------------------------------------------- preludes --
+
+static const char* kGpuPrelude = R"CEK(
+// ---- cekirdekler_amd GPU prelude (gfx950) ----
+#define CEK_GPU 1
+#define get_global_id(d) ((d) == 0 ? ((long long)blockIdx.x * (long long)blockDim.x + (long long)threadIdx.x + __cek_off) : (d) == 1 ? (long long)(blockIdx.y * blockDim.y + threadIdx.y) : (long long)(blockIdx.z * blockDim.z + threadIdx.z))
+#define get_local_id(d) ((long long)((d) == 0 ? threadIdx.x : (d) == 1 ? threadIdx.y : threadIdx.z))
+#define get_group_id(d) ((long long)((d) == 0 ? blockIdx.x : (d) == 1 ? blockIdx.y : blockIdx.z))
+#define get_local_size(d) ((long long)((d) == 0 ? blockDim.x : (d) == 1 ? blockDim.y : blockDim.z))
+#define get_global_size(d) ((d) == 0 ? __cek_gsize : (long long)((d) == 1 ? gridDim.y * blockDim.y : gridDim.z * blockDim.z))
+#define get_num_groups(d) ((d) == 0 ? __cek_gsize / (long long)blockDim.x : (long long)((d) == 1 ? gridDim.y : gridDim.z))
+#define get_global_offset(d) ((d) == 0 ? __cek_off : 0ll)
+#define cek_global_group_id() ((long long)blockIdx.x + __cek_off / (long long)blockDim.x)
+#define cek_local_group_id() ((long long)blockIdx.x)
+#define cek_local_num_groups() ((long long)gridDim.x)
+#ifdef CEK_OPENCL_DIALECT
+typedef unsigned int uint; typedef unsigned char uchar; typedef unsigned short ushort; typedef unsigned long ulong;
+__device__ inline float native_sqrt(float x) { return __fsqrt_rn(x); }
+__device__ inline float native_rsqrt(float x) { return rsqrtf(x); }
+__device__ inline float native_exp(float x) { return __expf(x); }
+__device__ inline float native_sin(float x) { return __sinf(x); }
+__device__ inline float native_cos(float x) { return __cosf(x); }
+__device__ inline float native_divide(float a, float b) { return __fdividef(a, b); }
+__device__ inline float mad(float a, float b, float c) { return fmaf(a, b, c); }
+__device__ inline float clamp(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+__device__ inline int atomic_add(int* p, int v) { return atomicAdd(p, v); }
+__device__ inline int atomic_inc(int* p) { return atomicAdd(p, 1); }
+#endif
+// ---- end prelude ----
+)CEK";
+
+static const char* kCpuPrelude = R"CEK(
+// ---- cekirdekler_amd CPU prelude (host device) ----
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <ucontext.h>
+#define CEK_CPU 1
+struct dim3 { unsigned x = 1, y = 1, z = 1; };
+static thread_local dim3 threadIdx, blockIdx, blockDim, gridDim;
+static thread_local long long __cek_off = 0, __cek_gsize = 0;
+#define __global__
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#define __noinline__
+#define __restrict__ __restrict
+#define __launch_bounds__(...)
+#define __shared__ static thread_local
+struct float2 { float x, y; }; struct float3 { float x, y, z; }; struct float4 { float x, y, z, w; };
+struct int2 { int x, y; }; struct int4 { int x, y, z, w; }; struct uint2 { unsigned x, y; }; struct uint4 { unsigned x, y, z, w; };
+struct double2 { double x, y; };
+static inline float2 make_float2(float a, float b) { return {a, b}; }
+static inline float3 make_float3(float a, float b, float c) { return {a, b, c}; }
+static inline float4 make_float4(float a, float b, float c, float d) { return {a, b, c, d}; }
+static inline int2 make_int2(int a, int b) { return {a, b}; }
+static inline int4 make_int4(int a, int b, int c, int d) { return {a, b, c, d}; }
+static inline float rsqrtf(float x) { return 1.0f / std::sqrt(x); }
+static inline double rsqrt(double x) { return 1.0 / std::sqrt(x); }
+static inline float __fdividef(float a, float b) { return a / b; }
+static inline float __fsqrt_rn(float x) { return std::sqrt(x); }
+using std::min; using std::max;
+template <class T> static inline T atomicAdd(T* p, T v) {
+  T old, nv; __atomic_load(p, &old, __ATOMIC_RELAXED);
+  do { nv = old + v; } while (!__atomic_compare_exchange(p, &old, &nv, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST));
+  return old;
+}
+static inline int atomicAdd(int* p, int v) { return __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST); }
+static inline unsigned atomicAdd(unsigned* p, unsigned v) { return __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST); }
+static inline long long atomicAdd(long long* p, long long v) { return __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST); }
+template <class T> static inline T atomicMax(T* p, T v) { T o = *p; while (o < v && !__atomic_compare_exchange_n(p, &o, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {} return o; }
+template <class T> static inline T atomicMin(T* p, T v) { T o = *p; while (o > v && !__atomic_compare_exchange_n(p, &o, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {} return o; }
+template <class T> static inline T atomicExch(T* p, T v) { return __atomic_exchange_n(p, v, __ATOMIC_SEQ_CST); }
+static inline void __threadfence() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
+// Work-group barrier on the CPU device: every work-item of a group is a
+// fiber (ucontext) on one host thread; __syncthreads() yields to the group
+// scheduler, which resumes the items round-robin.
+struct __CekFibers { ucontext_t sched; ucontext_t* items; int cur; };
+static thread_local __CekFibers* __cek_fib = nullptr;
+static inline void __syncthreads() { if (__cek_fib) swapcontext(&__cek_fib->items[__cek_fib->cur], &__cek_fib->sched); }
+#define get_global_id(d) ((d) == 0 ? ((long long)blockIdx.x * (long long)blockDim.x + (long long)threadIdx.x + __cek_off) : 0ll)
+#define get_local_id(d) ((long long)((d) == 0 ? threadIdx.x : 0))
+#define get_group_id(d) ((long long)((d) == 0 ? blockIdx.x : 0))
+#define get_local_size(d) ((long long)((d) == 0 ? blockDim.x : 1))
+#define get_global_size(d) ((d) == 0 ? __cek_gsize : 1ll)
+#define get_num_groups(d) ((d) == 0 ? __cek_gsize / (long long)blockDim.x : 1ll)
+#define get_global_offset(d) ((d) == 0 ? __cek_off : 0ll)
+#define cek_global_group_id() ((long long)blockIdx.x + __cek_off / (long long)blockDim.x)
+#define cek_local_group_id() ((long long)blockIdx.x)
+#define cek_local_num_groups() ((long long)gridDim.x)
+#ifdef CEK_OPENCL_DIALECT
+typedef unsigned int uint; typedef unsigned char uchar; typedef unsigned short ushort; typedef unsigned long ulong;
+static inline float native_sqrt(float x) { return std::sqrt(x); }
+static inline float native_rsqrt(float x) { return 1.0f / std::sqrt(x); }
+static inline float native_exp(float x) { return std::exp(x); }
+static inline float native_sin(float x) { return std::sin(x); }
+static inline float native_cos(float x) { return std::cos(x); }
+static inline float native_divide(float a, float b) { return a / b; }
+static inline float mad(float a, float b, float c) { return a * b + c; }
+static inline float clamp(float x, float lo, float hi) { return std::fmin(std::fmax(x, lo), hi); }
+static inline int atomic_add(int* p, int v) { return atomicAdd(p, v); }
+static inline int atomic_inc(int* p) { return atomicAdd(p, 1); }
+#endif
+// ---- end prelude ----
+)CEK";
+
+std::string gpu_rewrite(const std::string& src) {
+  std::string s = is_opencl_dialect(src) ? translate_opencl(src) : strip_comments(src);
+  // hiprtc supplies the HIP runtime itself.
+  s = regex_replace_all(s, R"(#\s*include\s*[<"]hip/hip_runtime\.h[>"])", "");
+  auto sites = find_sites(s);
+  for (auto it = sites.rbegin(); it != sites.rend(); ++it) {
+    const auto& k = *it;
+    std::string inside = s.substr(k.open + 1, k.close - k.open - 1);
+    std::string hidden = "long long __cek_off, long long __cek_gsize";
+    if (k.sig.arity == 0) {
+      s.replace(k.open + 1, k.close - k.open - 1, hidden);
+    } else {
+      s.insert(k.close, ", " + hidden);
+    }
+    if (!k.has_extern_c) s.insert(k.global_pos, "extern \"C\" ");
+  }
+  return std::string(kGpuPrelude) + "#line 1\n" + s;
+}
+
+std::string cpu_rewrite(const std::string& src) {
+  std::string s = is_opencl_dialect(src) ? translate_opencl(src) : strip_comments(src);
+  s = regex_replace_all(s, R"(#\s*include\s*[<"]hip/[\w\.]+[>"])", "");
+  auto sites = find_sites(s);
+  for (auto it = sites.rbegin(); it != sites.rend(); ++it)
+    if (!it->has_extern_c) s.insert(it->global_pos, "extern \"C\" ");
+  bool barriers = std::regex_search(s, std::regex(R"(__syncthreads\s*\()"));
+  std::ostringstream os;
+  os << kCpuPrelude << "#line 1\n" << s << "\n// ---- runners ----\n";
+  std::set<std::string> seen;
+  for (auto& k : sites) {
+    if (!seen.insert(k.sig.name).second) continue;
+    const std::string& n = k.sig.name;
+    std::ostringstream call, ptype;
+    call << "reinterpret_cast<void (*)(";
+    for (int i = 0; i < k.sig.arity; ++i) call << (i ? ", " : "") << "void*";
+    call << ")>(&" << n << ")(";
+    for (int i = 0; i < k.sig.arity; ++i) call << (i ? ", " : "") << "args[" << i << "]";
+    call << ")";
+    std::string c = call.str();
+    if (!barriers) {
+      os << "extern \"C\" void __cek_run_" << n
+         << "(void** args, long long off, long long gsize, long long first, long long count, int L) {\n"
+         << "  (void)args; __cek_off = off; __cek_gsize = gsize; blockDim.x = (unsigned)L;\n"
+         << "  gridDim.x = (unsigned)(gsize / L);\n"
+         << "  for (long long i = first; i < first + count; ++i) {\n"
+         << "    long long r = i - off; blockIdx.x = (unsigned)(r / L); threadIdx.x = (unsigned)(r % L);\n"
+         << "    " << c << ";\n  }\n}\n";
+    } else {
+      // Fiber runner: whole groups only (first/count multiples of L).
+      os << "static thread_local void** __cek_args_" << n << ";\n"
+         << "static thread_local char* __cek_done_" << n << ";\n"
+         << "static void __cek_entry_" << n << "() { void** args = __cek_args_" << n << "; " << c
+         << "; __cek_done_" << n << "[threadIdx.x] = 1; }\n"
+         << "extern \"C\" void __cek_run_" << n
+         << "(void** args, long long off, long long gsize, long long first, long long count, int L) {\n"
+         << "  __cek_off = off; __cek_gsize = gsize; blockDim.x = (unsigned)L; gridDim.x = (unsigned)(gsize / L);\n"
+         << "  __cek_args_" << n << " = args;\n"
+         << "  const size_t stack = 64 * 1024;\n"
+         << "  static thread_local char* stacks = nullptr; static thread_local int cap = 0;\n"
+         << "  static thread_local ucontext_t* items = nullptr; static thread_local char* done = nullptr;\n"
+         << "  if (cap < L) { delete[] stacks; delete[] items; delete[] done; stacks = new char[stack * L];\n"
+         << "    items = new ucontext_t[L]; done = new char[L]; cap = L; }\n"
+         << "  __cek_done_" << n << " = done;\n"
+         << "  __CekFibers fib; fib.items = items; __cek_fib = &fib;\n"
+         << "  for (long long g0 = first; g0 < first + count; g0 += L) {\n"
+         << "    blockIdx.x = (unsigned)((g0 - off) / L);\n"
+         << "    for (int t = 0; t < L; ++t) { getcontext(&items[t]); items[t].uc_stack.ss_sp = stacks + stack * t;\n"
+         << "      items[t].uc_stack.ss_size = stack; items[t].uc_link = &fib.sched;\n"
+         << "      makecontext(&items[t], __cek_entry_" << n << ", 0); done[t] = 0; }\n"
+         << "    int remaining = L;\n"
+         << "    while (remaining > 0) {\n"
+         << "      for (int t = 0; t < L; ++t) { if (done[t]) continue; fib.cur = t; threadIdx.x = (unsigned)t;\n"
+         << "        swapcontext(&fib.sched, &items[t]); }\n"
+         << "      remaining = 0; for (int t = 0; t < L; ++t) remaining += !done[t];\n"
+         << "    }\n"
+         << "  }\n  __cek_fib = nullptr;\n}\n";
+    }
+  }
+  std::string out = os.str();
+  return out;
+}
+
+// ------------------------------------------------------------ compilers --
+
+static std::mutex g_jit_mu;
+static std::map<std::string, std::string> g_code_cache;
+
+static std::string rocm_path() {
+  const char* e = getenv("ROCM_PATH");
+  return e && *e ? e : "/opt/rocm";
+}
+
+bool compile_gpu(const std::string& rsrc, const std::vector<std::string>& options,
+                 const std::string& arch_in, std::string& code, std::string& log) {
+  std::string arch = arch_in.empty() ? "gfx950" : arch_in.substr(0, arch_in.find(':'));
+  std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++17",
+                                   "-I" + rocm_path() + "/include"};
+  for (auto& o : options) opts.push_back(o);
+  std::string key_src = rsrc;
+  for (auto& o : opts) key_src += "\x01" + o;
+  std::string key = hash_hex(key_src);
+  {
+    std::lock_guard<std::mutex> g(g_jit_mu);
+    auto it = g_code_cache.find(key);
+    if (it != g_code_cache.end()) {
+      code = it->second;
+      return true;
+    }
+  }
+  std::string path = cache_dir() + "/gpu_" + arch + "_" + key + ".hsaco";
+  if (read_file(path, code) && !code.empty()) {
+    std::lock_guard<std::mutex> g(g_jit_mu);
+    g_code_cache[key] = code;
+    return true;
+  }
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, rsrc.c_str(), "cek_kernels.hip", 0, nullptr, nullptr) !=
+      HIPRTC_SUCCESS) {
+    log = "hiprtcCreateProgram failed";
+    return false;
+  }
+  std::vector<const char*> copts;
+  for (auto& o : opts) copts.push_back(o.c_str());
+  hiprtcResult r = hiprtcCompileProgram(prog, static_cast<int>(copts.size()), copts.data());
+  size_t ls = 0;
+  hiprtcGetProgramLogSize(prog, &ls);
+  if (ls > 1) {
+    std::string l(ls, '\0');
+    hiprtcGetProgramLog(prog, &l[0]);
+    l.resize(strlen(l.c_str()));
+    log = l;
+  }
+  if (r != HIPRTC_SUCCESS) {
+    if (log.empty()) log = hiprtcGetErrorString(r);
+    hiprtcDestroyProgram(&prog);
+    return false;
+  }
+  size_t cs = 0;
+  hiprtcGetCodeSize(prog, &cs);
+  code.assign(cs, '\0');
+  hiprtcGetCode(prog, &code[0]);
+  hiprtcDestroyProgram(&prog);
+  write_file_atomic(path, code);
+  std::lock_guard<std::mutex> g(g_jit_mu);
+  g_code_cache[key] = code;
+  return true;
+}
+
+bool compile_cpu(const std::string& rsrc, const std::vector<std::string>& options,
+                 std::string& so_path, std::string& log) {
+  const char* cxx_env = getenv("CEK_CXX");
+  std::string cxx = cxx_env && *cxx_env ? cxx_env : "g++";
+  // -ffp-contract=off: results match the host reference (numpy) bit-for-bit.
+  std::string flags = "-O3 -march=native -ffp-contract=off -fPIC -shared -std=c++17 -w";
+  for (auto& o : options) flags += " " + o;
+  std::string key = hash_hex(rsrc + "\x01" + cxx + "\x01" + flags);
+  std::string dir = cache_dir();
+  so_path = dir + "/cpu_" + key + ".so";
+  struct stat st;
+  if (stat(so_path.c_str(), &st) == 0 && st.st_size > 0) return true;
+  std::lock_guard<std::mutex> g(g_jit_mu);
+  std::string src_path = dir + "/cpu_" + key + "." + std::to_string(getpid()) + ".cpp";
+  std::string tmp_so = so_path + ".tmp." + std::to_string(getpid());
+  std::string log_path = src_path + ".log";
+  write_file_atomic(src_path, rsrc);
+  std::string cmd = cxx + " " + flags + " -o " + tmp_so + " " + src_path + " > " + log_path + " 2>&1";
+  int rc = std::system(cmd.c_str());
+  read_file(log_path, log);
+  unlink(log_path.c_str());
+  unlink(src_path.c_str());
+  if (rc != 0) {
+    unlink(tmp_so.c_str());
+    if (log.empty()) log = "host compiler failed: " + cmd;
+    return false;
+  }
+  rename(tmp_so.c_str(), so_path.c_str());
+  return true;
+}
+
+// ---------------------------------------------------------------- Program --
+
+std::shared_ptr<Program> Program::build(const DeviceInfo& dev, const std::string& src,
+                                        const std::vector<std::string>& options,
+                                        const std::vector<std::string>& prebuilt) {
+  auto p = std::shared_ptr<Program>(new Program());
+  p->type_ = dev.type;
+  double t0 = now_ms();
+  p->kernels_ = src.empty() ? std::vector<KernelSig>{} : parse_kernels(src);
+  if (dev.type == kGPU) {
+    CEK_HIP(hipSetDevice(dev.ordinal));
+    if (!src.empty()) {
+      std::string code, log;
+      if (!compile_gpu(gpu_rewrite(src), options, dev.arch, code, log)) {
+        p->log_ = log;
+        return p;
+      }
+      p->log_ = log;
+      hipModule_t m;
+      CEK_HIP(hipModuleLoadData(&m, code.data()));
+      p->modules_.push_back(m);
+      for (auto& k : p->kernels_) {
+        hipFunction_t f;
+        CEK_HIP(hipModuleGetFunction(&f, m, k.name.c_str()));
+        p->gpu_fns_[k.name] = f;
+      }
+    }
+    // prebuilt entries: "path|name1,name2"
+    for (auto& pb : prebuilt) {
+      auto bar = pb.find('|');
+      std::string path = pb.substr(0, bar);
+      std::string names = bar == std::string::npos ? "" : pb.substr(bar + 1);
+      hipModule_t m;
+      CEK_HIP(hipModuleLoad(&m, path.c_str()));
+      p->modules_.push_back(m);
+      std::stringstream ss(names);
+      std::string n;
+      while (std::getline(ss, n, ',')) {
+        if (n.empty()) continue;
+        hipFunction_t f;
+        CEK_HIP(hipModuleGetFunction(&f, m, n.c_str()));
+        p->gpu_fns_[n] = f;
+        p->kernels_.push_back({n, -1});
+      }
+    }
+  } else {
+    if (!src.empty()) {
+      std::string so, log;
+      if (!compile_cpu(cpu_rewrite(src), options, so, log)) {
+        p->log_ = log;
+        return p;
+      }
+      p->log_ = log;
+      p->dl_ = dlopen(so.c_str(), RTLD_NOW | RTLD_LOCAL);
+      if (!p->dl_) {
+        p->log_ = std::string("dlopen failed: ") + dlerror();
+        return p;
+      }
+      for (auto& k : p->kernels_) {
+        void* f = dlsym(p->dl_, ("__cek_run_" + k.name).c_str());
+        if (!f) {
+          p->log_ += "missing runner for " + k.name + "\n";
+          return p;
+        }
+        p->cpu_fns_[k.name] = reinterpret_cast<CpuRunner>(f);
+      }
+    }
+  }
+  if (p->kernels_.empty()) {
+    p->log_ += "no kernel found in source (expected `__global__ void name(...)`)";
+    return p;
+  }
+  p->build_ms_ = now_ms() - t0;
+  p->ok_ = true;
+  return p;
+}
+
+Program::~Program() {
+  for (auto m : modules_) (void)hipModuleUnload(m);
+  // dlclose intentionally skipped: thread_local destructors in the kernel
+  // object may still be registered on pool threads.
+}
+
+bool Program::has(const std::string& name) const {
+  return type_ == kGPU ? gpu_fns_.count(name) > 0 : cpu_fns_.count(name) > 0;
+}
+
+hipFunction_t Program::gpu_fn(const std::string& name) const {
+  auto it = gpu_fns_.find(name);
+  if (it == gpu_fns_.end()) throw Error("kernel not found: " + name);
+  return it->second;
+}
+
+CpuRunner Program::cpu_fn(const std::string& name) const {
+  auto it = cpu_fns_.find(name);
+  if (it == cpu_fns_.end()) throw Error("kernel not found on CPU device: " + name);
+  return it->second;
+}
+
+}  // namespace cek

@@ -1,0 +1,344 @@
+#include "worker.h"
+
+#include "memory.h"
+
+namespace cek {
+
+// ----------------------------------------------------------------- CpuPool --
+
+CpuPool::CpuPool(int threads) {
+  for (int i = 1; i < threads; ++i) threads_.emplace_back([this] { loop(); });
+}
+
+CpuPool::~CpuPool() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : threads_) t.join();
+}
+
+void CpuPool::loop() {
+  uint64_t seen = 0;
+  for (;;) {
+    const std::function<void(long long)>* fn;
+    long long n;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      fn = fn_;
+      n = n_;
+      if (!fn) continue;
+      ++active_;
+    }
+    for (long long i = next_++; i < n; i = next_++) (*fn)(i);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      --active_;
+    }
+    done_cv_.notify_all();
+  }
+}
+
+void CpuPool::parallel_for(long long n, const std::function<void(long long)>& fn) {
+  if (n <= 0) return;
+  if (threads_.empty() || n == 1) {
+    for (long long i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    fn_ = &fn;
+    n_ = n;
+    next_ = 0;
+    ++gen_;
+  }
+  cv_.notify_all();
+  for (long long i = next_++; i < n; i = next_++) fn(i);
+  std::unique_lock<std::mutex> lk(mu_);
+  done_cv_.wait(lk, [&] { return active_ == 0 && next_ >= n; });
+  fn_ = nullptr;
+}
+
+// ------------------------------------------------------------------ Worker --
+
+Worker::Worker(const DeviceInfo& dev, std::shared_ptr<Program> prog, int queue_concurrency,
+               bool no_pipelining)
+    : dev_(dev), prog_(std::move(prog)), qconc_(queue_concurrency < 1 ? 1 : (queue_concurrency > 16 ? 16 : queue_concurrency)),
+      no_pipelining_(no_pipelining) {
+  cq_.assign(16, nullptr);
+  marker_issued_per_slot_.assign(32, 0);
+  if (gpu()) {
+    set_device();
+    bool pinned = false;
+    marker_words_ = static_cast<uint64_t*>(host_alloc(32 * sizeof(uint64_t), 4096, &pinned));
+    std::memset(marker_words_, 0, 32 * sizeof(uint64_t));
+  } else {
+    pool_.reset(new CpuPool(dev_.cpu_threads > 0 ? dev_.cpu_threads : 1));
+  }
+  th_ = std::thread([this] { thread_loop(); });
+}
+
+Worker::~Worker() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (th_.joinable()) th_.join();
+  if (gpu()) {
+    try {
+      set_device();
+      sync_all();
+    } catch (...) {
+    }
+    release_all();
+    for (auto e : events_) (void)hipEventDestroy(e);
+    if (main_) (void)hipStreamDestroy(main_);
+    for (auto s : cq_)
+      if (s) (void)hipStreamDestroy(s);
+    for (auto& h : pq_)
+      for (auto s : h)
+        if (s) (void)hipStreamDestroy(s);
+    host_free(marker_words_);
+  }
+}
+
+void Worker::set_device() const {
+  if (gpu()) CEK_HIP(hipSetDevice(dev_.ordinal));
+}
+
+void* Worker::buffer(const ArraySpec& a) {
+  if (!gpu()) return a.host;
+  if (a.zc) {
+    host_register(a.host, a.bytes);
+    std::lock_guard<std::mutex> g(buf_mu_);
+    zc_[a.uid] = true;
+    return host_device_ptr(a.host);
+  }
+  std::lock_guard<std::mutex> g(buf_mu_);
+  auto it = bufs_.find(a.uid);
+  if (it != bufs_.end()) {
+    if (it->second.second >= a.bytes) return it->second.first;
+    (void)hipFree(it->second.first);
+    bytes_allocated_ -= it->second.second;
+    bufs_.erase(it);
+  }
+  void* d = nullptr;
+  set_device();
+  hipError_t e = hipMalloc(&d, a.bytes ? a.bytes : 1);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    throw Error("hipMalloc of " + std::to_string(a.bytes) + " bytes failed on " + dev_.name);
+  }
+  bufs_[a.uid] = {d, a.bytes};
+  bytes_allocated_ += a.bytes;
+  return d;
+}
+
+void Worker::release(uint64_t uid) {
+  std::lock_guard<std::mutex> g(buf_mu_);
+  auto it = bufs_.find(uid);
+  if (it != bufs_.end()) {
+    set_device();
+    (void)hipFree(it->second.first);
+    bytes_allocated_ -= it->second.second;
+    bufs_.erase(it);
+  }
+  zc_.erase(uid);
+}
+
+void Worker::release_all() {
+  std::lock_guard<std::mutex> g(buf_mu_);
+  if (gpu()) {
+    (void)hipSetDevice(dev_.ordinal);
+    for (auto& kv : bufs_) (void)hipFree(kv.second.first);
+  }
+  bufs_.clear();
+  zc_.clear();
+  bytes_allocated_ = 0;
+}
+
+hipStream_t Worker::main_stream() {
+  if (!gpu()) return nullptr;
+  if (!main_) {
+    set_device();
+    CEK_HIP(hipStreamCreateWithFlags(&main_, hipStreamNonBlocking));
+  }
+  return main_;
+}
+
+hipStream_t Worker::compute_stream(int i) {
+  if (!gpu()) return nullptr;
+  i %= 16;
+  if (!cq_[i]) {
+    set_device();
+    CEK_HIP(hipStreamCreateWithFlags(&cq_[i], hipStreamNonBlocking));
+  }
+  return cq_[i];
+}
+
+hipStream_t Worker::pipe_stream(int half, int role) {
+  if (!gpu()) return nullptr;
+  hipStream_t& s = pq_[half & 1][role % 3];
+  if (!s) {
+    set_device();
+    CEK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  }
+  return s;
+}
+
+int Worker::next_compute_queue() { return rr_.fetch_add(1) % qconc_; }
+
+hipEvent_t Worker::event(int slot) {
+  while (static_cast<int>(events_.size()) <= slot) {
+    set_device();
+    hipEvent_t e;
+    CEK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    events_.push_back(e);
+  }
+  return events_[slot];
+}
+
+void Worker::sync_all() {
+  if (!gpu()) return;
+  set_device();
+  if (main_) CEK_HIP(hipStreamSynchronize(main_));
+  for (auto s : cq_)
+    if (s) CEK_HIP(hipStreamSynchronize(s));
+  for (auto& h : pq_)
+    for (auto s : h)
+      if (s) CEK_HIP(hipStreamSynchronize(s));
+}
+
+int Worker::stream_slot(hipStream_t s) {
+  if (s == main_) return 0;
+  for (int i = 0; i < 16; ++i)
+    if (cq_[i] == s) return 1 + i;
+  for (int h = 0; h < 2; ++h)
+    for (int r = 0; r < 3; ++r)
+      if (pq_[h][r] == s) return 17 + h * 3 + r;
+  return 31;
+}
+
+void Worker::h2d(hipStream_t s, const ArraySpec& a, uint64_t elem_begin, uint64_t elem_count) {
+  if (!gpu() || a.zc || elem_count == 0) return;
+  uint64_t off = elem_begin * a.elem_size, n = elem_count * a.elem_size;
+  if (off >= a.bytes) return;
+  if (off + n > a.bytes) n = a.bytes - off;
+  char* d = static_cast<char*>(buffer(a));
+  CEK_HIP(hipMemcpyAsync(d + off, static_cast<const char*>(a.host) + off, n, hipMemcpyHostToDevice, s));
+}
+
+void Worker::d2h(hipStream_t s, const ArraySpec& a, uint64_t elem_begin, uint64_t elem_count) {
+  if (!gpu() || a.zc || elem_count == 0) return;
+  uint64_t off = elem_begin * a.elem_size, n = elem_count * a.elem_size;
+  if (off >= a.bytes) return;
+  if (off + n > a.bytes) n = a.bytes - off;
+  char* d = static_cast<char*>(buffer(a));
+  CEK_HIP(hipMemcpyAsync(static_cast<char*>(a.host) + off, d + off, n, hipMemcpyDeviceToHost, s));
+}
+
+void Worker::launch(hipStream_t s, const std::string& kernel, const std::vector<ArraySpec>& arrs,
+                    long long offset, long long count, int local, long long gsize) {
+  if (count <= 0) return;
+  if (local <= 0) throw Error("local range must be positive");
+  if (count % local != 0)
+    throw Error("range " + std::to_string(count) + " is not a multiple of local range " +
+                std::to_string(local));
+  if (gpu()) {
+    hipFunction_t f = prog_->gpu_fn(kernel);
+    std::vector<void*> ptrs(arrs.size());
+    for (size_t i = 0; i < arrs.size(); ++i) ptrs[i] = buffer(arrs[i]);
+    long long off = offset, gs = gsize;
+    std::vector<void*> params(arrs.size() + 2);
+    for (size_t i = 0; i < arrs.size(); ++i) params[i] = &ptrs[i];
+    params[arrs.size()] = &off;
+    params[arrs.size() + 1] = &gs;
+    unsigned grid = static_cast<unsigned>(count / local);
+    CEK_HIP(hipModuleLaunchKernel(f, grid, 1, 1, static_cast<unsigned>(local), 1, 1, dyn_lds_, s,
+                                  params.data(), nullptr));
+  } else {
+    CpuRunner fn = prog_->cpu_fn(kernel);
+    std::vector<void*> ptrs(arrs.size());
+    for (size_t i = 0; i < arrs.size(); ++i) ptrs[i] = arrs[i].host;
+    long long groups = count / local;
+    // chunk groups so every pool thread gets several (amortise dispatch)
+    long long nthreads = pool_->size();
+    long long per = std::max<long long>(1, groups / (nthreads * 8));
+    long long tasks = (groups + per - 1) / per;
+    void** argv = ptrs.data();
+    pool_->parallel_for(tasks, [&](long long t) {
+      long long g0 = t * per, g1 = std::min(groups, g0 + per);
+      fn(argv, offset, gsize, offset + g0 * local, (g1 - g0) * local, local);
+    });
+  }
+}
+
+void Worker::add_marker(hipStream_t s) {
+  ++markers_issued_;
+  if (!gpu()) return;
+  int slot = stream_slot(s);
+  uint64_t v = ++marker_issued_per_slot_[slot];
+  CEK_HIP(hipStreamWriteValue64(s, host_device_ptr(&marker_words_[slot]), v, 0));
+}
+
+long long Worker::markers_reached() {
+  if (!gpu()) return markers_issued_;
+  long long r = 0;
+  for (int i = 0; i < 32; ++i) r += static_cast<long long>(__atomic_load_n(&marker_words_[i], __ATOMIC_ACQUIRE));
+  return r;
+}
+
+void Worker::post(std::function<void()> fn) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    q_.push_back(std::move(fn));
+  }
+  cv_.notify_one();
+}
+
+void Worker::wait() {
+  std::unique_lock<std::mutex> lk(mu_);
+  idle_cv_.wait(lk, [&] { return q_.empty() && !busy_; });
+  if (err_) {
+    auto e = err_;
+    err_ = nullptr;
+    std::rethrow_exception(e);
+  }
+}
+
+void Worker::thread_loop() {
+  bool device_set = false;
+  for (;;) {
+    std::function<void()> job;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (stop_ && q_.empty()) return;
+      job = std::move(q_.front());
+      q_.pop_front();
+      busy_ = true;
+    }
+    try {
+      if (!device_set && gpu()) {
+        set_device();
+        device_set = true;
+      }
+      job();
+    } catch (...) {
+      std::lock_guard<std::mutex> g(mu_);
+      if (!err_) err_ = std::current_exception();
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      busy_ = false;
+    }
+    idle_cv_.notify_all();
+  }
+}
+
+}  // namespace cek

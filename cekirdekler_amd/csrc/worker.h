@@ -1,0 +1,143 @@
+// Per-device worker: the MI355X-native counterpart of the reference's
+// ClObject.Worker (Worker.cs:33-1738).  A worker owns one device, a lazily
+// created pool of HIP streams (main, up to 16 round-robin compute streams,
+// and read/compute/write streams for the two event-pipeline halves — the
+// reference's 20-21 OpenCL queues, Worker.cs:75-259), the compiled program,
+// one full-length device replica per host array (Worker.cs:576-720), marker
+// words for fine-grained queue control, and a persistent host thread that
+// executes fan-out jobs (replacing Parallel.For, Cores.cs:747-834).
+//
+// The CPU device executes the same kernel source compiled for the host on a
+// thread pool; it works directly on host memory (no copies).
+#pragma once
+#include <condition_variable>
+#include <deque>
+#include <exception>
+#include <map>
+#include <thread>
+#include <unordered_map>
+
+#include "common.h"
+#include "device.h"
+#include "jit.h"
+
+namespace cek {
+
+// One kernel-parameter array of a compute() call (ClArray flags,
+// ClArray.cs:1742-1888; token semantics Worker.cs:827-834, :1349-1356).
+struct ArraySpec {
+  uint64_t uid = 0;       // identity of the host array (buffer-cache key)
+  void* host = nullptr;   // host pointer
+  uint64_t bytes = 0;     // total bytes of the host array
+  int elem_size = 4;
+  bool read = true;       // H2D the whole array to every device
+  bool partial = false;   // H2D only this device's slice (wins over read)
+  bool write = true;      // D2H this device's slice
+  bool write_all = false; // device (index mod D) D2H the whole array
+  bool ro = false, wo = false;  // access hints
+  bool zc = false;        // zero-copy: kernel reads/writes host memory
+  int epw = 1;            // elements per work item
+};
+
+class CpuPool {
+ public:
+  explicit CpuPool(int threads);
+  ~CpuPool();
+  // Run fn(i) for i in [0, n) across the pool; blocks until done.
+  void parallel_for(long long n, const std::function<void(long long)>& fn);
+  int size() const { return static_cast<int>(threads_.size()) + 1; }
+
+ private:
+  void loop();
+  std::vector<std::thread> threads_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(long long)>* fn_ = nullptr;
+  long long n_ = 0;
+  std::atomic<long long> next_{0};
+  int active_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+class Worker {
+ public:
+  Worker(const DeviceInfo& dev, std::shared_ptr<Program> prog, int queue_concurrency,
+         bool no_pipelining);
+  ~Worker();
+
+  const DeviceInfo& dev() const { return dev_; }
+  bool gpu() const { return dev_.type == kGPU; }
+  Program& program() { return *prog_; }
+
+  // --- buffers ---------------------------------------------------------
+  void* buffer(const ArraySpec& a);  // device-visible pointer for a
+  void release(uint64_t uid);
+  void release_all();
+  uint64_t bytes_allocated() const { return bytes_allocated_; }
+
+  // --- streams ---------------------------------------------------------
+  hipStream_t main_stream();
+  hipStream_t compute_stream(int i);        // i in [0, queue_concurrency)
+  hipStream_t pipe_stream(int half, int role);  // role 0=read 1=compute 2=write
+  int next_compute_queue();                 // round robin (Worker.cs:435-458)
+  int queue_concurrency() const { return qconc_; }
+  hipEvent_t event(int slot);               // pooled, timing disabled
+  void sync_all();                          // finish every created stream
+  void set_device() const;
+
+  // --- ops (enqueue on GPU; synchronous on the CPU device) --------------
+  void h2d(hipStream_t s, const ArraySpec& a, uint64_t elem_begin, uint64_t elem_count);
+  void d2h(hipStream_t s, const ArraySpec& a, uint64_t elem_begin, uint64_t elem_count);
+  void launch(hipStream_t s, const std::string& kernel, const std::vector<ArraySpec>& arrs,
+              long long offset, long long count, int local, long long gsize);
+  void set_dynamic_lds(unsigned bytes) { dyn_lds_ = bytes; }
+
+  // --- markers (fine-grained queue control, ClCommandQueue.cs:103-112) ---
+  void add_marker(hipStream_t s);
+  long long markers_reached();
+  long long markers_issued() const { return markers_issued_; }
+
+  // --- job thread --------------------------------------------------------
+  void post(std::function<void()> fn);
+  void wait();  // rethrows the first job exception
+
+  // --- timing (Worker.cs:753-807) ---------------------------------------
+  std::map<int, double> bench_ms;
+
+ private:
+  void thread_loop();
+  int stream_slot(hipStream_t s);
+
+  DeviceInfo dev_;
+  std::shared_ptr<Program> prog_;
+  int qconc_;
+  bool no_pipelining_;
+  unsigned dyn_lds_ = 0;
+  std::unordered_map<uint64_t, std::pair<void*, uint64_t>> bufs_;
+  std::unordered_map<uint64_t, bool> zc_;
+  uint64_t bytes_allocated_ = 0;
+  std::mutex buf_mu_;
+
+  hipStream_t main_ = nullptr;
+  std::vector<hipStream_t> cq_;
+  hipStream_t pq_[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
+  std::vector<hipEvent_t> events_;
+  std::atomic<int> rr_{0};
+
+  // markers: one 64-bit word per stream slot in pinned host memory
+  uint64_t* marker_words_ = nullptr;
+  std::vector<uint64_t> marker_issued_per_slot_;
+  long long markers_issued_ = 0;
+
+  std::unique_ptr<CpuPool> pool_;
+
+  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_, idle_cv_;
+  std::deque<std::function<void()>> q_;
+  bool busy_ = false, stop_ = false;
+  std::exception_ptr err_;
+};
+
+}  // namespace cek

@@ -1,0 +1,148 @@
+// bf16 GEMM on CDNA4 matrix cores, fp32 accumulate / fp32 output
+// ("SGEMM 8192² bf16" of BASELINE.json), range-partitionable by compute():
+//
+//   C = A · Bᵀ      A: [M][K] bf16 row-major, Bt: [N][K] bf16 row-major
+//   C is written TILE-MAJOR: tile t = (tm, tn) (tn fastest) occupies
+//   C[t·BM·BN ...] row-major inside the tile, so any contiguous range of
+//   tiles — the slice a device gets from the load balancer — is one
+//   contiguous byte range (the reference's partial write of
+//   [ref·e, (ref+r)·e), Worker.cs:1349-1352, with e = BM·BN / local).
+//
+// Work decomposition for compute(): one work-group (local = 128·WN threads)
+// per BM×BN tile, global range = tiles × local.  The work-group's absolute
+// tile is its XCD-remapped local block id + __cek_off / local.
+//
+// Structure (cdna_hip_programming.md §5): 256×BN tile, BK = 64, 2·WN waves
+// (2 along M × WN along N), each wave 128×64 of C as 8×4 tiles of
+// v_mfma_f32_16x16x32_bf16; both operands staged global→LDS with
+// global_load_lds_dwordx4 (16 B/lane, lane-linear LDS image) into two LDS
+// stages — the next K-tile's DMA is issued before the current tile's MFMAs
+// and retired by one vmcnt(0)+barrier per K-tile.  LDS rows are 128 B; the
+// 16-B chunk index is XOR-swizzled with (row & 7) on the global SOURCE
+// address and on the ds_read_b128 address (rule 21), which makes every
+// fragment read conflict-free (each 16-lane group hits 16 distinct slots).
+#include "cek_kernel.h"
+
+namespace {
+
+template <int WN>
+__device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
+                                          const uint16_t* __restrict__ A,
+                                          const uint16_t* __restrict__ Bt, float* __restrict__ C,
+                                          char* smem, long long off) {
+  constexpr int BM = 256, BN = 64 * WN, BK = 64;
+  constexpr int NWAVES = 2 * WN, NT = 64 * NWAVES;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_INSTR = A_BYTES / 1024 / NWAVES;
+  constexpr int B_INSTR = B_BYTES / 1024 / NWAVES;
+
+  const int N = dims[1], K = dims[2];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WN, wc = wave % WN;
+  const long long t = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
+  const int ntn = N / BN;
+  const int tm = (int)(t / ntn), tn = (int)(t % ntn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // Staging: instruction `ins` of this wave fills LDS bytes [ins·1 KiB, +1 KiB)
+  // = 8 rows × 128 B; lane l lands at row ins·8 + l/8, physical chunk l%8,
+  // which holds logical chunk (l%8) ^ (row & 7).
+  const uint16_t* a_src[A_INSTR];
+  const uint16_t* b_src[B_INSTR];
+#pragma unroll
+  for (int j = 0; j < A_INSTR; ++j) {
+    const int ins = wave * A_INSTR + j, row = ins * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ (row & 7);
+    a_src[j] = A + (size_t)(m0 + row) * K + lc * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < B_INSTR; ++j) {
+    const int ins = wave * B_INSTR + j, row = ins * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ (row & 7);
+    b_src[j] = Bt + (size_t)(n0 + row) * K + lc * 8;
+  }
+
+  auto stage = [&](int buf, int kt) {
+    char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < A_INSTR; ++j)
+      __builtin_amdgcn_global_load_lds((glb_cvoid*)(a_src[j] + (size_t)kt * BK),
+                                       (lds_void*)(base + (wave * A_INSTR + j) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < B_INSTR; ++j)
+      __builtin_amdgcn_global_load_lds((glb_cvoid*)(b_src[j] + (size_t)kt * BK),
+                                       (lds_void*)(base + A_BYTES + (wave * B_INSTR + j) * 1024), 16, 0, 0);
+  };
+
+  // Fragment read offsets (bytes) inside a stage: row (wr·128 + i·16 + l%16),
+  // logical chunk s·4 + l/16, physical = logical ^ (l & 7).
+  const int fr = lane & 15, fq = lane >> 4;
+  int a_off[2], b_off[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int pc = (s * 4 + fq) ^ (lane & 7);
+    a_off[s] = (wr * 128 + fr) * 128 + pc * 16;
+    b_off[s] = A_BYTES + (wc * 64 + fr) * 128 + pc * 16;
+  }
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    const char* base = smem + cur * STAGE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 a[8], b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // Epilogue: acc[i][j][r] is C(row = wr·128 + i·16 + fq·4 + r, col = wc·64 + j·16 + fr)
+  float* ct = C + (size_t)t * BM * BN;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        ct[(size_t)(wr * 128 + i * 16 + fq * 4 + r) * BN + wc * 64 + j * 16 + fr] = acc[i][j][r];
+}
+
+}  // namespace
+
+// 256×256 tiles, 512 threads (8 waves), 128 KiB LDS.
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * (256 * 64 * 2 + 256 * 64 * 2)];
+  gemm_tile<4>(dims, A, Bt, C, smem, __cek_off);
+}
+
+// 256×128 tiles, 256 threads (4 waves), 96 KiB LDS — twice the tiles, for
+// strongly scaled slices (8 GPUs × 1024 rows of an 8192² problem).
+extern "C" __global__ __launch_bounds__(256) void cek_sgemm_bf16_256x128(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * (256 * 64 * 2 + 128 * 64 * 2)];
+  gemm_tile<2>(dims, A, Bt, C, smem, __cek_off);
+}

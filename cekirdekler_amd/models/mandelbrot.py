@@ -1,0 +1,76 @@
+"""Mandelbrot renderer on the AOT CDNA4 kernel (BASELINE config
+"Mandelbrot 4096×4096, 1×MI355X, event-driven read/compute/write pipeline").
+
+The image is one 1-D range of quads (4 pixels per work item); with
+``pipeline=True`` each device's slice is cut into ``blobs`` chunks whose
+kernel runs overlap the previous chunks' device→host copies (the reference's
+event-driven pipeline, Cores.cs:1197-1367).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ..arrays import ClArray
+from ..cruncher import PIPELINE_EVENT, ClNumberCruncher
+from ..ops.library import library
+
+FLOP_PER_ITER = 8
+
+
+class MandelbrotRenderer:
+    def __init__(self, width: int = 4096, height: int = 4096, max_iter: int = 256,
+                 view=(-2.0, -1.5, 3.0, 3.0), devices=None, cruncher: ClNumberCruncher | None = None):
+        if (width * height) % 1024:
+            raise ValueError("width*height must be a multiple of 1024")
+        x0, y0, w, h = view
+        self.width, self.height, self.max_iter = width, height, max_iter
+        self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library("mandelbrot"))
+        self.view = ClArray(np.array([x0, y0, w / width, h / height], np.float32))
+        self.size = ClArray(np.array([width, height, max_iter, 0], np.int32))
+        for a in (self.view, self.size):
+            a.write = False
+        self.out = ClArray(width * height, np.int32)
+        self.out.read = False
+        self.out.elements_per_work_item = 4
+        self.global_range = width * height // 4
+        self._last_id = None
+
+    def render(self, compute_id: int = 1, pipeline: bool = True, blobs: int = 8,
+               pipeline_type: bool = PIPELINE_EVENT) -> np.ndarray:
+        self.view.next_param(self.size, self.out).compute(
+            self.cr, compute_id, "cek_mandelbrot_f32", self.global_range, 256, 0, pipeline,
+            pipeline_type, blobs)
+        self._last_id = compute_id
+        return self.out.array.reshape(self.height, self.width)
+
+    def local_slice(self) -> slice:
+        cid = self._last_id
+        refs, rng = self.cr.references(cid), self.cr.ranges(cid)
+        base = self.cr._cores.global_base
+        n = self.cr._cores.num_devices
+        lo = refs[base] * 4
+        hi = (refs[base + n - 1] + rng[base + n - 1]) * 4
+        return slice(lo, hi)
+
+    def flops(self) -> float:
+        """FLOPs of the pixels this process computed (8 per iteration)."""
+        it = self.out.array[self.local_slice()].astype(np.int64)
+        return float(FLOP_PER_ITER * (it + 1).sum())
+
+    def reference(self, rows=None) -> np.ndarray:
+        x0, y0, dx, dy = (float(v) for v in self.view.array)
+        ys = np.arange(self.height if rows is None else rows, dtype=np.float32)
+        xs = np.arange(self.width, dtype=np.float32)
+        cr = (np.float32(x0) + xs * np.float32(dx))[None, :].repeat(len(ys), 0)
+        ci = (np.float32(y0) + ys * np.float32(dy))[:, None].repeat(self.width, 1)
+        zr = np.zeros_like(cr)
+        zi = np.zeros_like(cr)
+        n = np.full(cr.shape, self.max_iter, np.int32)
+        for it in range(self.max_iter):
+            zr2, zi2 = zr * zr, zi * zi
+            esc = (zr2 + zi2 > 4) & (n == self.max_iter)
+            n[esc] = it
+            t = zr * zi
+            zi = t + t + ci
+            zr = zr2 - zi2 + cr
+        return n

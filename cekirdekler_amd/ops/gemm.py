@@ -1,0 +1,105 @@
+"""Range-partitioned bf16 GEMM (the "SGEMM 8192² bf16" config of BASELINE.json).
+
+``C = A · Bᵀ`` with A ``[M][K]`` and Bt ``[N][K]`` bf16 row-major, C fp32 in
+tile-major layout (see ``kernels/sgemm_bf16.hip``).  The global range is one
+work-group per output tile, so the load balancer splits the problem across
+devices in whole tiles and each device's C slice is one contiguous range
+(``elements_per_work_item = BM·BN / local``).
+
+``resident=True`` keeps A and B on the devices after the first upload and
+leaves C in device memory (the BASELINE "device-resident" number);
+``resident=False`` is the reference's host-resident semantics: A and B are
+uploaded and every device downloads its C slice on each call.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ..arrays import ClArray
+from ..cruncher import ClNumberCruncher
+from .library import library
+
+TILES = {"256x256": (256, 256, 512, "cek_sgemm_bf16_256x256"),
+         "256x128": (256, 128, 256, "cek_sgemm_bf16_256x128")}
+
+
+def to_bf16_bits(x: np.ndarray) -> np.ndarray:
+    """fp32 → bf16 bit patterns (round to nearest even), as uint16."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    return r
+
+
+def from_bf16_bits(b: np.ndarray) -> np.ndarray:
+    return (b.astype(np.uint32) << 16).view(np.float32)
+
+
+def untile(c: np.ndarray, M: int, N: int, BM: int, BN: int) -> np.ndarray:
+    """Tile-major C → row-major [M][N]."""
+    return c.reshape(M // BM, N // BN, BM, BN).transpose(0, 2, 1, 3).reshape(M, N)
+
+
+class GemmBf16:
+    def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256",
+                 cruncher: ClNumberCruncher | None = None, fill: str = "random", seed: int = 0):
+        BM, BN, L, kname = TILES[tile]
+        if M % BM or N % BN or K % 64:
+            raise ValueError(f"M%{BM}, N%{BN} and K%64 must be 0 (got {M},{N},{K})")
+        self.M, self.N, self.K, self.BM, self.BN, self.L, self.kernel = M, N, K, BM, BN, L, kname
+        self.tiles = (M // BM) * (N // BN)
+        self.global_range = self.tiles * L
+        self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library("sgemm_bf16"))
+        self.dims = ClArray(np.array([M, N, K, 0], np.int32))
+        self.dims.write = False
+        self.A = ClArray(M * K, "bfloat16")
+        self.B = ClArray(N * K, "bfloat16")
+        self.C = ClArray(M * N, np.float32)
+        for a in (self.A, self.B):
+            a.write = False
+        self.C.read = False
+        self.C.elements_per_work_item = BM * BN // L
+        if fill == "random":
+            rng = np.random.default_rng(seed)
+            self.A.array[:] = to_bf16_bits(rng.uniform(-1, 1, M * K).astype(np.float32))
+            self.B.array[:] = to_bf16_bits(rng.uniform(-1, 1, N * K).astype(np.float32))
+        self._uploaded = False
+
+    @property
+    def flops(self) -> float:
+        return 2.0 * self.M * self.N * self.K
+
+    def run(self, compute_id: int = 1, resident: bool = True) -> None:
+        first = not self._uploaded
+        for a in (self.dims, self.A, self.B):
+            a.read = first or not resident
+        self.C.write = not resident
+        self.dims.next_param(self.A, self.B, self.C).compute(
+            self.cr, compute_id, self.kernel, self.global_range, self.L)
+        self._uploaded = True
+
+    def result(self, download: bool = True) -> np.ndarray:
+        """Row-major fp32 C (downloads every device's slice when resident)."""
+        if download:
+            rng = self.cr.ranges(self.cr._cores.last_compute_id)
+            refs = self.cr.references(self.cr._cores.last_compute_id)
+            e = self.C.elements_per_work_item
+            for dev in range(self.cr._cores.num_devices):
+                g = self.cr._cores.global_base + dev
+                lo, n = refs[g] * e, rng[g] * e
+                self._download_slice(dev, lo, n)
+        return untile(self.C.array, self.M, self.N, self.BM, self.BN)
+
+    def _download_slice(self, dev: int, lo: int, n: int) -> None:
+        # a sub-view ClArray sharing the same uid would alias buffers; the
+        # native download copies the whole replica, slice afterwards
+        tmp = np.empty_like(self.C.array)
+        saved = self.C.array.copy()
+        self.cr.download(self.C, dev)
+        tmp[:] = self.C.array
+        self.C.array[:] = saved
+        self.C.array[lo:lo + n] = tmp[lo:lo + n]
+
+    def reference(self, rows: slice = slice(None)) -> np.ndarray:
+        a = from_bf16_bits(self.A.array).reshape(self.M, self.K)[rows].astype(np.float64)
+        b = from_bf16_bits(self.B.array).reshape(self.N, self.K).astype(np.float64)
+        return a @ b.T

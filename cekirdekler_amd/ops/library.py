@@ -1,0 +1,37 @@
+"""Registry of the AOT gfx950 kernel library (``kernels/*.hip`` →
+``*.hsaco``, built by :mod:`cekirdekler_amd.build_native`).
+
+Each entry maps a library name to its code object and exported kernel names,
+in the ``prebuilt`` form accepted by :class:`ClNumberCruncher`.  Library
+kernels follow the runtime launch ABI (arrays, then the hidden offset and
+global size), so they are range-partitioned and load-balanced by compute()
+exactly like user kernel strings.
+"""
+from __future__ import annotations
+
+import os
+
+from .._native import kernel_dir
+
+LIBRARY = {
+    "sgemm_bf16": ["cek_sgemm_bf16_256x256", "cek_sgemm_bf16_256x128"],
+    "mandelbrot": ["cek_mandelbrot_f32"],
+    "reduce": ["cek_reduce_sum_f32", "cek_reduce_sum_f32_final"],
+    "stream": ["cek_saxpy_f32", "cek_copy_u8", "cek_vec_add_f32"],
+}
+
+
+def code_object(name: str) -> str:
+    path = os.path.join(kernel_dir(), name + ".hsaco")
+    if not os.path.exists(path):
+        from .. import build_native
+
+        build_native.build_kernels()
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"kernel library {name!r} not built: {path}")
+    return path
+
+
+def library(*names: str):
+    """``prebuilt`` entries for the given library names."""
+    return [(code_object(n), LIBRARY[n]) for n in names]

@@ -1,0 +1,33 @@
+"""GPU probe: time the AOT GEMM kernels through compute() vs torch.matmul."""
+import sys, time, json
+sys.path.insert(0, '.')
+import numpy as np
+import torch
+import cekirdekler_amd as ck
+from cekirdekler_amd.ops.gemm import GemmBf16
+
+res = {}
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+g0 = ck.ClPlatforms.all().gpus()[0]
+for tile in ["256x256", "256x128"]:
+    g = GemmBf16(n, n, n, devices=g0, tile=tile)
+    for _ in range(3): g.run(resident=True)
+    torch.cuda.synchronize()
+    t = time.perf_counter(); K = 20
+    for _ in range(K): g.run(resident=True)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) * 1e3 / K
+    res[tile] = {"ms": ms, "tflops": g.flops / ms / 1e9, "dev_ms": g.cr.benchmarks(1)}
+    if n <= 8192:
+        rows = slice(0, 256)
+        c = g.result(download=True)[rows]
+        ref = g.reference(rows)
+        res[tile]["max_err"] = float(np.abs(c - ref).max())
+a = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
+b = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
+for _ in range(3): torch.matmul(a, b.t())
+torch.cuda.synchronize(); t = time.perf_counter()
+for _ in range(20): torch.matmul(a, b.t())
+torch.cuda.synchronize(); ms = (time.perf_counter() - t) * 1e3 / 20
+res["torch_bf16_nt"] = {"ms": ms, "tflops": 2 * n**3 / ms / 1e9}
+print(json.dumps(res, indent=1))
