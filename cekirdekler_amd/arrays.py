@@ -240,6 +240,10 @@ class ClArray:
         self._wo = False
         self.zero_copy = False
         self.elements_per_work_item = 1
+        # extension: >0 means N elements per work-GROUP (per-group outputs such
+        # as reduction partials); the slice of a device is then
+        # [ref/L·N, (ref+r)/L·N)
+        self.elements_per_group = 0
         self._registered = False
         self._disposed = False
 
@@ -479,7 +483,8 @@ class ClArray:
             self._registered = bool(cek.host_register(arr.ctypes.data, arr.nbytes))
         return cek.ArraySpec(self._uid, arr.ctypes.data, arr.nbytes, arr.itemsize,
                              self._read, self._partial, self._write, self._write_all,
-                             self._ro, self._wo, bool(self.zero_copy), int(self.elements_per_work_item))
+                             self._ro, self._wo, bool(self.zero_copy), int(self.elements_per_work_item),
+                             int(self.elements_per_group))
 
     @property
     def uid(self) -> int:

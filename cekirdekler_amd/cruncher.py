@@ -305,7 +305,12 @@ class ClNumberCruncher:
             raise ClComputeError("no kernel name given")
         for a in group.arrays:
             if a._partial or (a._write and not a._write_all):
-                if a.N < G * a.elements_per_work_item:
+                if a.elements_per_group > 0:
+                    if a.N < (G // L) * a.elements_per_group:
+                        raise ClComputeError(
+                            f"Array-size error: (number of groups)*(elements per group)="
+                            f"({(G // L) * a.elements_per_group}) must be <= array length ({a.N}).")
+                elif a.N < G * a.elements_per_work_item:
                     raise ClComputeError(
                         f"Array-size error: (global range)*(number of array elements per work item)="
                         f"({G * a.elements_per_work_item}) must be equal to or less than array length ({a.N}).")

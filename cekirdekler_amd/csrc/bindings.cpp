@@ -112,7 +112,7 @@ PYBIND11_MODULE(_cek, m) {
   py::class_<ArraySpec>(m, "ArraySpec")
       .def(py::init<>())
       .def(py::init([](uint64_t uid, uint64_t host, uint64_t bytes, int elem_size, bool read, bool partial,
-                       bool write, bool write_all, bool ro, bool wo, bool zc, int epw) {
+                       bool write, bool write_all, bool ro, bool wo, bool zc, int epw, int epg) {
              ArraySpec a;
              a.uid = uid;
              a.host = reinterpret_cast<void*>(host);
@@ -126,11 +126,12 @@ PYBIND11_MODULE(_cek, m) {
              a.wo = wo;
              a.zc = zc;
              a.epw = epw;
+             a.epg = epg;
              return a;
            }),
            py::arg("uid"), py::arg("host"), py::arg("bytes"), py::arg("elem_size"), py::arg("read") = true,
            py::arg("partial") = false, py::arg("write") = true, py::arg("write_all") = false,
-           py::arg("ro") = false, py::arg("wo") = false, py::arg("zc") = false, py::arg("epw") = 1)
+           py::arg("ro") = false, py::arg("wo") = false, py::arg("zc") = false, py::arg("epw") = 1, py::arg("epg") = 0)
       .def_readwrite("uid", &ArraySpec::uid)
       .def_property("host", [](const ArraySpec& a) { return reinterpret_cast<uint64_t>(a.host); },
                     [](ArraySpec& a, uint64_t p) { a.host = reinterpret_cast<void*>(p); })
@@ -143,7 +144,8 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("ro", &ArraySpec::ro)
       .def_readwrite("wo", &ArraySpec::wo)
       .def_readwrite("zc", &ArraySpec::zc)
-      .def_readwrite("epw", &ArraySpec::epw);
+      .def_readwrite("epw", &ArraySpec::epw)
+      .def_readwrite("epg", &ArraySpec::epg);
 
   py::class_<ComputeCall>(m, "ComputeCall")
       .def(py::init<>())

@@ -250,8 +250,10 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
   for (auto& a : c.arrays) {
     if (a.zc) continue;
     if (a.partial) {
-      wk.h2d(s, a, static_cast<uint64_t>(ref) * a.epw, static_cast<uint64_t>(range) * a.epw);
-      *h2d += static_cast<uint64_t>(range) * a.epw * a.elem_size;
+      uint64_t b, n;
+      a.slice(ref, range, c.local_range, b, n);
+      wk.h2d(s, a, b, n);
+      *h2d += n * a.elem_size;
     }
   }
   full_reads(wk, s, c, h2d);
@@ -265,8 +267,10 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
       if (a.zc || !(a.write || a.wo) || a.write_all) continue;
       std::vector<uint64_t> offs(global_devices_), sizes(global_devices_);
       for (int g = 0; g < global_devices_; ++g) {
-        offs[g] = static_cast<uint64_t>(st.references[g]) * a.epw * a.elem_size;
-        sizes[g] = static_cast<uint64_t>(st.ranges[g]) * a.epw * a.elem_size;
+        uint64_t b, n;
+        a.slice(st.references[g], st.ranges[g], c.local_range, b, n);
+        offs[g] = b * a.elem_size;
+        sizes[g] = n * a.elem_size;
         if (offs[g] + sizes[g] > a.bytes) sizes[g] = offs[g] < a.bytes ? a.bytes - offs[g] : 0;
       }
       comm_->allgatherv(wk.buffer(a), offs, sizes, s);
@@ -285,8 +289,10 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
       wk.d2h(s, a, 0, a.bytes / a.elem_size);
       *d2h += a.bytes;
     } else {
-      wk.d2h(s, a, static_cast<uint64_t>(ref) * a.epw, static_cast<uint64_t>(range) * a.epw);
-      *d2h += static_cast<uint64_t>(range) * a.epw * a.elem_size;
+      uint64_t b, n;
+      a.slice(ref, range, c.local_range, b, n);
+      wk.d2h(s, a, b, n);
+      *d2h += n * a.elem_size;
     }
   }
   if (fine_grained) wk.add_marker(s);
@@ -315,8 +321,10 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
       long long off = ref + h * (range / halves) + k * chunk;
       for (auto& a : c.arrays) {
         if (a.zc || !a.partial) continue;
-        wk.h2d(rs, a, static_cast<uint64_t>(off) * a.epw, static_cast<uint64_t>(chunk) * a.epw);
-        *h2d += static_cast<uint64_t>(chunk) * a.epw * a.elem_size;
+        uint64_t b, n;
+        a.slice(off, chunk, c.local_range, b, n);
+        wk.h2d(rs, a, b, n);
+        *h2d += n * a.elem_size;
       }
       if (wk.gpu()) {
         hipEvent_t er = wk.event(slot++);
@@ -331,8 +339,10 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
       }
       for (auto& a : c.arrays) {
         if (a.zc || !a.write || a.write_all) continue;
-        wk.d2h(ws, a, static_cast<uint64_t>(off) * a.epw, static_cast<uint64_t>(chunk) * a.epw);
-        *d2h += static_cast<uint64_t>(chunk) * a.epw * a.elem_size;
+        uint64_t b, n;
+        a.slice(off, chunk, c.local_range, b, n);
+        wk.d2h(ws, a, b, n);
+        *d2h += n * a.elem_size;
       }
     }
   }
@@ -384,14 +394,18 @@ void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long
     long long off = ref + k * chunk;
     for (auto& a : c.arrays) {
       if (a.zc || !a.partial) continue;
-      wk.h2d(s, a, static_cast<uint64_t>(off) * a.epw, static_cast<uint64_t>(chunk) * a.epw);
-      *h2d += static_cast<uint64_t>(chunk) * a.epw * a.elem_size;
+      uint64_t b, n;
+      a.slice(off, chunk, c.local_range, b, n);
+      wk.h2d(s, a, b, n);
+      *h2d += n * a.elem_size;
     }
     launch_kernels(wk, s, c, off, chunk);
     for (auto& a : c.arrays) {
       if (a.zc || !a.write || a.write_all) continue;
-      wk.d2h(s, a, static_cast<uint64_t>(off) * a.epw, static_cast<uint64_t>(chunk) * a.epw);
-      *d2h += static_cast<uint64_t>(chunk) * a.epw * a.elem_size;
+      uint64_t b, n;
+      a.slice(off, chunk, c.local_range, b, n);
+      wk.d2h(s, a, b, n);
+      *d2h += n * a.elem_size;
     }
   }
   if (wk.gpu()) {

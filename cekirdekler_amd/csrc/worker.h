@@ -37,6 +37,17 @@ struct ArraySpec {
   bool ro = false, wo = false;  // access hints
   bool zc = false;        // zero-copy: kernel reads/writes host memory
   int epw = 1;            // elements per work item
+  int epg = 0;            // >0: elements per work-GROUP instead (per-group outputs)
+  // Element slice [begin, begin+count) owned by work items [ref, ref+range).
+  void slice(long long ref, long long range, long long local, uint64_t& begin, uint64_t& count) const {
+    if (epg > 0) {
+      begin = static_cast<uint64_t>(ref / local) * epg;
+      count = static_cast<uint64_t>(range / local) * epg;
+    } else {
+      begin = static_cast<uint64_t>(ref) * epw;
+      count = static_cast<uint64_t>(range) * epw;
+    }
+  }
 };
 
 class CpuPool {

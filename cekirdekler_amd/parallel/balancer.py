@@ -1,0 +1,167 @@
+"""Load balancers.
+
+* :func:`load_balance` / :func:`initial_split` — thin wrappers over the
+  native implementation of the reference law (HelperFunctions.cs:190-280),
+  which the scheduler runs per compute id.
+* :func:`load_balance_py` — an independent pure-Python transcription of the
+  same law, used by the tests to pin the native one.
+* :class:`ClusterLoadBalancer` — node-level balancing for the cluster layer
+  (ClusterLoadBalancer.cs:143-349): equal split in units of the LCM of the
+  node steps, then ``t + 0.3·(p − t)`` snapped to each node's step; the
+  remainder runs on the local "mainframe" node.
+* :func:`convergence_iters` — the "load-balance iters" metric: computes until
+  every share stays within a tolerance of its steady state.
+"""
+from __future__ import annotations
+
+import math
+from functools import reduce
+from typing import List, Sequence, Tuple
+
+from .._native import cek
+
+HISTORY_DEPTH = 10
+
+
+def load_balance(bench: Sequence[float], smooth: bool, history: List[List[float]], total: int,
+                 ranges: Sequence[int], step: int) -> Tuple[List[int], List[List[float]]]:
+    r, h = cek.load_balance(list(map(float, bench)), bool(smooth), history, int(total),
+                            list(map(int, ranges)), int(step))
+    return list(r), [list(x) for x in h]
+
+
+def initial_split(devices: int, smooth: bool, history: List[List[float]], total: int,
+                  step: int) -> Tuple[List[int], List[List[float]]]:
+    r, h = cek.initial_split(int(devices), bool(smooth), history, int(total), int(step))
+    return list(r), [list(x) for x in h]
+
+
+def empty_history(devices: int) -> List[List[float]]:
+    return [[0.0] * devices for _ in range(HISTORY_DEPTH)]
+
+
+def _trunc(x: float) -> int:
+    return int(math.trunc(x))
+
+
+def load_balance_py(bench, smooth, history, total, ranges, step):
+    """Pure-Python transcription of HelperFunctions.loadBalance."""
+    n = len(ranges)
+    ranges = list(ranges)
+    history = [list(h) for h in history]
+    total_bench = sum(bench) + 0.01 * n
+    thr = [(total_bench / (bench[i] + 0.01)) * (ranges[i] + 1) for i in range(n)]
+    total_thr = sum(thr)
+    if total_thr <= 0.0000001:
+        total_thr = 0.01
+    norm = [0.0] * n
+    if smooth:
+        norm = [t / total_thr for t in thr]
+        history = history[1:] + [norm]
+        norm = [sum(h[i] for h in history) / len(history) for i in range(n)]
+    tmp = [0] * n
+    for i in range(n):
+        p = norm[i] if (smooth and history[0][0] > 0.00001) else thr[i] / total_thr
+        if ranges[i] != 0:
+            tmp[i] = ranges[i] - _trunc((ranges[i] - total * p) * 0.3)
+        else:
+            tmp[i] = _trunc(total * (total_bench / (bench[i] + 0.01)) / total_thr)
+    for i in range(n):
+        rem = int(math.fmod(tmp[i], step))
+        ranges[i] = tmp[i] - rem if rem < step // 2 else tmp[i] + (step - rem)
+    while sum(ranges) > total:
+        ranges[ranges.index(max(ranges))] -= step
+    while sum(ranges) < total:
+        ranges[ranges.index(max(ranges))] += step
+    return ranges, history
+
+
+def convergence_iters(shares: Sequence[float], tol: float = 0.05) -> int:
+    """1-based index of the first call after which every later share stays
+    within ``tol`` (relative) of the final (steady-state) share."""
+    steady = shares[-1]
+    for i in range(len(shares)):
+        if all(abs(s - steady) <= tol * abs(steady) for s in shares[i:]):
+            return i + 1
+    return len(shares)
+
+
+def simulate(speeds: Sequence[float], total: int, step: int, calls: int = 30, smooth: bool = True):
+    """Run the native law against devices with fixed throughputs (items/ms);
+    returns the list of range vectors per call.  Used to measure convergence
+    without hardware noise."""
+    d = len(speeds)
+    hist = empty_history(d)
+    ranges, hist = initial_split(d, smooth, hist, total, step)
+    out = [list(ranges)]
+    for _ in range(calls - 1):
+        bench = [r / s for r, s in zip(ranges, speeds)]
+        ranges, hist = load_balance(bench, smooth, hist, total, ranges, step)
+        out.append(list(ranges))
+    return out
+
+
+# --------------------------------------------------------------------- cluster
+
+
+def _gcd(a: int, b: int) -> int:
+    return math.gcd(a, b) or 64
+
+
+def lcm(values: Sequence[int]) -> int:
+    return reduce(lambda a, b: a // _gcd(a, b) * b, values)
+
+
+class ClusterLoadBalancer:
+    """Node-level balancer (reference ClusterLoadBalancer)."""
+
+    def equal_split(self, total: int, steps: Sequence[int]) -> Tuple[List[int], int]:
+        """Returns (per-node ranges, remainder for the mainframe)."""
+        n = len(steps)
+        l = lcm(list(steps))
+        layers = (total // l) // n
+        if layers == 0:
+            ranges = list(steps)
+            return ranges, total - sum(ranges)
+        ranges = [layers * l] * n
+        left = total - layers * l * n
+        extra = left // l
+        for i in range(extra):
+            ranges[i] += l
+        left -= extra * l
+        return ranges, left
+
+    @staticmethod
+    def _nearest(d: float, a: int, m: int) -> int:
+        tmp = int(d * m)
+        k = tmp // a
+        if tmp - k * a >= a // 2:
+            k += 1
+        return max(1, k) * a
+
+    def balance(self, ms: Sequence[float], total: int, ranges: Sequence[int], steps: Sequence[int],
+                mainframe_items: int = 0) -> Tuple[List[int], int]:
+        n = len(ranges)
+        ms = [max(abs(t), 0.0001) for t in ms]
+        perf = [ranges[i] / ms[i] for i in range(n)]
+        tp = sum(perf) or 0.001
+        if total - mainframe_items == 0:
+            mainframe_items = 0
+        out = []
+        for i in range(n):
+            p = perf[i] / tp
+            t = ranges[i] / float(total - mainframe_items)
+            out.append(self._nearest(t + 0.3 * (p - t), steps[i], total))
+        s = sum(out)
+        if s <= total:
+            return out, total - s
+        excess = s - total
+        for i in range(n):
+            k = max(1, excess // steps[i])
+            if steps[i] * k < excess:
+                k += 1
+            cut = steps[i] * k
+            if out[i] - cut > 0:
+                out[i] -= cut
+                return out, cut - excess
+        return out, 0

@@ -1,0 +1,79 @@
+"""Load-balancer law: native vs an independent Python transcription of
+HelperFunctions.loadBalance (reference HelperFunctions.cs:190-280), plus the
+properties the reference documents (sum preserved, multiples of step, 0.3
+damping, smoothing active once 10 calls of history exist)."""
+import random
+
+import pytest
+from hypothesis import given, settings, strategies as st
+
+from cekirdekler_amd.parallel import balancer as B
+
+
+@settings(max_examples=200, deadline=None)
+@given(n=st.integers(1, 8), steps_mult=st.integers(1, 64), step=st.sampled_from([64, 256, 1024]),
+       smooth=st.booleans(), seed=st.integers(0, 10**6))
+def test_native_matches_python_transcription(n, steps_mult, step, smooth, seed):
+    rnd = random.Random(seed)
+    total = step * n * steps_mult
+    hist = B.empty_history(n)
+    r_nat, h_nat = B.initial_split(n, smooth, hist, total, step)
+    r_py, h_py = B.load_balance_py([10.0] * n, smooth, hist, total,
+                                   [total // n + (total - (total // n) * n if i == 0 else 0) for i in range(n)], step)
+    assert r_nat == r_py
+    for _ in range(12):
+        bench = [rnd.uniform(0.0, 50.0) for _ in range(n)]
+        r_nat2, h_nat = B.load_balance(bench, smooth, h_nat, total, r_nat, step)
+        r_py2, h_py = B.load_balance_py(bench, smooth, h_py, total, r_py, step)
+        assert r_nat2 == r_py2
+        for a, b in zip(h_nat, h_py):
+            assert a == pytest.approx(b)
+        r_nat, r_py = r_nat2, r_py2
+        assert sum(r_nat) == total
+        assert all(r % step == 0 for r in r_nat)
+
+
+def test_initial_split_remainder_to_device_zero():
+    r, _ = B.initial_split(3, False, B.empty_history(3), 10 * 256, 256)
+    assert sum(r) == 2560
+    assert all(x % 256 == 0 for x in r)
+
+
+def test_damping_closes_30_percent_of_gap():
+    # 2 devices, device 1 twice as slow: fair share of device 0 is 2/3
+    total, step = 3 * 1024 * 64, 64
+    seq = B.simulate([2.0, 1.0], total, step, calls=40, smooth=False)
+    share = [r[0] / total for r in seq]
+    gaps = [abs(2 / 3 - s) for s in share]
+    # residual shrinks by ~0.7 per call while far from the step quantum
+    for k in range(1, 6):
+        assert gaps[k] <= gaps[k - 1] * 0.75 + step / total
+    assert abs(share[-1] - 2 / 3) < 0.01
+
+
+def test_convergence_iters_2to1_within_budget():
+    total, step = 8 * 1024 * 256, 256
+    seq = B.simulate([2.0, 1.0], total, step, calls=40, smooth=False)
+    shares = [r[0] / total for r in seq]
+    assert B.convergence_iters(shares, 0.05) <= 10  # ≤10 computes, law-identical
+
+
+def test_smoothing_uses_history_only_when_full():
+    n, total, step = 2, 4096, 64
+    hist = B.empty_history(n)
+    r, hist = B.initial_split(n, True, hist, total, step)
+    # first 9 calls: oldest slot still zero -> raw shares used
+    for k in range(9):
+        assert hist[0][0] == 0.0
+        r, hist = B.load_balance([1.0, 3.0], True, hist, total, r, step)
+    assert hist[0][0] > 0
+
+
+def test_cluster_equal_split_and_balance():
+    cb = B.ClusterLoadBalancer()
+    ranges, rem = cb.equal_split(10 * 768, [256, 768])
+    assert sum(ranges) + rem == 10 * 768
+    assert ranges[0] % 768 == 0 and ranges[1] % 768 == 0
+    new, rem2 = cb.balance([10.0, 5.0], 10 * 768, ranges, [256, 768])
+    assert sum(new) + rem2 == 10 * 768
+    assert new[1] > ranges[1]  # faster node gains work

@@ -1,0 +1,154 @@
+"""compute() on the CPU device (the reference's de-facto fake backend,
+SURVEY §4): flag semantics, logical multi-device splits, pipelines, repeats,
+enqueue mode, barrier kernels (fibers) and the usage-type-2 Cores API.  The
+SAXPY 1M config of BASELINE.json must match numpy bit-for-bit."""
+import numpy as np
+import pytest
+
+import cekirdekler_amd as ck
+
+SRC = """
+__global__ void saxpy(const float* a, const float* x, float* y) {
+  long long i = get_global_id(0);
+  y[i] = a[0] * x[i] + y[i];
+}
+__global__ void copy2(const float* src, float* dst) {
+  long long i = get_global_id(0);
+  dst[2 * i] = src[2 * i];
+  dst[2 * i + 1] = src[2 * i + 1];
+}
+__global__ void inc(float* x) { x[get_global_id(0)] += 1.0f; }
+__global__ void count(float* x, int* c) { if (get_global_id(0) == 0) c[0] += 1; }
+__global__ void groupsum(const float* x, float* out) {
+  __shared__ float s[64];
+  int l = (int)get_local_id(0);
+  s[l] = x[get_global_id(0)];
+  __syncthreads();
+  for (int w = 32; w > 0; w >>= 1) { if (l < w) s[l] += s[l + w]; __syncthreads(); }
+  if (l == 0) out[get_global_id(0) / 64] = s[0];
+}
+"""
+
+
+@pytest.fixture(scope="module")
+def cpu():
+    return ck.ClPlatforms.all().cpus(True)
+
+
+@pytest.fixture(scope="module")
+def cr(cpu):
+    c = ck.ClNumberCruncher(cpu, SRC)
+    assert c.error_code() == 0, c.error_message()
+    return c
+
+
+def test_saxpy_1m_bit_exact(cr):
+    n = 1 << 20
+    a = ck.ClArray(np.array([1.7], np.float32))
+    a.write = False
+    x = ck.ClArray(np.random.rand(n).astype(np.float32))
+    y0 = np.random.rand(n).astype(np.float32)
+    y = ck.ClArray(y0.copy())
+    a.next_param(x, y).compute(cr, 1, "saxpy", n, 256)
+    np.testing.assert_array_equal(y.array, np.float32(1.7) * x.array + y0)
+
+
+def test_elements_per_work_item_and_partial(cpu):
+    devs = cpu + cpu + cpu
+    cr = ck.ClNumberCruncher(devs, SRC)
+    n = 3 * 64 * 16
+    src = ck.ClArray(np.arange(2 * n, dtype=np.float32))
+    dst = ck.ClArray(np.zeros(2 * n, np.float32))
+    src.partial_read = True
+    src.elements_per_work_item = 2
+    dst.elements_per_work_item = 2
+    dst.read = False
+    for _ in range(3):
+        src.next_param(dst).compute(cr, 2, "copy2", n, 64)
+    np.testing.assert_array_equal(dst.array, src.array)
+    r = cr.ranges(2)
+    assert len(r) == 3 and sum(r) == n and all(x % 64 == 0 for x in r)
+
+
+@pytest.mark.parametrize("ptype", [ck.PIPELINE_EVENT, ck.PIPELINE_DRIVER])
+def test_pipelines_on_cpu(cpu, ptype):
+    cr = ck.ClNumberCruncher(cpu + cpu, SRC)
+    n = 2 * 256 * 8 * 4
+    x = ck.ClArray(np.zeros(n, np.float32))
+    x.partial_read = True
+    for k in range(3):
+        x.compute(cr, 3, "inc", n, 256, 0, True, ptype, 8)
+    np.testing.assert_array_equal(x.array, 3.0)
+    assert cr.last_record()["pipelined"]
+
+
+def test_repeat_with_sync_kernel(cr):
+    x = ck.ClArray(np.zeros(1024, np.float32))
+    c = ck.ClArray(np.zeros(1, np.int32))
+    c.write_all = True
+    cr.repeat_count = 5
+    cr.repeat_kernel_name = "count"
+    try:
+        x.next_param(c).compute(cr, 4, "inc", 1024, 64)
+    finally:
+        cr.repeat_count = 1
+        cr.repeat_kernel_name = ""
+    np.testing.assert_array_equal(x.array, 5.0)
+    assert c.array[0] == 5  # sync kernel (global=local, offset 0) runs after each repeat
+
+
+def test_barrier_kernel_uses_fibers(cr):
+    n = 64 * 32
+    x = ck.ClArray(np.random.rand(n).astype(np.float32))
+    out = ck.ClArray(np.zeros(n // 64, np.float32))
+    out.elements_per_work_item = 1
+    out.write_all = True
+    x.next_param(out).compute(cr, 5, "groupsum", n, 64)
+    np.testing.assert_allclose(out.array, x.array.reshape(-1, 64).sum(1), rtol=1e-5)
+
+
+def test_validation_errors(cr):
+    x = ck.ClArray(np.zeros(100, np.float32))
+    with pytest.raises(ck.ClComputeError):
+        x.compute(cr, 6, "inc", 100, 64)        # not a multiple of local
+    with pytest.raises(ck.ClComputeError):
+        x.compute(cr, 6, "inc", 128, 64)        # array shorter than G*epw
+    assert cr.number_of_errors_happened >= 2
+
+
+def test_enqueue_mode_and_markers(cr):
+    x = ck.ClArray(np.zeros(4096, np.float32))
+    cr.fine_grained_queue_control = True
+    cr.enqueue_mode = True
+    for _ in range(10):
+        x.compute(cr, 8, "inc", 4096, 256)
+    cr.enqueue_mode = False
+    cr.fine_grained_queue_control = False
+    np.testing.assert_array_equal(x.array, 10.0)
+    assert cr.count_markers_reached() >= 10
+    assert cr.count_markers_remaining() == 0
+
+
+def test_usage_type_2_cores_api():
+    cores = ck.Cores("cpu", SRC, local_range=64)
+    n = 1024
+    a = np.array([2.0], np.float32)
+    x = np.arange(n, dtype=np.float32)
+    y = np.ones(n, np.float32)
+    cores.compute("saxpy", 1, "", [a, x, y], [" read ", " partial read ", " partial read write "], [1, 1, 1],
+                  n, 1)
+    np.testing.assert_array_equal(y, 2 * x + 1)
+    rep = cores.performance_report(1)
+    assert "Compute-ID: 1" in rep and "workitems" in rep
+
+
+def test_load_balancer_with_injected_imbalance(cpu):
+    cr = ck.ClNumberCruncher(cpu + cpu, SRC)
+    cr.set_time_scale(1, 3.0)
+    n = 1 << 16
+    x = ck.ClArray(np.zeros(n, np.float32))
+    for _ in range(25):
+        x.compute(cr, 9, "inc", n, 256)
+    r = cr.ranges(9)
+    assert r[0] > r[1] * 1.5
+    assert cr.normalized_global_ranges_of_devices(9)[0] > 0.55

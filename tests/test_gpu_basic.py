@@ -99,6 +99,7 @@ def test_reduce_sum():
     groups = n // (256 * 8)
     part = ck.ClArray(groups, np.float32)
     part.read = False
+    part.elements_per_group = 1
     G = n // 8
     x.next_param(part).compute(cr, 1, "cek_reduce_sum_f32", G, 256)
     np.testing.assert_allclose(part.array.sum(), x.array.astype(np.float64).sum(), rtol=1e-5)
