@@ -124,7 +124,10 @@ def bench_lb_iters():
     plats = ck.ClPlatforms.all()
     gpus = plats.gpus()
     devs = (gpus[0] + gpus[0]) if len(gpus) else (plats.cpus(True) + plats.cpus(True))
-    src = "__global__ void k(float* x){ long long i = get_global_id(0); x[i] = x[i] * 1.0001f + 1.0f; }"
+    # compute-heavy kernel so a device's time is proportional to its range
+    # (fixed launch/sync overheads would otherwise bias the steady state)
+    src = """__global__ void k(float* x){ long long i = get_global_id(0); float v = x[i];
+        for (int j = 0; j < 2048; ++j) v = v * 0.999f + 1.0f; x[i] = v; }"""
     cr = ck.ClNumberCruncher(devs, src)
     cr.set_time_scale(1, 2.0)
     n = 1 << 22

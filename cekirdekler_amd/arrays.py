@@ -478,13 +478,22 @@ class ClArray:
 
     # ------------------------------------------------------------ native spec
     def _spec(self):
+        # The native spec is cached per (storage uid, flags): the uid changes
+        # whenever the host storage does, so the pointer inside stays valid.
+        key = (self._uid, self._read, self._partial, self._write, self._write_all, self._ro, self._wo,
+               self.zero_copy, self.elements_per_work_item, self.elements_per_group)
+        cached = getattr(self, "_spec_cache", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
         arr = self.array
         if self.zero_copy and self._fast is None and not self._registered:
             self._registered = bool(cek.host_register(arr.ctypes.data, arr.nbytes))
-        return cek.ArraySpec(self._uid, arr.ctypes.data, arr.nbytes, arr.itemsize,
+        spec = cek.ArraySpec(self._uid, arr.ctypes.data, arr.nbytes, arr.itemsize,
                              self._read, self._partial, self._write, self._write_all,
                              self._ro, self._wo, bool(self.zero_copy), int(self.elements_per_work_item),
                              int(self.elements_per_group))
+        self._spec_cache = (key, spec)
+        return spec
 
     @property
     def uid(self) -> int:

@@ -25,13 +25,13 @@
 
 namespace {
 
-template <int WN>
+template <int WM, int WN, int FM, int FN, bool PIPE>
 __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
                                           const uint16_t* __restrict__ A,
                                           const uint16_t* __restrict__ Bt, float* __restrict__ C,
                                           char* smem, long long off) {
-  constexpr int BM = 256, BN = 64 * WN, BK = 64;
-  constexpr int NWAVES = 2 * WN, NT = 64 * NWAVES;
+  constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN, BK = 64;
+  constexpr int NWAVES = WM * WN, NT = 64 * NWAVES;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int A_INSTR = A_BYTES / 1024 / NWAVES;
   constexpr int B_INSTR = B_BYTES / 1024 / NWAVES;
@@ -82,67 +82,108 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int pc = (s * 4 + fq) ^ (lane & 7);
-    a_off[s] = (wr * 128 + fr) * 128 + pc * 16;
-    b_off[s] = A_BYTES + (wc * 64 + fr) * 128 + pc * 16;
+    a_off[s] = (wr * 16 * FM + fr) * 128 + pc * 16;
+    b_off[s] = A_BYTES + (wc * 16 * FN + fr) * 128 + pc * 16;
   }
 
-  f32x4 acc[8][4];
+  f32x4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / BK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
-    const char* base = smem + cur * STAGE;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 a[8], b[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
+  if constexpr (!PIPE) {
+    stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+      const char* base = smem + cur * STAGE;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 a[FM], b[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) b[j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) a[i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    // Register double-buffered fragments: k-step 1 of the current K-tile is
+    // read from LDS while k-step 0's MFMAs run, and k-step 0 of the next
+    // K-tile is read (right after the barrier that publishes its DMA) while
+    // k-step 1's MFMAs run — LDS latency hides under MFMA issue.
+    bf16x8 xa[FM], xb[FN], ya[FM], yb[FN];
+    auto ld = [&](bf16x8(&a)[FM], bf16x8(&b)[FN], const char* base, int s) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
+    };
+    auto mma = [&](const bf16x8(&a)[FM], const bf16x8(&b)[FN]) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    ld(xa, xb, smem, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      const char* base = smem + cur * STAGE;
+      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+      ld(ya, yb, base, 1);
+      mma(xa, xb);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kt + 1 < nk) ld(xa, xb, smem + (cur ^ 1) * STAGE, 0);
+      mma(ya, yb);
+    }
   }
 
-  // Epilogue: acc[i][j][r] is C(row = wr·128 + i·16 + fq·4 + r, col = wc·64 + j·16 + fr)
+  // Epilogue: acc[i][j][r] is C(row = wr·16FM + i·16 + fq·4 + r, col = wc·16FN + j·16 + fr)
   float* ct = C + (size_t)t * BM * BN;
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        ct[(size_t)(wr * 128 + i * 16 + fq * 4 + r) * BN + wc * 64 + j * 16 + fr] = acc[i][j][r];
+        ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr] = acc[i][j][r];
 }
 
 }  // namespace
 
-// 256×256 tiles, 512 threads (8 waves), 128 KiB LDS.
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * (256 * 64 * 2 + 256 * 64 * 2)];
-  gemm_tile<4>(dims, A, Bt, C, smem, __cek_off);
-}
+#define CEK_GEMM_KERNEL(NAME, WM, WN, FM, FN, PIPE)                                              \
+  extern "C" __global__ __launch_bounds__(64 * WM * WN) void NAME(                                \
+      const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {              \
+    __shared__ __attribute__((aligned(16))) char smem[2 * (WM * 16 * FM + WN * 16 * FN) * 64 * 2]; \
+    gemm_tile<WM, WN, FM, FN, PIPE>(dims, A, Bt, C, smem, __cek_off);                              \
+  }
 
-// 256×128 tiles, 256 threads (4 waves), 96 KiB LDS — twice the tiles, for
-// strongly scaled slices (8 GPUs × 1024 rows of an 8192² problem).
-extern "C" __global__ __launch_bounds__(256) void cek_sgemm_bf16_256x128(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * (256 * 64 * 2 + 128 * 64 * 2)];
-  gemm_tile<2>(dims, A, Bt, C, smem, __cek_off);
-}
+// 256×256 tiles, 8 waves (2×4, 128×64 each), 128 KiB LDS, 1 block/CU.
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256, 2, 4, 8, 4, false)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256p, 2, 4, 8, 4, true)
+// 256×128 tiles, 8 waves (4×2, 64×64 each), 96 KiB LDS — twice the tiles
+// for strongly scaled slices (8 GPUs × 1024 rows of an 8192² problem).
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128, 4, 2, 4, 4, false)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128p, 4, 2, 4, 4, true)
+// 128×128 tiles, 4 waves (2×2, 64×64 each), 64 KiB LDS, 2 blocks/CU.
+CEK_GEMM_KERNEL(cek_sgemm_bf16_128x128, 2, 2, 4, 4, false)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_128x128p, 2, 2, 4, 4, true)

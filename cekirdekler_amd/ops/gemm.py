@@ -19,8 +19,16 @@ from ..arrays import ClArray
 from ..cruncher import ClNumberCruncher
 from .library import library
 
-TILES = {"256x256": (256, 256, 512, "cek_sgemm_bf16_256x256"),
-         "256x128": (256, 128, 256, "cek_sgemm_bf16_256x128")}
+# tile name -> (BM, BN, work-group size, kernel); "p" = register
+# double-buffered fragment pipeline
+TILES = {
+    "256x256": (256, 256, 512, "cek_sgemm_bf16_256x256"),
+    "256x256p": (256, 256, 512, "cek_sgemm_bf16_256x256p"),
+    "256x128": (256, 128, 512, "cek_sgemm_bf16_256x128"),
+    "256x128p": (256, 128, 512, "cek_sgemm_bf16_256x128p"),
+    "128x128": (128, 128, 256, "cek_sgemm_bf16_128x128"),
+    "128x128p": (128, 128, 256, "cek_sgemm_bf16_128x128p"),
+}
 
 
 def to_bf16_bits(x: np.ndarray) -> np.ndarray:

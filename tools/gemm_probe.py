@@ -9,20 +9,24 @@ from cekirdekler_amd.ops.gemm import GemmBf16
 res = {}
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 g0 = ck.ClPlatforms.all().gpus()[0]
-for tile in ["256x256", "256x128"]:
-    g = GemmBf16(n, n, n, devices=g0, tile=tile)
+shapes = [(n, n, n)] + ([(n // 8, n, n)] if n >= 4096 else [])
+from cekirdekler_amd.ops.gemm import TILES
+for (M, N, K), tile in [(s, t) for s in shapes for t in TILES]:
+    g = GemmBf16(M, N, K, devices=g0, tile=tile)
     for _ in range(3): g.run(resident=True)
     torch.cuda.synchronize()
-    t = time.perf_counter(); K = 20
-    for _ in range(K): g.run(resident=True)
+    t = time.perf_counter(); REPS = 20
+    for _ in range(REPS): g.run(resident=True)
     torch.cuda.synchronize()
-    ms = (time.perf_counter() - t) * 1e3 / K
-    res[tile] = {"ms": ms, "tflops": g.flops / ms / 1e9, "dev_ms": g.cr.benchmarks(1)}
+    ms = (time.perf_counter() - t) * 1e3 / REPS
+    key = f"{M}x{N}x{K}/{tile}"
+    res[key] = {"ms": ms, "tflops": g.flops / ms / 1e9, "dev_ms": g.cr.benchmarks(1)}
     if n <= 8192:
         rows = slice(0, 256)
         c = g.result(download=True)[rows]
         ref = g.reference(rows)
-        res[tile]["max_err"] = float(np.abs(c - ref).max())
+        res[key]["max_err"] = float(np.abs(c - ref).max())
+    g.cr.dispose()
 a = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
 b = torch.randn(n, n, device="cuda", dtype=torch.bfloat16)
 for _ in range(3): torch.matmul(a, b.t())
