@@ -25,7 +25,7 @@
 
 namespace {
 
-template <int WM, int WN, int FM, int FN, bool PIPE>
+template <int WM, int WN, int FM, int FN, int MODE>
 __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
                                           const uint16_t* __restrict__ A,
                                           const uint16_t* __restrict__ Bt, float* __restrict__ C,
@@ -33,8 +33,15 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN, BK = 64;
   constexpr int NWAVES = WM * WN, NT = 64 * NWAVES;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int A_INSTR = A_BYTES / 1024 / NWAVES;
-  constexpr int B_INSTR = B_BYTES / 1024 / NWAVES;
+  // MODE 0: one LDS stage in flight, all waves stage; MODE 1: + register
+  // double-buffered fragments; MODE 2: ping-pong — the two halves of the
+  // work-group (waves < NWAVES/2 = G0, the rest = G1, one of each per SIMD)
+  // alternate between an LDS-read section and an MFMA section, one
+  // s_barrier apart, so each SIMD's matrix pipe always has one wave issuing;
+  // G0 also issues all LDS-DMA staging.
+  constexpr int STAGERS = MODE == 2 ? NWAVES / 2 : NWAVES;
+  constexpr int A_INSTR = A_BYTES / 1024 / STAGERS;
+  constexpr int B_INSTR = B_BYTES / 1024 / STAGERS;
 
   const int N = dims[1], K = dims[2];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -48,30 +55,22 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   // Staging: instruction `ins` of this wave fills LDS bytes [ins·1 KiB, +1 KiB)
   // = 8 rows × 128 B; lane l lands at row ins·8 + l/8, physical chunk l%8,
   // which holds logical chunk (l%8) ^ (row & 7).
-  const uint16_t* a_src[A_INSTR];
-  const uint16_t* b_src[B_INSTR];
-#pragma unroll
-  for (int j = 0; j < A_INSTR; ++j) {
-    const int ins = wave * A_INSTR + j, row = ins * 8 + (lane >> 3);
-    const int lc = (lane & 7) ^ (row & 7);
-    a_src[j] = A + (size_t)(m0 + row) * K + lc * 8;
-  }
-#pragma unroll
-  for (int j = 0; j < B_INSTR; ++j) {
-    const int ins = wave * B_INSTR + j, row = ins * 8 + (lane >> 3);
-    const int lc = (lane & 7) ^ (row & 7);
-    b_src[j] = Bt + (size_t)(n0 + row) * K + lc * 8;
-  }
+  // Within one wave-instruction the 8 rows are ins·8 .. ins·8+7, so the
+  // logical chunk (l%8) ^ (row&7) = (l%8) ^ (l/8) is the same for every
+  // instruction: one per-lane base pointer plus a uniform row stride.
+  const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
+  const uint16_t* a_base = A + (size_t)(m0 + wave * A_INSTR * 8 + lrow) * K + lchunk * 8;
+  const uint16_t* b_base = Bt + (size_t)(n0 + wave * B_INSTR * 8 + lrow) * K + lchunk * 8;
 
   auto stage = [&](int buf, int kt) {
     char* base = smem + buf * STAGE;
 #pragma unroll
     for (int j = 0; j < A_INSTR; ++j)
-      __builtin_amdgcn_global_load_lds((glb_cvoid*)(a_src[j] + (size_t)kt * BK),
+      __builtin_amdgcn_global_load_lds((glb_cvoid*)(a_base + (size_t)j * 8 * K + (size_t)kt * BK),
                                        (lds_void*)(base + (wave * A_INSTR + j) * 1024), 16, 0, 0);
 #pragma unroll
     for (int j = 0; j < B_INSTR; ++j)
-      __builtin_amdgcn_global_load_lds((glb_cvoid*)(b_src[j] + (size_t)kt * BK),
+      __builtin_amdgcn_global_load_lds((glb_cvoid*)(b_base + (size_t)j * 8 * K + (size_t)kt * BK),
                                        (lds_void*)(base + A_BYTES + (wave * B_INSTR + j) * 1024), 16, 0, 0);
   };
 
@@ -93,7 +92,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / BK;
-  if constexpr (!PIPE) {
+  if constexpr (MODE == 0) {
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -119,7 +118,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
-  } else {
+  } else if constexpr (MODE == 1) {
     // Register double-buffered fragments: k-step 1 of the current K-tile is
     // read from LDS while k-step 0's MFMAs run, and k-step 0 of the next
     // K-tile is read (right after the barrier that publishes its DMA) while
@@ -155,6 +154,56 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       if (kt + 1 < nk) ld(xa, xb, smem + (cur ^ 1) * STAGE, 0);
       mma(ya, yb);
     }
+  } else {
+    // Ping-pong.  Interval n (between two block barriers): one group runs its
+    // 4·FM·FN MFMAs of K-tile k while the other reads K-tile k(+1)'s
+    // fragments.  G0 stages K-tile k+1 into the free LDS buffer during its
+    // read section of K-tile k and retires it (vmcnt(0)) at the end of its
+    // MFMA section, one barrier before anyone reads it; every read section
+    // ends with lgkmcnt(0) before its barrier, so a buffer is never
+    // restaged while still being read.
+    const bool g1 = wave >= NWAVES / 2;
+    bf16x8 fa[2][FM], fb[2][FN];
+    auto ldall = [&](const char* base) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[s][j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[s][i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
+      }
+    };
+    auto mmaall = [&]() {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][i], fb[s][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    auto bar = [] {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    if (!g1) stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (g1) bar();  // stagger G1 by one section
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* base = smem + (kt & 1) * STAGE;
+      if (!g1 && kt + 1 < nk) stage((kt + 1) & 1, kt + 1);
+      ldall(base);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bar();
+      mmaall();
+      if (!g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+    }
+    if (!g1) bar();  // equal barrier counts for both groups
   }
 
   // Epilogue: acc[i][j][r] is C(row = wr·16FM + i·16 + fq·4 + r, col = wc·16FN + j·16 + fr)
@@ -170,20 +219,22 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 
 }  // namespace
 
-#define CEK_GEMM_KERNEL(NAME, WM, WN, FM, FN, PIPE)                                              \
+#define CEK_GEMM_KERNEL(NAME, WM, WN, FM, FN, MODE)                                              \
   extern "C" __global__ __launch_bounds__(64 * WM * WN) void NAME(                                \
       const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {              \
     __shared__ __attribute__((aligned(16))) char smem[2 * (WM * 16 * FM + WN * 16 * FN) * 64 * 2]; \
-    gemm_tile<WM, WN, FM, FN, PIPE>(dims, A, Bt, C, smem, __cek_off);                              \
+    gemm_tile<WM, WN, FM, FN, MODE>(dims, A, Bt, C, smem, __cek_off);                              \
   }
 
 // 256×256 tiles, 8 waves (2×4, 128×64 each), 128 KiB LDS, 1 block/CU.
-CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256, 2, 4, 8, 4, false)
-CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256p, 2, 4, 8, 4, true)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256, 2, 4, 8, 4, 0)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256p, 2, 4, 8, 4, 1)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256pp, 2, 4, 8, 4, 2)
 // 256×128 tiles, 8 waves (4×2, 64×64 each), 96 KiB LDS — twice the tiles
 // for strongly scaled slices (8 GPUs × 1024 rows of an 8192² problem).
-CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128, 4, 2, 4, 4, false)
-CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128p, 4, 2, 4, 4, true)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128, 4, 2, 4, 4, 0)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128p, 4, 2, 4, 4, 1)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128pp, 4, 2, 4, 4, 2)
 // 128×128 tiles, 4 waves (2×2, 64×64 each), 64 KiB LDS, 2 blocks/CU.
-CEK_GEMM_KERNEL(cek_sgemm_bf16_128x128, 2, 2, 4, 4, false)
-CEK_GEMM_KERNEL(cek_sgemm_bf16_128x128p, 2, 2, 4, 4, true)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_128x128, 2, 2, 4, 4, 0)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_128x128p, 2, 2, 4, 4, 1)

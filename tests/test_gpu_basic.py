@@ -54,7 +54,8 @@ def test_logical_devices_pipelines(pipeline, ptype):
     assert sum(cr.ranges(5)) == n
 
 
-@pytest.mark.parametrize("tile", ["256x256", "256x256p", "256x128", "256x128p", "128x128", "128x128p"])
+@pytest.mark.parametrize("tile", ["256x256", "256x256p", "256x256pp", "256x128", "256x128p", "256x128pp",
+                                  "128x128", "128x128p"])
 def test_gemm_bf16_matches_fp64(tile):
     from cekirdekler_amd.ops.gemm import GemmBf16
 
