@@ -8,7 +8,7 @@
 //   contiguous byte range (the reference's partial write of
 //   [ref·e, (ref+r)·e), Worker.cs:1349-1352, with e = BM·BN / local).
 //
-// Work decomposition for compute(): one work-group (local = 128·WN threads)
+// Work decomposition for compute(): one work-group (local = 64·WM·WN threads)
 // per BM×BN tile, global range = tiles × local.  The work-group's absolute
 // tile is its XCD-remapped local block id + __cek_off / local.
 //
@@ -43,13 +43,20 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   constexpr int A_INSTR = A_BYTES / 1024 / STAGERS;
   constexpr int B_INSTR = B_BYTES / 1024 / STAGERS;
 
-  const int N = dims[1], K = dims[2];
+  const int M = dims[0], N = dims[1], K = dims[2], GM = dims[3] > 0 ? dims[3] : 1;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave / WN, wc = wave % WN;
   const long long t = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
-  const int ntn = N / BN;
-  const int tm = (int)(t / ntn), tn = (int)(t % ntn);
+  // Grouped tile order (dims[3] = GM row panels per group, tiles walk down
+  // the group's rows first): the 32 work-groups an XCD runs at once cover a
+  // GM × (32/GM) block of C, so A and B K-slices are shared through that
+  // XCD's L2 instead of re-fetched per tile.  C storage stays tile-major by
+  // t, so a device's contiguous tile range is still one contiguous slice.
+  const int ntn = N / BN, ntm = M / BM;
+  const int per_group = GM * ntn, grp = (int)(t / per_group), first = grp * GM;
+  const int gsz = min(ntm - first, GM), in_g = (int)(t % per_group);
+  const int tm = first + in_g % gsz, tn = in_g / gsz;
   const int m0 = tm * BM, n0 = tn * BN;
 
   // Staging: instruction `ins` of this wave fills LDS bytes [ins·1 KiB, +1 KiB)

@@ -44,14 +44,31 @@ def from_bf16_bits(b: np.ndarray) -> np.ndarray:
     return (b.astype(np.uint32) << 16).view(np.float32)
 
 
-def untile(c: np.ndarray, M: int, N: int, BM: int, BN: int) -> np.ndarray:
-    """Tile-major C → row-major [M][N]."""
-    return c.reshape(M // BM, N // BN, BM, BN).transpose(0, 2, 1, 3).reshape(M, N)
+def tile_coords(t: np.ndarray, M: int, N: int, BM: int, BN: int, group_m: int):
+    """Tile index → (tile row, tile col) under the kernel's grouped order."""
+    ntm, ntn = M // BM, N // BN
+    gm = max(1, group_m)
+    per = gm * ntn
+    first = (t // per) * gm
+    gsz = np.minimum(ntm - first, gm)
+    in_g = t % per
+    return first + in_g % gsz, in_g // gsz
+
+
+def untile(c: np.ndarray, M: int, N: int, BM: int, BN: int, group_m: int = 1) -> np.ndarray:
+    """Tile-major C (grouped tile order) → row-major [M][N]."""
+    ntm, ntn = M // BM, N // BN
+    tiles = c.reshape(ntm * ntn, BM, BN)
+    tm, tn = tile_coords(np.arange(ntm * ntn), M, N, BM, BN, group_m)
+    out = np.empty((ntm, ntn, BM, BN), c.dtype)
+    out[tm, tn] = tiles
+    return out.transpose(0, 2, 1, 3).reshape(M, N)
 
 
 class GemmBf16:
     def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256",
-                 cruncher: ClNumberCruncher | None = None, fill: str = "random", seed: int = 0):
+                 cruncher: ClNumberCruncher | None = None, fill: str = "random", seed: int = 0,
+                 group_m: int = 4):
         BM, BN, L, kname = TILES[tile]
         if M % BM or N % BN or K % 64:
             raise ValueError(f"M%{BM}, N%{BN} and K%64 must be 0 (got {M},{N},{K})")
@@ -59,7 +76,8 @@ class GemmBf16:
         self.tiles = (M // BM) * (N // BN)
         self.global_range = self.tiles * L
         self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library("sgemm_bf16"))
-        self.dims = ClArray(np.array([M, N, K, 0], np.int32))
+        self.group_m = group_m
+        self.dims = ClArray(np.array([M, N, K, group_m], np.int32))
         self.dims.write = False
         self.A = ClArray(M * K, "bfloat16")
         self.B = ClArray(N * K, "bfloat16")
@@ -97,7 +115,7 @@ class GemmBf16:
                 g = self.cr._cores.global_base + dev
                 lo, n = refs[g] * e, rng[g] * e
                 self._download_slice(dev, lo, n)
-        return untile(self.C.array, self.M, self.N, self.BM, self.BN)
+        return untile(self.C.array, self.M, self.N, self.BM, self.BN, self.group_m)
 
     def _download_slice(self, dev: int, lo: int, n: int) -> None:
         # a sub-view ClArray sharing the same uid would alias buffers; the

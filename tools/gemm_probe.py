@@ -11,15 +11,17 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 g0 = ck.ClPlatforms.all().gpus()[0]
 shapes = [(n, n, n)] + ([(n // 8, n, n)] if n >= 4096 else [])
 from cekirdekler_amd.ops.gemm import TILES
-for (M, N, K), tile in [(s, t) for s in shapes for t in TILES]:
-    g = GemmBf16(M, N, K, devices=g0, tile=tile)
+tiles = sys.argv[2].split(",") if len(sys.argv) > 2 else list(TILES)
+groups = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 4, 8]
+for (M, N, K), tile, gm in [(s, t, g) for s in shapes for t in tiles for g in groups]:
+    g = GemmBf16(M, N, K, devices=g0, tile=tile, group_m=gm)
     for _ in range(3): g.run(resident=True)
     torch.cuda.synchronize()
     t = time.perf_counter(); REPS = 20
     for _ in range(REPS): g.run(resident=True)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t) * 1e3 / REPS
-    key = f"{M}x{N}x{K}/{tile}"
+    key = f"{M}x{N}x{K}/{tile}/g{gm}"
     res[key] = {"ms": ms, "tflops": g.flops / ms / 1e9, "dev_ms": g.cr.benchmarks(1)}
     if n <= 8192:
         rows = slice(0, 256)
