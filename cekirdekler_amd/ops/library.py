@@ -25,7 +25,9 @@ LIBRARY = {
 
 def code_object(name: str) -> str:
     path = os.path.join(kernel_dir(), name + ".hsaco")
-    if not os.path.exists(path):
+    src = os.path.join(kernel_dir(), name + ".hip")
+    stale = os.path.exists(src) and (not os.path.exists(path) or os.path.getmtime(src) > os.path.getmtime(path))
+    if stale:
         from .. import build_native
 
         build_native.build_kernels()
