@@ -66,19 +66,25 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   // logical chunk (l%8) ^ (row&7) = (l%8) ^ (l/8) is the same for every
   // instruction: one per-lane base pointer plus a uniform row stride.
   const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
-  const uint16_t* a_base = A + (size_t)(m0 + wave * A_INSTR * 8 + lrow) * K + lchunk * 8;
-  const uint16_t* b_base = Bt + (size_t)(n0 + wave * B_INSTR * 8 + lrow) * K + lchunk * 8;
+  // per-lane 32-bit byte offset + wave-uniform 64-bit base (saddr form)
+  const unsigned lane_off = (unsigned)(lrow * K + lchunk * 8) * 2u;
+  const char* a_wave = (const char*)(A + (size_t)(m0 + wave * A_INSTR * 8) * K);
+  const char* b_wave = (const char*)(Bt + (size_t)(n0 + wave * B_INSTR * 8) * K);
 
   auto stage = [&](int buf, int kt) {
     char* base = smem + buf * STAGE;
 #pragma unroll
-    for (int j = 0; j < A_INSTR; ++j)
-      __builtin_amdgcn_global_load_lds((glb_cvoid*)(a_base + (size_t)j * 8 * K + (size_t)kt * BK),
+    for (int j = 0; j < A_INSTR; ++j) {
+      const char* u = a_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 2;
+      __builtin_amdgcn_global_load_lds((glb_cvoid*)(u + lane_off),
                                        (lds_void*)(base + (wave * A_INSTR + j) * 1024), 16, 0, 0);
+    }
 #pragma unroll
-    for (int j = 0; j < B_INSTR; ++j)
-      __builtin_amdgcn_global_load_lds((glb_cvoid*)(b_base + (size_t)j * 8 * K + (size_t)kt * BK),
+    for (int j = 0; j < B_INSTR; ++j) {
+      const char* u = b_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 2;
+      __builtin_amdgcn_global_load_lds((glb_cvoid*)(u + lane_off),
                                        (lds_void*)(base + A_BYTES + (wave * B_INSTR + j) * 1024), 16, 0, 0);
+    }
   };
 
   // Fragment read offsets (bytes) inside a stage: row (wr·128 + i·16 + l%16),
