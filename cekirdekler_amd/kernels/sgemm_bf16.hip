@@ -38,8 +38,11 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   // work-group (waves < NWAVES/2 = G0, the rest = G1, one of each per SIMD)
   // alternate between an LDS-read section and an MFMA section, one
   // s_barrier apart, so each SIMD's matrix pipe always has one wave issuing;
-  // G0 also issues all LDS-DMA staging.
-  constexpr int STAGERS = MODE == 2 ? NWAVES / 2 : NWAVES;
+  // G0 also issues all LDS-DMA staging.  MODE 3: ping-pong with the DMA
+  // split — G0 stages the A tile during its read section, G1 stages the B
+  // tile of the K-tile after next at the start of its MFMA section, so each
+  // DMA has ~1.5 sections to land.
+  constexpr int STAGERS = MODE >= 2 ? NWAVES / 2 : NWAVES;
   constexpr int A_INSTR = A_BYTES / 1024 / STAGERS;
   constexpr int B_INSTR = B_BYTES / 1024 / STAGERS;
 
@@ -68,23 +71,31 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
   // per-lane 32-bit byte offset + wave-uniform 64-bit base (saddr form)
   const unsigned lane_off = (unsigned)(lrow * K + lchunk * 8) * 2u;
-  const char* a_wave = (const char*)(A + (size_t)(m0 + wave * A_INSTR * 8) * K);
-  const char* b_wave = (const char*)(Bt + (size_t)(n0 + wave * B_INSTR * 8) * K);
+  const int sw = MODE >= 2 ? wave % (NWAVES / 2) : wave;  // staging wave index
+  const char* a_wave = (const char*)(A + (size_t)(m0 + sw * A_INSTR * 8) * K);
+  const char* b_wave = (const char*)(Bt + (size_t)(n0 + sw * B_INSTR * 8) * K);
 
-  auto stage = [&](int buf, int kt) {
+  auto stage_a = [&](int buf, int kt) {
     char* base = smem + buf * STAGE;
 #pragma unroll
     for (int j = 0; j < A_INSTR; ++j) {
       const char* u = a_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 2;
       __builtin_amdgcn_global_load_lds((glb_cvoid*)(u + lane_off),
-                                       (lds_void*)(base + (wave * A_INSTR + j) * 1024), 16, 0, 0);
+                                       (lds_void*)(base + (sw * A_INSTR + j) * 1024), 16, 0, 0);
     }
+  };
+  auto stage_b = [&](int buf, int kt) {
+    char* base = smem + buf * STAGE + A_BYTES;
 #pragma unroll
     for (int j = 0; j < B_INSTR; ++j) {
       const char* u = b_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 2;
       __builtin_amdgcn_global_load_lds((glb_cvoid*)(u + lane_off),
-                                       (lds_void*)(base + A_BYTES + (wave * B_INSTR + j) * 1024), 16, 0, 0);
+                                       (lds_void*)(base + (sw * B_INSTR + j) * 1024), 16, 0, 0);
     }
+  };
+  auto stage = [&](int buf, int kt) {
+    stage_a(buf, kt);
+    stage_b(buf, kt);
   };
 
   // Fragment read offsets (bytes) inside a stage: row (wr·128 + i·16 + l%16),
@@ -167,7 +178,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       if (kt + 1 < nk) ld(xa, xb, smem + (cur ^ 1) * STAGE, 0);
       mma(ya, yb);
     }
-  } else {
+  } else if constexpr (MODE == 2) {
     // Ping-pong.  Interval n (between two block barriers): one group runs its
     // 4·FM·FN MFMAs of K-tile k while the other reads K-tile k(+1)'s
     // fragments.  G0 stages K-tile k+1 into the free LDS buffer during its
@@ -217,6 +228,57 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       bar();
     }
     if (!g1) bar();  // equal barrier counts for both groups
+  } else {
+    // Ping-pong with split DMA (see MODE comment above).
+    const bool g1 = wave >= NWAVES / 2;
+    bf16x8 fa[2][FM], fb[2][FN];
+    auto ldall = [&](const char* base) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[s][j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[s][i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
+      }
+    };
+    auto mmaall = [&]() {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][i], fb[s][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    auto bar = [] {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    if (!g1) {
+      stage_a(0, 0);
+    } else {
+      stage_b(0, 0);
+      if (nk > 1) stage_b(1, 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (g1) bar();
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* base = smem + (kt & 1) * STAGE;
+      if (!g1 && kt + 1 < nk) stage_a((kt + 1) & 1, kt + 1);
+      ldall(base);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+      if (g1 && kt + 2 < nk) stage_b(kt & 1, kt + 2);
+      mmaall();
+      if (!g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+    }
+    if (!g1) bar();
   }
 
   // Epilogue: acc[i][j][r] is C(row = wr·16FM + i·16 + fq·4 + r, col = wc·16FN + j·16 + fr)
@@ -243,11 +305,13 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256, 2, 4, 8, 4, 0)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256p, 2, 4, 8, 4, 1)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256pp, 2, 4, 8, 4, 2)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256ps, 2, 4, 8, 4, 3)
 // 256×128 tiles, 8 waves (4×2, 64×64 each), 96 KiB LDS — twice the tiles
 // for strongly scaled slices (8 GPUs × 1024 rows of an 8192² problem).
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128, 4, 2, 4, 4, 0)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128p, 4, 2, 4, 4, 1)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128pp, 4, 2, 4, 4, 2)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128ps, 4, 2, 4, 4, 3)
 // 128×128 tiles, 4 waves (2×2, 64×64 each), 64 KiB LDS, 2 blocks/CU.
 CEK_GEMM_KERNEL(cek_sgemm_bf16_128x128, 2, 2, 4, 4, 0)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_128x128p, 2, 2, 4, 4, 1)

@@ -25,9 +25,11 @@ TILES = {
     "256x256": (256, 256, 512, "cek_sgemm_bf16_256x256"),
     "256x256p": (256, 256, 512, "cek_sgemm_bf16_256x256p"),
     "256x256pp": (256, 256, 512, "cek_sgemm_bf16_256x256pp"),
+    "256x256ps": (256, 256, 512, "cek_sgemm_bf16_256x256ps"),
     "256x128": (256, 128, 512, "cek_sgemm_bf16_256x128"),
     "256x128p": (256, 128, 512, "cek_sgemm_bf16_256x128p"),
     "256x128pp": (256, 128, 512, "cek_sgemm_bf16_256x128pp"),
+    "256x128ps": (256, 128, 512, "cek_sgemm_bf16_256x128ps"),
     "128x128": (128, 128, 256, "cek_sgemm_bf16_128x128"),
     "128x128p": (128, 128, 256, "cek_sgemm_bf16_128x128p"),
 }

@@ -14,8 +14,8 @@ import os
 from .._native import kernel_dir
 
 LIBRARY = {
-    "sgemm_bf16": ["cek_sgemm_bf16_256x256", "cek_sgemm_bf16_256x256p", "cek_sgemm_bf16_256x256pp",
-                   "cek_sgemm_bf16_256x128", "cek_sgemm_bf16_256x128p", "cek_sgemm_bf16_256x128pp",
+    "sgemm_bf16": ["cek_sgemm_bf16_256x256", "cek_sgemm_bf16_256x256p", "cek_sgemm_bf16_256x256pp", "cek_sgemm_bf16_256x256ps",
+                   "cek_sgemm_bf16_256x128", "cek_sgemm_bf16_256x128p", "cek_sgemm_bf16_256x128pp", "cek_sgemm_bf16_256x128ps",
                    "cek_sgemm_bf16_128x128", "cek_sgemm_bf16_128x128p"],
     "mandelbrot": ["cek_mandelbrot_f32"],
     "reduce": ["cek_reduce_sum_f32", "cek_reduce_sum_f32_final"],

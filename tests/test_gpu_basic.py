@@ -54,7 +54,7 @@ def test_logical_devices_pipelines(pipeline, ptype):
     assert sum(cr.ranges(5)) == n
 
 
-@pytest.mark.parametrize("tile", ["256x256", "256x256p", "256x256pp", "256x128", "256x128p", "256x128pp",
+@pytest.mark.parametrize("tile", ["256x256", "256x256p", "256x256pp", "256x256ps", "256x128", "256x128p", "256x128pp", "256x128ps",
                                   "128x128", "128x128p"])
 def test_gemm_bf16_matches_fp64(tile):
     from cekirdekler_amd.ops.gemm import GemmBf16
