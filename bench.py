@@ -89,7 +89,7 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     from cekirdekler_amd.parallel.distributed import DistributedCruncher
 
     if tile is None:
-        tile = "256x256" if (size // 256) ** 2 // ctx.world >= 256 else "256x128"
+        tile = "256x256pp" if (size // 256) ** 2 // ctx.world >= 256 else "256x128pp"
     cr = DistributedCruncher("", ctx=ctx, prebuilt=library("sgemm_bf16"))
     g = GemmBf16(size, size, size, cruncher=cr, tile=tile)
     ms = timed(ctx, lambda: g.run(compute_id=1, resident=True), steps, warmup)
@@ -129,6 +129,7 @@ def bench_lb_iters():
     src = """__global__ void k(float* x){ long long i = get_global_id(0); float v = x[i];
         for (int j = 0; j < 2048; ++j) v = v * 0.999f + 1.0f; x[i] = v; }"""
     cr = ck.ClNumberCruncher(devs, src)
+    cr.cores.serial = True  # logical devices share one GPU: time them in isolation
     cr.set_time_scale(1, 2.0)
     n = 1 << 22
     x = ck.ClArray(n, np.float32)

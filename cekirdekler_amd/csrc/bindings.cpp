@@ -226,6 +226,7 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("no_compute", &Cores::no_compute)
       .def_readwrite("fine_grained", &Cores::fine_grained)
       .def_readwrite("smooth", &Cores::smooth)
+      .def_readwrite("serial", &Cores::serial)
       .def_readwrite("dist_gather_writes", &Cores::dist_gather_writes)
       .def_readwrite("dist_broadcast_reads", &Cores::dist_broadcast_reads)
       .def("set_time_scale", &Cores::set_time_scale)

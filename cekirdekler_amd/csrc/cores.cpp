@@ -467,7 +467,7 @@ void Cores::compute(const ComputeCall& c) {
 
   auto it = state_.find(c.compute_id);
   bool fresh = it == state_.end() || it->second.global_range != G ||
-               it->second.local_range != L ||
+               (it->second.local_range != 0 && it->second.local_range != L) ||
                static_cast<int>(it->second.ranges.size()) != D;
   BalancerState& st = state_[c.compute_id];
   if (fresh) {
@@ -478,6 +478,10 @@ void Cores::compute(const ComputeCall& c) {
     st.local_range = L;
   }
   st.global_offset = c.global_offset;
+  st.local_range = L;  // (restored states carry no local range)
+  if (st.history.size() != static_cast<size_t>(kHistoryDepth))
+    st.history.assign(kHistoryDepth, std::vector<double>(D, 0.0));
+  if (st.bench.size() != static_cast<size_t>(D)) st.bench.assign(D, 0.0);
   const bool first = fresh || std::all_of(st.ranges.begin(), st.ranges.end(), [](long long r) { return r == 0; });
   if (!(enqueue_mode_ && !first)) {
     if (first) {
@@ -507,8 +511,11 @@ void Cores::compute(const ComputeCall& c) {
 
   std::vector<double> ms(nloc, 0.0);
   std::vector<uint64_t> h2d(nloc, 0), d2h(nloc, 0);
-  if (nloc == 1) {
-    run_device(0, c, st.references[global_base_], st.ranges[global_base_], pipelined, &ms[0], &h2d[0], &d2h[0]);
+  if (nloc == 1 || serial) {
+    for (int w = 0; w < nloc; ++w) {
+      int g = global_base_ + w;
+      run_device(w, c, st.references[g], st.ranges[g], pipelined, &ms[w], &h2d[w], &d2h[w]);
+    }
   } else {
     for (int w = 0; w < nloc; ++w) {
       int g = global_base_ + w;

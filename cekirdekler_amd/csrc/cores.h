@@ -81,6 +81,7 @@ class Cores {
   bool no_compute = false;
   bool fine_grained = false;
   bool smooth = true;
+  bool serial = false;  // run devices one after another (isolated timings)
   void set_time_scale(int device, double scale);  // injected heterogeneity (tests/bench)
   void set_dynamic_lds(unsigned bytes);
 
