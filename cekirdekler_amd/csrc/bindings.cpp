@@ -91,6 +91,23 @@ PYBIND11_MODULE(_cek, m) {
   m.def("host_is_pinned", [](uint64_t p) { return host_is_pinned(reinterpret_cast<void*>(p)); });
   m.def("host_register", [](uint64_t p, uint64_t n) { return host_register(reinterpret_cast<void*>(p), n); });
   m.def("host_unregister", [](uint64_t p) { host_unregister(reinterpret_cast<void*>(p)); });
+  // Unified-address copy between any two of {host, GPU i, GPU j}: device→device
+  // goes over xGMI (peer), host↔device over PCIe; plain memcpy without a GPU.
+  m.def("memcpy_default", [](uint64_t d, uint64_t s, uint64_t n) {
+    py::gil_scoped_release r;
+    if (n == 0) return;
+    if (gpu_count() == 0) {
+      copy_memory(reinterpret_cast<void*>(d), reinterpret_cast<const void*>(s), n);
+      return;
+    }
+    CEK_HIP(hipMemcpy(reinterpret_cast<void*>(d), reinterpret_cast<const void*>(s), n, hipMemcpyDefault));
+  });
+  m.def("device_synchronize", [](int ordinal) {
+    py::gil_scoped_release r;
+    if (gpu_count() == 0) return;
+    CEK_HIP(hipSetDevice(ordinal));
+    CEK_HIP(hipDeviceSynchronize());
+  });
   m.def("copy_memory", [](uint64_t d, uint64_t s, uint64_t n) {
     py::gil_scoped_release r;
     copy_memory(reinterpret_cast<void*>(d), reinterpret_cast<const void*>(s), n);

@@ -1,0 +1,420 @@
+"""Stage pipelines.
+
+**Device→device stage pipeline** (reference ``ClPipeline`` /
+``ClPipelineStage``, ClPipeline.cs:41-1874).  A linear chain of stages, each
+with its own device set, kernels and input/hidden/output buffers.  Inputs and
+outputs are double-buffered: on every :meth:`ClPipeline.push_data` all stages
+compute concurrently on their current buffers while the previous results move
+one stage forward through the duplicates; then current and duplicate swap.
+Results appear after ~2·stages pushes (same ready-counter rule as the
+reference, :114-124).
+
+MI355X-native difference: the reference moves every stage transition
+device→host→device (ClPipeline.cs:1422-1574).  Here a single-device stage
+keeps its buffers device-resident and forwards output→next input with a
+unified-address device→device copy (xGMI peer copy between GPUs, no host
+bounce); only multi-device stages fall back to host staging.
+
+**Single-device multi-queue pipeline** (reference ``DevicePipeline`` /
+``DevicePipelineStage`` / ``DevicePipelineArray(Type)``,
+ClPipeline.cs:2363-3234).  N stages on one device, each launched on its own
+HIP stream (enqueue mode + async queues) so their kernels overlap;
+TRANSITION arrays are double-buffered between neighbouring stages,
+INPUT/OUTPUT arrays double-buffered towards the host.
+"""
+from __future__ import annotations
+
+import enum
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+from .._native import cek, gpu_available
+from ..arrays import ClArray, ClParameterGroup, as_clarray
+from ..cruncher import ClNumberCruncher
+from ..hardware import ClDevices
+
+_peer_enabled = False
+_peer_lock = threading.Lock()
+
+
+def _enable_peers() -> None:
+    global _peer_enabled
+    with _peer_lock:
+        if not _peer_enabled and gpu_available():
+            cek.enable_peer_access()
+            _peer_enabled = True
+
+
+def _clone(a: ClArray) -> ClArray:
+    d = ClArray(a.N, a.dtype if not a.is_bf16 else "bfloat16")
+    d.array[:] = a.array
+    d.elements_per_work_item = a.elements_per_work_item
+    return d
+
+
+# =========================================================================== device → device
+
+
+class ClPipelineStage:
+    """One stage: devices + kernels + input/hidden/output buffers."""
+
+    def __init__(self, debug: bool = False):
+        self.debug = debug
+        self.devices: Optional[ClDevices] = None
+        self.kernel_source = ""
+        self.kernel_names: List[str] = []
+        self.global_ranges: List[int] = []
+        self.local_ranges: List[int] = []
+        self.init_names: List[str] = []
+        self.init_globals: List[int] = []
+        self.init_locals: List[int] = []
+        self.inputs: List[ClArray] = []
+        self.hiddens: List[ClArray] = []
+        self.outputs: List[ClArray] = []
+        self._in_dup: List[ClArray] = []
+        self._out_dup: List[ClArray] = []
+        self.previous: Optional["ClPipelineStage"] = None
+        self.next: Optional["ClPipelineStage"] = None
+        self.cruncher: Optional[ClNumberCruncher] = None
+        self.elapsed_time = 0.0
+        self.stage_id = 0
+        self._resident = False
+
+    # ---- building -----------------------------------------------------------
+    def add_devices(self, devices: ClDevices) -> None:
+        self.devices = devices if self.devices is None else self.devices + devices
+
+    def add_kernels(self, kernels: str, kernel_names: str, global_ranges: Sequence[int],
+                    local_ranges: Sequence[int]) -> None:
+        self.kernel_source += "\n" + kernels
+        names = kernel_names.split() if isinstance(kernel_names, str) else list(kernel_names)
+        if len(names) != len(global_ranges) or len(names) != len(local_ranges):
+            raise ValueError("one global and one local range per kernel name")
+        self.kernel_names += names
+        self.global_ranges += list(global_ranges)
+        self.local_ranges += list(local_ranges)
+
+    def initializer_kernel(self, names: str, global_ranges: Sequence[int], local_ranges: Sequence[int]) -> None:
+        """Kernels run once on both buffer sets when the pipeline is built
+        (reference initializerKernel, ClPipeline.cs:1678)."""
+        self.init_names = names.split()
+        self.init_globals = list(global_ranges)
+        self.init_locals = list(local_ranges)
+
+    def add_input_buffers(self, *arrays) -> None:
+        self.inputs += [as_clarray(a) for a in arrays]
+
+    def add_hidden_buffers(self, *arrays) -> None:
+        self.hiddens += [as_clarray(a) for a in arrays]
+
+    def add_output_buffers(self, *arrays) -> None:
+        self.outputs += [as_clarray(a) for a in arrays]
+
+    def prepend_to_stage(self, stage: "ClPipelineStage") -> None:
+        """This stage runs before ``stage``."""
+        self.next, stage.previous = stage, self
+
+    def append_to_stage(self, stage: "ClPipelineStage") -> None:
+        """This stage runs after ``stage``."""
+        stage.next, self.previous = self, stage
+
+    addDevices = add_devices
+    addKernels = add_kernels
+    initializerKernel = initializer_kernel
+    addInputBuffers = add_input_buffers
+    addHiddenBuffers = add_hidden_buffers
+    addOutputBuffers = add_output_buffers
+    prependToStage = prepend_to_stage
+    appendToStage = append_to_stage
+
+    def make_pipeline(self) -> "ClPipeline":
+        head = self
+        while head.previous is not None:
+            head = head.previous
+        stages = []
+        s = head
+        while s is not None:
+            stages.append(s)
+            s = s.next
+        for i, st in enumerate(stages):
+            st.stage_id = i
+            st._setup()
+        for st in stages:
+            st._run_initializers()
+        return ClPipeline(stages, self.debug)
+
+    makePipeline = make_pipeline
+
+    # ---- runtime --------------------------------------------------------------
+    def _setup(self) -> None:
+        if self.devices is None or len(self.devices) == 0:
+            raise ValueError(f"stage {self.stage_id} has no devices")
+        self.cruncher = ClNumberCruncher(self.devices, self.kernel_source, no_pipelining=True)
+        if self.cruncher.error_code():
+            raise RuntimeError(f"stage {self.stage_id} build failed:\n{self.cruncher.error_message()}")
+        self._resident = len(self.devices) == 1
+        if self._resident and self.devices.device(0).is_gpu:
+            _enable_peers()
+        self._in_dup = [_clone(a) for a in self.inputs]
+        self._out_dup = [_clone(a) for a in self.outputs]
+        for a in self.inputs + self._in_dup:
+            a.write, a.partial_read = False, False
+            a.read = not self._resident
+        for a in self.outputs + self._out_dup:
+            a.read, a.partial_read = False, False
+            a.write = not self._resident
+        for a in self.hiddens:
+            a.read, a.partial_read, a.write = False, False, False
+        if self._resident:
+            # materialise every replica with the host contents once
+            for a in self.inputs + self._in_dup + self.outputs + self._out_dup + self.hiddens:
+                self.cruncher.upload(a, 0)
+
+    def _group(self, dup: bool) -> ClParameterGroup:
+        ins = self._in_dup if dup else self.inputs
+        outs = self._out_dup if dup else self.outputs
+        return ClParameterGroup(ins + self.hiddens + outs)
+
+    def _run_initializers(self) -> None:
+        for dup in (False, True):
+            g = self._group(dup)
+            for k, G, L in zip(self.init_names, self.init_globals, self.init_locals):
+                g.compute(self.cruncher, 1000 + self.stage_id, k, G, L)
+
+    def run(self) -> None:
+        t0 = time.perf_counter()
+        g = self._group(False)
+        for i, (k, G, L) in enumerate(zip(self.kernel_names, self.global_ranges, self.local_ranges)):
+            g.compute(self.cruncher, 1 + i, k, G, L)
+        self.elapsed_time = (time.perf_counter() - t0) * 1e3
+
+    def _replica_ptr(self, a: ClArray) -> int:
+        return self.cruncher.device_pointer(a, 0)
+
+    def switch_input_buffers(self) -> None:
+        self.inputs, self._in_dup = self._in_dup, self.inputs
+
+    def switch_output_buffers(self) -> None:
+        self.outputs, self._out_dup = self._out_dup, self.outputs
+
+
+def _copy_array(dst_stage: Optional[ClPipelineStage], dst: ClArray, src_stage: Optional[ClPipelineStage],
+                src: ClArray) -> None:
+    """Move src's data into dst: device→device when both sides are
+    device-resident, else through host memory."""
+    n = min(src.nbytes, dst.nbytes)
+    src_dev = src_stage is not None and src_stage._resident
+    dst_dev = dst_stage is not None and dst_stage._resident
+    if src_dev and dst_dev:
+        cek.memcpy_default(dst_stage._replica_ptr(dst), src_stage._replica_ptr(src), n)
+    elif src_dev:
+        cek.memcpy_default(dst.host_pointer(), src_stage._replica_ptr(src), n)
+    elif dst_dev:
+        cek.memcpy_default(dst_stage._replica_ptr(dst), src.host_pointer(), n)
+    else:
+        cek.copy_memory(dst.host_pointer(), src.host_pointer(), n)
+
+
+class ClPipeline:
+    """A built device-to-device pipeline (reference ``ClPipeline``)."""
+
+    def __init__(self, stages: List[ClPipelineStage], debug: bool = False):
+        self.stages = stages
+        self.debug = debug
+        self.counter = 0
+        self._pool = ThreadPoolExecutor(max_workers=max(2, 2 * len(stages)))
+
+    def _forward(self, k: int, data, results) -> None:
+        st = self.stages[k]
+        last = len(self.stages) - 1
+        if k == 0 and data is not None:
+            for dst, d in zip(st._in_dup, data):
+                src = as_clarray(d)
+                _copy_array(st, dst, None, src)
+        if k < last:
+            nxt = self.stages[k + 1]
+            for dst, src in zip(nxt._in_dup, st._out_dup):
+                _copy_array(nxt, dst, st, src)
+        elif results is not None:
+            for r, src in zip(results, st._out_dup):
+                dst = as_clarray(r)
+                _copy_array(None, dst, st, src)
+                if not isinstance(r, ClArray):
+                    np.copyto(np.asarray(r).reshape(-1), dst.array[:np.asarray(r).size].reshape(-1))
+
+    def push_data(self, data: Optional[Sequence] = None, results: Optional[Sequence] = None) -> bool:
+        """Advance the pipeline one step; returns True once results are
+        flowing out (reference pushData, ClPipeline.cs:49-125)."""
+        S = len(self.stages)
+        futs = [self._pool.submit(st.run) for st in self.stages]
+        futs += [self._pool.submit(self._forward, k, data, results) for k in range(S)]
+        for f in futs:
+            f.result()
+        for i, st in enumerate(self.stages):
+            if data is not None or i != 0:
+                st.switch_input_buffers()
+            if results is not None or i != S - 1:
+                st.switch_output_buffers()
+        self.counter += 1
+        if data is None and results is None:
+            return self.counter > 2 * S - 2
+        if data is not None and results is not None:
+            return self.counter > 2 * S
+        return self.counter > 2 * S - 1
+
+    pushData = push_data
+
+    def elapsed_times(self) -> List[float]:
+        return [s.elapsed_time for s in self.stages]
+
+    def dispose(self) -> None:
+        self._pool.shutdown(wait=True)
+        for s in self.stages:
+            if s.cruncher:
+                s.cruncher.dispose()
+
+
+# =========================================================================== single device
+
+
+class DevicePipelineArrayType(enum.IntEnum):
+    INPUT = 0
+    OUTPUT = 1
+    INTERNAL = 2
+    TRANSITION = 3
+
+
+class DevicePipelineArray:
+    """An array bound to device-pipeline stages with a role."""
+
+    def __init__(self, type_: DevicePipelineArrayType, array):
+        self.type = DevicePipelineArrayType(type_)
+        self.array = as_clarray(array)
+        self.dup = _clone(self.array) if self.type != DevicePipelineArrayType.INTERNAL else None
+        self.stages: List["DevicePipelineStage"] = []
+
+    def buffers(self):
+        return (self.array, self.dup)
+
+
+class DevicePipelineStage:
+    def __init__(self, kernel_names: str, global_range: int, local_range: int):
+        self.kernel_names = kernel_names
+        self.global_range = global_range
+        self.local_range = local_range
+        self.arrays: List[DevicePipelineArray] = []
+        self.index = 0
+
+    def bind_array(self, arr: DevicePipelineArray) -> None:
+        self.arrays.append(arr)
+        arr.stages.append(self)
+
+    bindArray = bind_array
+
+
+class DevicePipeline:
+    """N stages on one device, overlapped on separate HIP streams."""
+
+    def __init__(self, device: ClDevices, kernel_source: str, queue_concurrency: int = 16):
+        if len(device) != 1:
+            raise ValueError("DevicePipeline runs on exactly one device")
+        self.cruncher = ClNumberCruncher(device, kernel_source, queue_concurrency=queue_concurrency)
+        if self.cruncher.error_code():
+            raise RuntimeError(self.cruncher.error_message())
+        self.stages: List[DevicePipelineStage] = []
+        self.serial = False
+        self._parity = 0
+        self._async = None
+
+    def add_stage(self, stage: DevicePipelineStage) -> None:
+        stage.index = len(self.stages)
+        self.stages.append(stage)
+
+    addStage = add_stage
+
+    def enable_serial_mode(self) -> None:
+        self.serial = True
+
+    def enable_parallel_mode(self) -> None:
+        self.serial = False
+
+    enableSerialMode = enable_serial_mode
+    enableParallelMode = enable_parallel_mode
+
+    @property
+    def query_timeline_overlap_percentage(self):
+        raise NotImplementedError("not implemented in the reference either (ClPipeline.cs:2391)")
+
+    def _args(self, st: DevicePipelineStage) -> ClParameterGroup:
+        p = self._parity
+        out = []
+        for a in st.arrays:
+            if a.type == DevicePipelineArrayType.INTERNAL:
+                buf = a.array
+                buf.read = buf.write = buf.partial_read = False
+            elif a.type == DevicePipelineArrayType.INPUT:
+                buf = a.buffers()[p]          # host fills the other one meanwhile
+                buf.read, buf.write, buf.partial_read = True, False, False
+            elif a.type == DevicePipelineArrayType.OUTPUT:
+                buf = a.buffers()[p]
+                buf.read, buf.write, buf.partial_read = False, True, False
+            else:  # TRANSITION: producer (first bound stage) writes p, consumer reads 1-p
+                producer = a.stages[0] is st
+                buf = a.buffers()[p if producer else 1 - p]
+                buf.read = buf.write = buf.partial_read = False
+            out.append(buf)
+        return ClParameterGroup(out)
+
+    def _enqueue(self) -> None:
+        cr = self.cruncher
+        if not self.serial:
+            cr.enqueue_mode = True
+            cr.enqueue_mode_async_enable = True
+        for st in self.stages:
+            self._args(st).compute(cr, 100 + st.index, st.kernel_names, st.global_range, st.local_range)
+
+    def _finish(self) -> None:
+        cr = self.cruncher
+        if not self.serial:
+            cr.enqueue_mode = False
+            cr.enqueue_mode_async_enable = False
+        self._parity ^= 1
+
+    def feed(self) -> None:
+        """One pipeline step: every stage runs once (concurrently)."""
+        self._enqueue()
+        self._finish()
+
+    def feed_async_begin(self) -> None:
+        self._enqueue()
+
+    def feed_async_end(self) -> None:
+        self._finish()
+
+    def feed_async(self, callback: Callable[[], None]) -> None:
+        """Enqueue a step, run ``callback`` (host work) while devices compute,
+        then complete the step."""
+        self._enqueue()
+        try:
+            callback()
+        finally:
+            self._finish()
+
+    feedAsync = feed_async
+    feedAsyncBegin = feed_async_begin
+    feedAsyncEnd = feed_async_end
+
+    def input_buffer(self, arr: DevicePipelineArray) -> ClArray:
+        """The host-side INPUT buffer the host may fill for the next feed."""
+        return arr.buffers()[1 - self._parity]
+
+    def output_buffer(self, arr: DevicePipelineArray) -> ClArray:
+        """The OUTPUT buffer holding the last completed feed's results."""
+        return arr.buffers()[1 - self._parity]
+
+    def dispose(self) -> None:
+        self.cruncher.dispose()

@@ -1,0 +1,72 @@
+"""Stage pipelines on the CPU device: device→device ClPipeline with double
+buffers (results appear after 2·stages pushes, like ClPipeline.cs:114-124)
+and the single-device multi-stream DevicePipeline."""
+import numpy as np
+
+import cekirdekler_amd as ck
+from cekirdekler_amd.parallel.pipeline import (ClPipelineStage, DevicePipeline, DevicePipelineArray,
+                                               DevicePipelineArrayType, DevicePipelineStage)
+
+N = 1024
+K1 = "__global__ void add1(const float* x, float* y) { long long i = get_global_id(0); y[i] = x[i] + 1.0f; }"
+K2 = "__global__ void mul2(const float* y, float* t, float* z) { long long i = get_global_id(0); t[i] = y[i]; z[i] = t[i] * 2.0f; }"
+K3 = "__global__ void sub3(const float* z, float* w) { long long i = get_global_id(0); w[i] = z[i] - 3.0f; }"
+
+
+def _stage(devs, src, name, ins, hid, outs):
+    s = ClPipelineStage()
+    s.add_devices(devs)
+    s.add_kernels(src, name, [N], [64])
+    s.add_input_buffers(*ins)
+    if hid:
+        s.add_hidden_buffers(*hid)
+    s.add_output_buffers(*outs)
+    return s
+
+
+def test_three_stage_pipeline_latency_and_values():
+    cpu = ck.ClPlatforms.all().cpus(True)
+    x, y1, y2, t, z1, z2, w = (np.zeros(N, np.float32) for _ in range(7))
+    s1 = _stage(cpu, K1, "add1", [x], None, [y1])
+    s2 = _stage(cpu, K2, "mul2", [y2], [t], [z1])
+    s3 = _stage(cpu, K3, "sub3", [z2], None, [w])
+    s1.prepend_to_stage(s2)
+    s3.append_to_stage(s2)
+    pipe = s1.make_pipeline()
+    res = np.zeros(N, np.float32)
+    seen = []
+    for p in range(12):
+        data = np.full(N, float(p), np.float32)
+        ready = pipe.push_data([data], [res])
+        if ready:
+            seen.append(float(res[0]))
+            assert np.all(res == res[0])
+    # f(p) = (p + 1) * 2 - 3, emitted with a lag of 2·stages = 6 pushes
+    assert seen == [(p + 1) * 2 - 3 for p in range(len(seen))]
+    assert len(seen) == 12 - 6
+    pipe.dispose()
+
+
+def test_device_pipeline_transition_double_buffer():
+    cpu = ck.ClPlatforms.all().cpus(True)
+    src = K1 + "\n" + K3
+    dp = DevicePipeline(cpu, src)
+    inp = DevicePipelineArray(DevicePipelineArrayType.INPUT, np.zeros(N, np.float32))
+    mid = DevicePipelineArray(DevicePipelineArrayType.TRANSITION, np.zeros(N, np.float32))
+    out = DevicePipelineArray(DevicePipelineArrayType.OUTPUT, np.zeros(N, np.float32))
+    a = DevicePipelineStage("add1", N, 64)
+    a.bind_array(inp)
+    a.bind_array(mid)
+    b = DevicePipelineStage("sub3", N, 64)
+    b.bind_array(mid)
+    b.bind_array(out)
+    dp.add_stage(a)
+    dp.add_stage(b)
+    got = []
+    for p in range(6):
+        dp.input_buffer(inp).array[:] = p
+        dp.feed()
+        got.append(float(dp.output_buffer(out).array[0]))
+    # value p enters at feed p+1, passes stage a at p+1, stage b at p+2
+    assert got[3:] == [(p + 1) - 3 for p in range(1, 4)]
+    dp.dispose()
