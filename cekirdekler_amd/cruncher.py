@@ -317,11 +317,12 @@ class ClNumberCruncher:
 
     def _compute_group(self, group: ClParameterGroup, compute_id: int, kernels, global_range: int,
                        local_range: int = 256, global_offset: int = 0, pipeline: bool = False,
-                       pipeline_type: bool = PIPELINE_EVENT, pipeline_blobs: int = 4) -> None:
+                       pipeline_type: bool = PIPELINE_EVENT, pipeline_blobs: int = 4, specs=None) -> None:
         names = split_kernel_names(kernels)
         G, L = int(global_range), int(local_range)
         try:
-            self._validate(group, names, G, L, pipeline, int(pipeline_blobs))
+            self._validate(group if specs is None else ClParameterGroup(), names, G, L, pipeline,
+                           int(pipeline_blobs))
         except ClComputeError:
             self.number_of_errors_happened += 1
             raise
@@ -329,7 +330,7 @@ class ClNumberCruncher:
         call.kernels = names
         call.repeats = max(1, int(self.repeat_count))
         call.repeat_kernel = self.repeat_kernel_name if self.repeat_count > 1 else ""
-        call.arrays = [a._spec() for a in group.arrays]
+        call.arrays = specs if specs is not None else [a._spec() for a in group.arrays]
         call.global_range = G
         call.local_range = L
         call.global_offset = int(global_offset)

@@ -259,6 +259,8 @@ PYBIND11_MODULE(_cek, m) {
       .def("last_record", &Cores::last_record)
       .def("markers_reached", &Cores::markers_reached)
       .def("markers_issued", &Cores::markers_issued)
+      .def("last_marker", &Cores::last_marker)
+      .def("marker_word", &Cores::marker_word)
       .def("finish", &Cores::finish, py::call_guard<py::gil_scoped_release>())
       .def("release_array", &Cores::release_array)
       .def("device_bytes", &Cores::device_bytes)

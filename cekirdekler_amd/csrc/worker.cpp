@@ -280,10 +280,21 @@ void Worker::launch(hipStream_t s, const std::string& kernel, const std::vector<
 
 void Worker::add_marker(hipStream_t s) {
   ++markers_issued_;
-  if (!gpu()) return;
+  if (!gpu()) {
+    last_slot_ = -1;
+    last_value_ = static_cast<uint64_t>(markers_issued_);
+    return;
+  }
   int slot = stream_slot(s);
   uint64_t v = ++marker_issued_per_slot_[slot];
+  last_slot_ = slot;
+  last_value_ = v;
   CEK_HIP(hipStreamWriteValue64(s, host_device_ptr(&marker_words_[slot]), v, 0));
+}
+
+uint64_t Worker::marker_word(int slot) const {
+  if (!gpu() || slot < 0) return static_cast<uint64_t>(markers_issued_);
+  return __atomic_load_n(&marker_words_[slot], __ATOMIC_ACQUIRE);
 }
 
 long long Worker::markers_reached() {

@@ -107,6 +107,10 @@ class Worker {
   // --- markers (fine-grained queue control, ClCommandQueue.cs:103-112) ---
   void add_marker(hipStream_t s);
   long long markers_reached();
+  // (slot, value) of the newest marker; a marker is reached once
+  // marker_word(slot) >= value.  CPU device: slot -1 (always reached).
+  std::pair<int, uint64_t> last_marker() const { return {last_slot_, last_value_}; }
+  uint64_t marker_word(int slot) const;
   long long markers_issued() const { return markers_issued_; }
 
   // --- job thread --------------------------------------------------------
@@ -140,6 +144,8 @@ class Worker {
   uint64_t* marker_words_ = nullptr;
   std::vector<uint64_t> marker_issued_per_slot_;
   long long markers_issued_ = 0;
+  int last_slot_ = -1;
+  uint64_t last_value_ = 0;
 
   std::unique_ptr<CpuPool> pool_;
 
