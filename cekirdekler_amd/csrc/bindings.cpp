@@ -268,5 +268,6 @@ PYBIND11_MODULE(_cek, m) {
       .def("upload", &Cores::upload, py::call_guard<py::gil_scoped_release>())
       .def("download", &Cores::download, py::call_guard<py::gil_scoped_release>())
       .def("copy_between", &Cores::copy_between, py::call_guard<py::gil_scoped_release>())
+      .def("share_slices", &Cores::share_slices, py::call_guard<py::gil_scoped_release>())
       .def("set_distributed", &Cores::set_distributed);
 }

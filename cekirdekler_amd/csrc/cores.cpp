@@ -209,6 +209,52 @@ void Cores::copy_between(int src_dev, const ArraySpec& src, int dst_dev, const A
   }
 }
 
+void Cores::share_slices(int id, const ArraySpec& a, long long local_range) {
+  auto it = state_.find(id);
+  if (it == state_.end()) throw Error("share_slices: unknown compute id");
+  const auto& st = it->second;
+  const int n = num_devices();
+  std::vector<uint64_t> off(n), len(n);
+  for (int w = 0; w < n; ++w) {
+    uint64_t b, c;
+    a.slice(st.references[global_base_ + w], st.ranges[global_base_ + w], local_range, b, c);
+    off[w] = b * a.elem_size;
+    len[w] = c * a.elem_size;
+    if (off[w] >= a.bytes) len[w] = 0;
+    else if (off[w] + len[w] > a.bytes) len[w] = a.bytes - off[w];
+  }
+  std::vector<char*> ptr(n);
+  for (int w = 0; w < n; ++w) {
+    workers_[w]->set_device();
+    ptr[w] = static_cast<char*>(workers_[w]->buffer(a));
+  }
+  for (int s = 0; s < n; ++s) {
+    Worker& ws = *workers_[s];
+    if (len[s] == 0) continue;
+    for (int d = 0; d < n; ++d) {
+      if (d == s) continue;
+      Worker& wd = *workers_[d];
+      if (ptr[d] == ptr[s]) continue;  // same memory (CPU devices share host arrays)
+      if (ws.gpu()) {
+        ws.set_device();
+        hipStream_t st_s = ws.main_stream();
+        if (wd.gpu() && wd.dev().ordinal != ws.dev().ordinal)
+          CEK_HIP(hipMemcpyPeerAsync(ptr[d] + off[s], wd.dev().ordinal, ptr[s] + off[s], ws.dev().ordinal,
+                                     len[s], st_s));
+        else
+          CEK_HIP(hipMemcpyAsync(ptr[d] + off[s], ptr[s] + off[s], len[s], hipMemcpyDefault, st_s));
+      } else if (wd.gpu()) {
+        wd.set_device();
+        CEK_HIP(hipMemcpyAsync(ptr[d] + off[s], ptr[s] + off[s], len[s], hipMemcpyHostToDevice,
+                               wd.main_stream()));
+      } else {
+        std::memcpy(ptr[d] + off[s], ptr[s] + off[s], len[s]);
+      }
+    }
+  }
+  for (auto& w : workers_) w->sync_all();
+}
+
 // ------------------------------------------------------------- compute --
 
 void Cores::launch_kernels(Worker& wk, hipStream_t s, const ComputeCall& c, long long ref,

@@ -108,6 +108,10 @@ class Cores {
   uint64_t device_pointer(int i, const ArraySpec& a);
   void upload(int i, const ArraySpec& a);    // whole array H2D (sync)
   void download(int i, const ArraySpec& a);  // whole array D2H (sync)
+  // Keep-resident all-gather inside one process: every device's slice of
+  // `a` (by the ranges of compute id `id`) is copied into every other
+  // device's replica, GPU↔GPU as peer copies over xGMI (no host bounce).
+  void share_slices(int id, const ArraySpec& a, long long local_range);
   void copy_between(int src_dev, const ArraySpec& src, int dst_dev, const ArraySpec& dst,
                     uint64_t bytes);  // device→device (peer/xGMI) copy, sync
 

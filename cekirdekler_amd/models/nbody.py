@@ -1,0 +1,119 @@
+"""All-pairs N-body simulation on the AOT CDNA4 kernels.
+
+The body range is split across devices by the load balancer (compute id 1
+for forces, 2 for integration).  Every device needs every position for the
+force pass, so after each step the position slices are made coherent again:
+
+* ``resident=True`` (MI355X-native): positions stay in device memory and each
+  device's updated slice is copied into the other devices' replicas
+  (:meth:`Cores.share_slices`: GPU↔GPU peer copies over xGMI);
+* ``resident=False`` (reference semantics, Tester.cs:7759-7765): slices go
+  device→host and the whole array host→device on the next step.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ..arrays import ClArray
+from ..cruncher import ClNumberCruncher
+from ..ops.library import library
+
+FLOP_PER_INTERACTION = 20
+L = 256
+
+
+def nbody_accel_reference(pos: np.ndarray, eps2: float, g: float = 1.0, chunk: int = 1024) -> np.ndarray:
+    """float64 all-pairs reference: a_i = G Σ_j m_j (x_j − x_i) / (|x_j − x_i|² + ε²)^{3/2}."""
+    p = pos.reshape(-1, 4).astype(np.float64)
+    out = np.zeros((len(p), 3))
+    for s in range(0, len(p), chunk):
+        d = p[None, :, :3] - p[s:s + chunk, None, :3]
+        r2 = (d * d).sum(-1) + eps2
+        inv3 = r2 ** -1.5
+        out[s:s + chunk] = g * (d * (p[None, :, 3] * inv3)[..., None]).sum(1)
+    return out
+
+
+class NBodySimulation:
+    def __init__(self, n: int, devices=None, cruncher: ClNumberCruncher | None = None, eps: float = 0.01,
+                 dt: float = 1e-3, g: float = 1.0, seed: int = 0, resident: bool = True):
+        if n % (2 * L):
+            raise ValueError(f"n must be a multiple of {2 * L}")
+        self.n = n
+        self.resident = resident
+        self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library("nbody"))
+        rng = np.random.default_rng(seed)
+        pos = np.empty((n, 4), np.float32)
+        pos[:, :3] = rng.standard_normal((n, 3)).astype(np.float32)
+        pos[:, 3] = 1.0 / n
+        self.pos = ClArray(pos.reshape(-1))
+        self.vel = ClArray(np.zeros(4 * n, np.float32))
+        self.acc = ClArray(np.zeros(4 * n, np.float32))
+        self.params = ClArray(np.array([eps * eps, g, float(n), dt], np.float32))
+        self.params.write = False
+        self.steps = 0
+        self._flags_force()
+
+    @property
+    def interactions_per_step(self) -> float:
+        return float(self.n) * float(self.n)
+
+    @property
+    def flops_per_step(self) -> float:
+        return FLOP_PER_INTERACTION * self.interactions_per_step
+
+    def _flags_force(self) -> None:
+        # force pass: all positions in, this device's accelerations out
+        first = self.steps == 0
+        self.pos.read = first or not self.resident
+        self.pos.partial_read = False
+        self.pos.write = False
+        self.acc.read = False
+        self.acc.write = not self.resident
+        self.acc.elements_per_work_item = 8  # 2 bodies × float4 per work item
+        self.params.read = first or not self.resident
+
+    def forces(self, compute_id: int = 1) -> None:
+        self._flags_force()
+        self.pos.next_param(self.acc, self.params).compute(self.cr, compute_id, "cek_nbody_f32", self.n // 2, L)
+
+    def integrate(self, compute_id: int = 2) -> None:
+        for a in (self.pos, self.vel, self.acc):
+            a.elements_per_work_item = 4
+            a.read = False
+            a.partial_read = not self.resident
+            a.write = not self.resident
+        self.acc.write = False
+        self.acc.partial_read = False
+        self.params.read = False
+        self.pos.next_param(self.vel, self.acc, self.params).compute(
+            self.cr, compute_id, "cek_nbody_integrate_f32", self.n, L)
+        if self.resident and self.cr.cores.num_devices > 1:
+            self.cr.cores.share_slices(compute_id, self.pos._spec(), L)
+
+    def step(self) -> None:
+        self.forces()
+        self.integrate()
+        self.steps += 1
+
+    def download(self) -> None:
+        """Bring device-resident state to the host (device 0 holds every
+        slice of pos after share_slices; vel/acc slices per device)."""
+        c = self.cr.cores
+        self.cr.download(self.pos, 0)
+        for name in ("vel", "acc"):
+            arr = getattr(self, name)
+            if c.num_devices == 1:
+                self.cr.download(arr, 0)
+                continue
+            cid = 2 if name == "vel" else 1
+            refs, rng = self.cr.references(cid), self.cr.ranges(cid)
+            e = 4 if name == "vel" else 8
+            full = np.empty_like(arr.array)
+            keep = arr.array.copy()
+            for d in range(c.num_devices):
+                self.cr.download(arr, d)
+                g = c.global_base + d
+                full[refs[g] * e:(refs[g] + rng[g]) * e] = arr.array[refs[g] * e:(refs[g] + rng[g]) * e]
+            keep[:] = full
+            arr.array[:] = keep

@@ -104,3 +104,29 @@ def test_reduce_sum():
     G = n // 8
     x.next_param(part).compute(cr, 1, "cek_reduce_sum_f32", G, 256)
     np.testing.assert_allclose(part.array.sum(), x.array.astype(np.float64).sum(), rtol=1e-5)
+
+
+def test_nbody_forces_match_fp64():
+    from cekirdekler_amd.models.nbody import NBodySimulation, nbody_accel_reference
+
+    sim = NBodySimulation(4096, devices=_gpu()[0], resident=False)
+    sim.forces()
+    got = sim.acc.array.reshape(-1, 4)[:, :3]
+    ref = nbody_accel_reference(sim.pos.array, 0.01 ** 2)
+    err = np.abs(got - ref).max() / np.abs(ref).max()
+    assert err < 1e-4, err
+
+
+@pytest.mark.parametrize("resident", [True, False])
+def test_nbody_steps_two_logical_devices(resident):
+    from cekirdekler_amd.models.nbody import NBodySimulation
+
+    g0 = _gpu()[0]
+    one = NBodySimulation(2048, devices=g0, resident=resident)
+    two = NBodySimulation(2048, devices=g0 + g0, resident=resident)
+    for _ in range(3):
+        one.step()
+        two.step()
+    one.download()
+    two.download()
+    np.testing.assert_allclose(two.pos.array, one.pos.array, rtol=1e-5, atol=1e-6)
