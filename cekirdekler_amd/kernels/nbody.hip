@@ -16,9 +16,11 @@
 #include "cek_kernel.h"
 
 extern "C" __global__ __launch_bounds__(256) void cek_nbody_f32(const float4* __restrict__ pos,
+                                                              float4* __restrict__ vel,
                                                               float4* __restrict__ acc,
                                                               const float* __restrict__ params,
                                                               CEK_HIDDEN) {
+  (void)vel;
   __shared__ float4 tile[256];
   const float eps2 = params[0], gconst = params[1];
   const int n = (int)params[2];
@@ -52,15 +54,11 @@ extern "C" __global__ __launch_bounds__(256) void cek_nbody_f32(const float4* __
   acc[i1] = make_float4(gconst * ax.y, gconst * ay.y, gconst * az.y, 0.f);
 }
 
-// Leapfrog kick-drift: v += a·dt; x += v·dt  (one body per work item).
-// params: {softening², G, n, dt}
-extern "C" __global__ __launch_bounds__(256) void cek_nbody_integrate_f32(float4* __restrict__ pos,
-                                                                       float4* __restrict__ vel,
-                                                                       const float4* __restrict__ acc,
-                                                                       const float* __restrict__ params,
-                                                                       CEK_HIDDEN) {
-  const long long i = cek_global_id();
-  const float dt = params[3];
+// Leapfrog kick-drift: v += a·dt; x += v·dt for the same two bodies per
+// work item as cek_nbody_f32, so both kernels run in one compute() on the
+// same balanced range (same argument list).  params: {softening², G, n, dt}
+__device__ __forceinline__ void kick_drift(float4* pos, float4* vel, const float4* acc, long long i,
+                                           float dt) {
   float4 p = pos[i], v = vel[i];
   const float4 a = acc[i];
   v.x += a.x * dt;
@@ -73,16 +71,32 @@ extern "C" __global__ __launch_bounds__(256) void cek_nbody_integrate_f32(float4
   vel[i] = v;
 }
 
-// Per-group partial kinetic + (softened) potential-free energy diagnostic:
-// energy[g] = Σ ½ m |v|² over the group's bodies.
+extern "C" __global__ __launch_bounds__(256) void cek_nbody_integrate_f32(float4* __restrict__ pos,
+                                                                       float4* __restrict__ vel,
+                                                                       const float4* __restrict__ acc,
+                                                                       const float* __restrict__ params,
+                                                                       CEK_HIDDEN) {
+  const long long w = cek_global_id();
+  const int L = blockDim.x;
+  const long long i0 = (w / L) * 2 * L + (w % L);
+  const float dt = params[3];
+  kick_drift(pos, vel, acc, i0, dt);
+  kick_drift(pos, vel, acc, i0 + L, dt);
+}
+
+// Per-group kinetic energy diagnostic: energy[g] = Σ ½ m |v|² over the
+// group's 2·L bodies (same work-item mapping as above).
 extern "C" __global__ __launch_bounds__(256) void cek_nbody_energy_f32(const float4* __restrict__ pos,
                                                                      const float4* __restrict__ vel,
                                                                      float* __restrict__ energy,
                                                                      CEK_HIDDEN) {
   __shared__ float ws[4];
-  const long long i = cek_global_id();
-  const float4 p = pos[i], v = vel[i];
-  float e = 0.5f * p.w * (v.x * v.x + v.y * v.y + v.z * v.z);
+  const long long w = cek_global_id();
+  const int L = blockDim.x;
+  const long long i0 = (w / L) * 2 * L + (w % L), i1 = i0 + L;
+  const float4 p0 = pos[i0], v0 = vel[i0], p1 = pos[i1], v1 = vel[i1];
+  float e = 0.5f * p0.w * (v0.x * v0.x + v0.y * v0.y + v0.z * v0.z) +
+            0.5f * p1.w * (v1.x * v1.x + v1.y * v1.y + v1.z * v1.z);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = e;

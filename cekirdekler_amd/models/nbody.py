@@ -1,7 +1,7 @@
 """All-pairs N-body simulation on the AOT CDNA4 kernels.
 
-The body range is split across devices by the load balancer (compute id 1
-for forces, 2 for integration).  Every device needs every position for the
+The body range is split across devices by the load balancer; one compute()
+runs the force kernel and the kick-drift kernel on the same balanced range.  Every device needs every position for the
 force pass, so after each step the position slices are made coherent again:
 
 * ``resident=True`` (MI355X-native): positions stay in device memory and each
@@ -52,7 +52,6 @@ class NBodySimulation:
         self.params = ClArray(np.array([eps * eps, g, float(n), dt], np.float32))
         self.params.write = False
         self.steps = 0
-        self._flags_force()
 
     @property
     def interactions_per_step(self) -> float:
@@ -62,43 +61,44 @@ class NBodySimulation:
     def flops_per_step(self) -> float:
         return FLOP_PER_INTERACTION * self.interactions_per_step
 
-    def _flags_force(self) -> None:
-        # force pass: all positions in, this device's accelerations out
+    def _flags(self) -> None:
         first = self.steps == 0
+        for a in (self.pos, self.vel, self.acc):
+            a.elements_per_work_item = 8  # 2 bodies × float4 per work item
+            a.partial_read = False
+        # positions: every device reads all of them
         self.pos.read = first or not self.resident
-        self.pos.partial_read = False
-        self.pos.write = False
+        self.pos.write = not self.resident
+        self.vel.partial_read = not self.resident or first
+        self.vel.read = False
+        self.vel.write = not self.resident
         self.acc.read = False
-        self.acc.write = not self.resident
-        self.acc.elements_per_work_item = 8  # 2 bodies × float4 per work item
+        self.acc.write = False
         self.params.read = first or not self.resident
 
-    def forces(self, compute_id: int = 1) -> None:
-        self._flags_force()
-        self.pos.next_param(self.acc, self.params).compute(self.cr, compute_id, "cek_nbody_f32", self.n // 2, L)
+    def forces(self, compute_id: int = 3) -> None:
+        """Accelerations only (no integration)."""
+        self._flags()
+        self.pos.write = False
+        self.acc.write = True
+        self.pos.next_param(self.vel, self.acc, self.params).compute(self.cr, compute_id, "cek_nbody_f32",
+                                                                    self.n // 2, L)
 
-    def integrate(self, compute_id: int = 2) -> None:
-        for a in (self.pos, self.vel, self.acc):
-            a.elements_per_work_item = 4
-            a.read = False
-            a.partial_read = not self.resident
-            a.write = not self.resident
-        self.acc.write = False
-        self.acc.partial_read = False
-        self.params.read = False
+    def step(self, compute_id: int = 1) -> None:
+        """Forces + kick-drift for every body, range-partitioned; then the
+        position slices are made coherent on every device."""
+        self._flags()
         self.pos.next_param(self.vel, self.acc, self.params).compute(
-            self.cr, compute_id, "cek_nbody_integrate_f32", self.n, L)
+            self.cr, compute_id, "cek_nbody_f32 cek_nbody_integrate_f32", self.n // 2, L)
         if self.resident and self.cr.cores.num_devices > 1:
             self.cr.cores.share_slices(compute_id, self.pos._spec(), L)
-
-    def step(self) -> None:
-        self.forces()
-        self.integrate()
         self.steps += 1
 
     def download(self) -> None:
         """Bring device-resident state to the host (device 0 holds every
         slice of pos after share_slices; vel/acc slices per device)."""
+        if not self.resident:
+            return  # host arrays already hold every slice
         c = self.cr.cores
         self.cr.download(self.pos, 0)
         for name in ("vel", "acc"):
@@ -106,9 +106,9 @@ class NBodySimulation:
             if c.num_devices == 1:
                 self.cr.download(arr, 0)
                 continue
-            cid = 2 if name == "vel" else 1
+            cid = 1
             refs, rng = self.cr.references(cid), self.cr.ranges(cid)
-            e = 4 if name == "vel" else 8
+            e = 8
             full = np.empty_like(arr.array)
             keep = arr.array.copy()
             for d in range(c.num_devices):

@@ -111,6 +111,7 @@ def test_nbody_forces_match_fp64():
 
     sim = NBodySimulation(4096, devices=_gpu()[0], resident=False)
     sim.forces()
+    sim.cr.sync()
     got = sim.acc.array.reshape(-1, 4)[:, :3]
     ref = nbody_accel_reference(sim.pos.array, 0.01 ** 2)
     err = np.abs(got - ref).max() / np.abs(ref).max()
