@@ -29,7 +29,7 @@ __global__ void saxpy(float* x, const int* it) {
 ap = argparse.ArgumentParser()
 ap.add_argument("--tasks", type=int, default=256)
 ap.add_argument("--gpus", type=int, default=0)
-ap.add_argument("--logical", type=int, default=4, help="logical devices per GPU when only one GPU")
+ap.add_argument("--logical", type=int, default=2, help="logical devices per GPU when only one GPU")
 ap.add_argument("--queues", type=int, default=3)
 a = ap.parse_args()
 g = ck.ClPlatforms.all().gpus()
@@ -39,11 +39,11 @@ if ng == 1 and a.logical > 1:
     for _ in range(a.logical - 1):
         devs = devs + g[0]
 rng = np.random.default_rng(3)
-N = 1 << 20
+N = 1 << 22
 tasks = []
 for t in range(a.tasks):
     kind = "spin" if t % 4 else "saxpy"
-    iters = int(rng.choice([64, 128, 256, 512]))
+    iters = int(rng.choice([256, 512, 1024, 2048]))
     x = ck.ClArray(np.ones(N, np.float32))
     x.read = x.write = False
     it = ck.ClArray(np.array([iters], np.int32))

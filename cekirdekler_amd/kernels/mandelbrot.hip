@@ -17,24 +17,33 @@ extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_f32(const float
   const int y = (int)(p0 / W), x = (int)(p0 % W);
   const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
   const float ci = y0 + y * dy;
-  f32x2 cra = {x0 + x * dx, x0 + (x + 1) * dx};
-  f32x2 crb = {x0 + (x + 2) * dx, x0 + (x + 3) * dx};
-  f32x2 zra = {0.f, 0.f}, zia = {0.f, 0.f}, zrb = {0.f, 0.f}, zib = {0.f, 0.f};
-  int na0 = max_iter, na1 = max_iter, nb0 = max_iter, nb1 = max_iter;
+  const f32x2 cra = {x0 + x * dx, x0 + (x + 1) * dx};
+  const f32x2 crb = {x0 + (x + 2) * dx, x0 + (x + 3) * dx};
   const f32x2 cic = {ci, ci};
-  for (int it = 0; it < max_iter; ++it) {
-    f32x2 zr2a = zra * zra, zi2a = zia * zia, zr2b = zrb * zrb, zi2b = zib * zib;
-    f32x2 ma = zr2a + zi2a, mb = zr2b + zi2b;
-    if (ma.x > 4.f && na0 == max_iter) na0 = it;
-    if (ma.y > 4.f && na1 == max_iter) na1 = it;
-    if (mb.x > 4.f && nb0 == max_iter) nb0 = it;
-    if (mb.y > 4.f && nb1 == max_iter) nb1 = it;
-    if ((na0 < max_iter) & (na1 < max_iter) & (nb0 < max_iter) & (nb1 < max_iter)) break;
-    f32x2 tza = zra * zia, tzb = zrb * zib;
-    zia = tza + tza + cic;
-    zib = tzb + tzb + cic;
-    zra = zr2a - zi2a + cra;
-    zrb = zr2b - zi2b + crb;
+  f32x2 zra = {0.f, 0.f}, zia = {0.f, 0.f}, zrb = {0.f, 0.f}, zib = {0.f, 0.f};
+  // Escape counting without per-iteration branches: a pixel's count grows
+  // while |z|² <= 4; once |z| > max(2, |c|) it never returns (inf/NaN compare
+  // false), so the count equals the first escape iteration.  The escape
+  // test that ends the loop runs once per 8 unrolled iterations.
+  int na0 = 0, na1 = 0, nb0 = 0, nb1 = 0;
+  for (int it = 0; it < max_iter; it += 8) {
+    f32x2 ma, mb;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const f32x2 zr2a = zra * zra, zi2a = zia * zia, zr2b = zrb * zrb, zi2b = zib * zib;
+      ma = zr2a + zi2a;
+      mb = zr2b + zi2b;
+      na0 += ma.x <= 4.f;
+      na1 += ma.y <= 4.f;
+      nb0 += mb.x <= 4.f;
+      nb1 += mb.y <= 4.f;
+      const f32x2 ta = zra * zia, tb = zrb * zib;
+      zia = ta + ta + cic;
+      zib = tb + tb + cic;
+      zra = zr2a - zi2a + cra;
+      zrb = zr2b - zi2b + crb;
+    }
+    if (!(ma.x <= 4.f) && !(ma.y <= 4.f) && !(mb.x <= 4.f) && !(mb.y <= 4.f)) break;
   }
-  out[q] = make_int4(na0, na1, nb0, nb1);
+  out[q] = make_int4(min(na0, max_iter), min(na1, max_iter), min(nb0, max_iter), min(nb1, max_iter));
 }

@@ -172,14 +172,21 @@ def nbody(n: int = 8 * 1024, devices: Optional[ClDevices] = None, stream: bool =
     if not check:
         cr.dispose()
         return 0
+    # The reference compares against a float32 host loop in the same order
+    # with an absolute 0.01; against a float64 reference the float32
+    # summation error scales with Σ|terms| (close pairs give huge terms), so
+    # the bound is 0.01 + 2e-6·Σ|terms|.
     err = 0
     for s in range(0, n, 1024):
         dx = x[s:s + 1024, None].astype(np.float64) - x[None, :]
         dy = y[s:s + 1024, None].astype(np.float64) - y[None, :]
         r = np.sqrt(dx * dx + dy * dy + 0.0001)
         inv = 1.0 / (r * r * r)
-        hfx, hfy = (dx * inv).sum(1), (dy * inv).sum(1)
-        bad = (np.abs(hfx - fx.array[s:s + 1024]) > 0.01) | (np.abs(hfy - fy.array[s:s + 1024]) > 0.01)
+        tx, ty = dx * inv, dy * inv
+        hfx, hfy = tx.sum(1), ty.sum(1)
+        bx = 0.01 + 2e-6 * np.abs(tx).sum(1)
+        by = 0.01 + 2e-6 * np.abs(ty).sum(1)
+        bad = (np.abs(hfx - fx.array[s:s + 1024]) > bx) | (np.abs(hfy - fy.array[s:s + 1024]) > by)
         err += int(bad.sum())
     cr.dispose()
     return 1 if err else 0
