@@ -61,7 +61,9 @@ def init_distributed(backend: Optional[str] = None) -> DistContext:
     os.environ.setdefault("MASTER_PORT", "29500")
     if not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if (gpu_available() and torch.cuda.is_available()) else "gloo"
+            # RCCL needs one GPU per rank; ranks sharing a GPU use gloo
+            backend = "nccl" if (gpu_available() and torch.cuda.is_available()
+                                 and torch.cuda.device_count() >= ctx.world) else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(ctx.local_rank)
         dist.init_process_group(backend=backend, rank=ctx.rank, world_size=ctx.world)
