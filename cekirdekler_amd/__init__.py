@@ -11,12 +11,13 @@ from .arrays import (BFLOAT16, ClArray, ClBf16Array, ClByteArray, ClCharArray, C
                      ClFloatArray, ClIntArray, ClLongArray, ClParameterGroup, ClUIntArray, FastArr)
 from .cruncher import (PIPELINE_DRIVER, PIPELINE_EVENT, AcceleratorType, ClComputeError,
                        ClNumberCruncher, Cores)
+from .aux_functions import ClBuiltInAuxilliaryFunctions
 from .hardware import ClDevice, ClDevices, ClPlatform, ClPlatforms
 
 __version__ = "0.1.0"
 
 __all__ = [
-    "AcceleratorType", "BFLOAT16", "CekError", "ClArray", "ClBf16Array", "ClByteArray", "ClCharArray",
+    "AcceleratorType", "BFLOAT16", "ClBuiltInAuxilliaryFunctions", "CekError", "ClArray", "ClBf16Array", "ClByteArray", "ClCharArray",
     "ClComputeError", "ClDevice", "ClDevices", "ClDoubleArray", "ClFloatArray", "ClIntArray",
     "ClLongArray", "ClNumberCruncher", "ClParameterGroup", "ClPlatform", "ClPlatforms", "ClUIntArray",
     "Cores", "FastArr", "PIPELINE_DRIVER", "PIPELINE_EVENT", "cek", "gpu_available",

@@ -1,0 +1,231 @@
+"""GPU tier for the framework features beyond plain compute(): the wave
+example on GPU and on GPU+CPU, auxiliary prelude (wave64 reduction),
+zero-copy arrays, enqueue mode with stream markers, repeat + sync kernel,
+the device→device ClPipeline and the single-GPU multi-stream DevicePipeline,
+the task pool, checkpoint/resume and the reference type matrix."""
+import threading
+
+import numpy as np
+import pytest
+
+import cekirdekler_amd as ck
+
+pytestmark = pytest.mark.gpu
+
+SRC = """
+__global__ void inc(float* x) { x[get_global_id(0)] += 1.0f; }
+__global__ void count(float* x, int* c) { if (get_global_id(0) == 0) c[0] += 1; }
+__global__ void scale(const float* a, float* x) { long long i = get_global_id(0); x[i] = a[0] * x[i]; }
+"""
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    return ck.ClPlatforms.all().gpus()
+
+
+@pytest.fixture(scope="module")
+def cr(gpu):
+    c = ck.ClNumberCruncher(gpu[0] + gpu[0], SRC)
+    assert c.error_code() == 0, c.error_message()
+    yield c
+    c.dispose()
+
+
+def test_wave_gpu_and_gpu_plus_cpu(gpu):
+    from cekirdekler_amd.models.wave import WaveSurface, grid_mesh
+
+    base, nrm = grid_mesh(224, 256)                 # the Kamera.cs mesh: 57,344 vertices
+    for devs in (gpu[0], gpu[0] + ck.ClPlatforms.all().cpus(True)):
+        w = WaveSurface(base, nrm, devices=devs)
+        for _ in range(8):
+            v = w.update()
+        ref = w.reference()
+        for c in "xyz":
+            # device sin/sqrt are not correctly rounded: 2 ulp-scale slack
+            np.testing.assert_allclose(v[c], ref[c], atol=2e-6)
+        assert sum(w.cr.ranges(1)) == w.range
+        w.cr.dispose()
+
+
+def test_aux_wave_sum_gpu(gpu):
+    aux = ck.ClBuiltInAuxilliaryFunctions(wave_sum=True, block_sum=True)
+    src = aux.wrap("""
+    __global__ void k(const float* x, float* w, float* b) {
+        __shared__ float scratch[256];
+        long long i = get_global_id(0);
+        float s = cek_wave_sum(x[i]);
+        if ((get_local_id(0) & 63) == 0) w[i / 64] = s;
+        float t = cek_block_sum(x[i], scratch);
+        if (get_local_id(0) == 0) b[cek_global_group_id()] = t;
+    }""")
+    c = ck.ClNumberCruncher(gpu[0], src)
+    assert c.error_code() == 0, c.error_message()
+    n = 1 << 16
+    x = ck.ClArray(np.random.default_rng(0).random(n).astype(np.float32)); x.write = False
+    w = ck.ClArray(np.zeros(n // 64, np.float32)); w.read = False
+    w.elements_per_group = 4
+    b = ck.ClArray(np.zeros(n // 256, np.float32)); b.read = False
+    b.elements_per_group = 1
+    x.next_param(w, b).compute(c, 1, "k", n, 256)
+    np.testing.assert_allclose(w.array, x.array.reshape(-1, 64).sum(1), rtol=1e-5)
+    np.testing.assert_allclose(b.array, x.array.reshape(-1, 256).sum(1), rtol=1e-5)
+    c.dispose()
+
+
+def test_zero_copy_arrays(cr):
+    n = 1 << 18
+    a = ck.ClArray(np.array([3.0], np.float32)); a.write = False
+    x = ck.ClArray(np.arange(n, dtype=np.float32))     # host numpy memory, registered
+    x.zero_copy = True
+    f = ck.ClArray(n, np.float32)                       # pinned FastArr
+    f.zero_copy = True
+    f.array[:] = 2
+    for _ in range(2):
+        a.next_param(x).compute(cr, 11, "scale", n, 256)
+        a.next_param(f).compute(cr, 12, "scale", n, 256)
+    np.testing.assert_array_equal(x.array, 9 * np.arange(n, dtype=np.float32))
+    np.testing.assert_array_equal(f.array, 18.0)
+
+
+@pytest.mark.parametrize("async_enqueue", [False, True])
+def test_enqueue_mode_markers(cr, async_enqueue):
+    x = ck.ClArray(np.zeros(1 << 16, np.float32))
+    cr.fine_grained_queue_control = True
+    cr.enqueue_mode_async_enable = async_enqueue
+    cr.enqueue_mode = True
+    for _ in range(20):
+        x.compute(cr, 13, "inc", 1 << 16, 256)
+    cr.enqueue_mode = False                             # drains every queue
+    cr.enqueue_mode_async_enable = False
+    cr.fine_grained_queue_control = False
+    np.testing.assert_array_equal(x.array, 20.0)
+    assert cr.count_markers_remaining() == 0
+    assert cr.count_markers_reached() >= 20
+
+
+def test_repeat_with_sync_kernel(cr):
+    x = ck.ClArray(np.zeros(4096, np.float32))
+    c = ck.ClArray(np.zeros(1, np.int32))
+    c.write_all = True
+    cr.repeat_count = 7
+    cr.repeat_kernel_name = "count"
+    try:
+        x.next_param(c).compute(cr, 14, "inc", 4096, 256)
+    finally:
+        cr.repeat_count = 1
+        cr.repeat_kernel_name = ""
+    np.testing.assert_array_equal(x.array, 7.0)
+    # the sync kernel runs on each device once per repeat
+    assert c.array[0] in (7, 14)
+
+
+def test_cl_pipeline_gpu(gpu):
+    from cekirdekler_amd.parallel.pipeline import ClPipelineStage
+
+    N = 1 << 16
+    K1 = "__global__ void add1(const float* x, float* y) { long long i = get_global_id(0); y[i] = x[i] + 1.0f; }"
+    K2 = "__global__ void mul2(const float* y, float* z) { long long i = get_global_id(0); z[i] = y[i] * 2.0f; }"
+
+    def stage(src, name, ins, outs):
+        s = ClPipelineStage()
+        s.add_devices(gpu[0])
+        s.add_kernels(src, name, [N], [256])
+        s.add_input_buffers(*ins)
+        s.add_output_buffers(*outs)
+        return s
+
+    x, y1, y2, z = (np.zeros(N, np.float32) for _ in range(4))
+    s1 = stage(K1, "add1", [x], [y1])
+    s2 = stage(K2, "mul2", [y2], [z])
+    s1.prepend_to_stage(s2)
+    pipe = s1.make_pipeline()
+    res = np.zeros(N, np.float32)
+    seen = []
+    for p in range(10):
+        if pipe.push_data([np.full(N, float(p), np.float32)], [res]):
+            assert np.all(res == res[0])
+            seen.append(float(res[0]))
+    assert seen == [(p + 1) * 2 for p in range(len(seen))] and len(seen) == 6
+    pipe.dispose()
+
+
+def test_device_pipeline_gpu(gpu):
+    from cekirdekler_amd.parallel.pipeline import (DevicePipeline, DevicePipelineArray,
+                                                   DevicePipelineArrayType, DevicePipelineStage)
+
+    N = 1 << 16
+    src = ("__global__ void add1(const float* x, float* y) { long long i = get_global_id(0); y[i] = x[i] + 1.0f; }\n"
+           "__global__ void sub3(const float* z, float* w) { long long i = get_global_id(0); w[i] = z[i] - 3.0f; }")
+    dp = DevicePipeline(gpu[0], src)
+    inp = DevicePipelineArray(DevicePipelineArrayType.INPUT, np.zeros(N, np.float32))
+    mid = DevicePipelineArray(DevicePipelineArrayType.TRANSITION, np.zeros(N, np.float32))
+    out = DevicePipelineArray(DevicePipelineArrayType.OUTPUT, np.zeros(N, np.float32))
+    a = DevicePipelineStage("add1", N, 256)
+    a.bind_array(inp)
+    a.bind_array(mid)
+    b = DevicePipelineStage("sub3", N, 256)
+    b.bind_array(mid)
+    b.bind_array(out)
+    dp.add_stage(a)
+    dp.add_stage(b)
+    got = []
+    for p in range(6):
+        dp.input_buffer(inp).array[:] = p
+        dp.feed()
+        got.append(float(dp.output_buffer(out).array[0]))
+    assert got[3:] == [(p + 1) - 3 for p in range(1, 4)]
+    dp.dispose()
+
+
+def test_task_pool_gpu(gpu):
+    from cekirdekler_amd.parallel.pool import ClDevicePool, ClDevicePoolType, ClTaskPool
+
+    src = "__global__ void fill(float* x, float* v) { x[get_global_id(0)] = v[0]; }"
+    pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, src, True, 8)
+    pool.add_device(gpu[0] + gpu[0])
+    tp = ClTaskPool()
+    arrays, done = [], []
+    lock = threading.Lock()
+    for i in range(64):
+        x = ck.ClArray(np.zeros(1 << 14, np.float32))
+        v = ck.ClArray(np.array([float(i)], np.float32)); v.write = False
+        t = x.next_param(v).task(1, "fill", 1 << 14, 256)
+        t.set_callback(lambda i=i: (lock.acquire(), done.append(i), lock.release()))
+        tp.feed(t)
+        arrays.append(x)
+    pool.enqueue_task_pool(tp)
+    pool.finish()
+    for i, x in enumerate(arrays):
+        np.testing.assert_array_equal(x.array, float(i))
+    assert sorted(done) == list(range(64))
+    pool.dispose()
+
+
+def test_checkpoint_resume_gpu(gpu, tmp_path):
+    from cekirdekler_amd.utils import checkpoint
+
+    c1 = ck.ClNumberCruncher(gpu[0] + gpu[0], SRC)
+    c1.set_time_scale(1, 3.0)
+    x = ck.ClArray(np.zeros(1 << 16, np.float32))
+    for _ in range(6):
+        x.compute(c1, 21, "inc", 1 << 16, 256)
+    path = tmp_path / "ck.bin"
+    checkpoint.save(str(path), {"x": x}, c1)
+    ranges = c1.ranges(21)
+    c1.dispose()
+    c2 = ck.ClNumberCruncher(gpu[0] + gpu[0], SRC)
+    arrays = checkpoint.load(str(path), cruncher=c2)
+    assert c2.ranges(21) == ranges
+    np.testing.assert_array_equal(arrays["x"], 6.0)
+    y = ck.ClArray(arrays["x"].copy())
+    y.compute(c2, 21, "inc", 1 << 16, 256)
+    np.testing.assert_array_equal(y.array, 7.0)
+    c2.dispose()
+
+
+def test_type_matrix_gpu(gpu):
+    from cekirdekler_amd.utils.tester import type_matrix
+
+    total, fails = type_matrix(gpu[0] + gpu[0], verbose=True)
+    assert total == 8 * 2 * 2 * 3 * 3 and fails == 0

@@ -1,0 +1,73 @@
+"""Wave-equation example (Kamera.cs:188-284) and the auxiliary-function
+prelude (ClBuiltInAuxilliaryFunctions.cs:28-47) on the host CPU device."""
+import numpy as np
+import pytest
+
+from cekirdekler_amd import ClArray, ClBuiltInAuxilliaryFunctions, ClNumberCruncher, ClPlatforms
+from cekirdekler_amd.models.wave import VERTEX, WaveSurface, grid_mesh, wave_reference
+
+
+@pytest.fixture(scope="module")
+def cpu():
+    return ClPlatforms.all().cpus(True)
+
+
+def test_wave_matches_host_loop(cpu):
+    base, nrm = grid_mesh(100, 37)            # 3700 vertices: not a multiple of 64
+    w = WaveSurface(base, nrm, devices=cpu)
+    for _ in range(6):
+        v = w.update()
+    ref = w.reference()
+    for c in "xyz":
+        np.testing.assert_allclose(v[c], ref[c], atol=1e-6)
+    assert np.abs(ref["z"]).max() > 0          # the surface actually moved
+    # padded tail untouched (the id < arguments[4] guard)
+    assert np.all(w.xyzo.array.view(VERTEX)[w.n:]["z"] == 0)
+
+
+def test_wave_reference_formula():
+    base, nrm = grid_mesh(8, 8)
+    out = wave_reference(base, nrm, 0.3, 0.5, base["x"][0], base["y"][0])
+    r = np.hypot(base["x"] - base["x"][0], base["y"] - base["y"][0])
+    np.testing.assert_allclose(out["z"], 0.02 * 0.3 * np.sin(40 * 0.5 + 100 * r), atol=1e-6)
+    np.testing.assert_array_equal(out["x"], base["x"])
+
+
+def test_aux_prelude_selection():
+    aux = ClBuiltInAuxilliaryFunctions()
+    assert str(aux) == ""
+    aux.exampleFunction = True                 # reference spelling
+    assert aux.example_function and "exampleFunction" in str(aux)
+    with pytest.raises(AttributeError):
+        aux.no_such_function = True
+
+
+def test_aux_functions_run_on_cpu(cpu):
+    aux = ClBuiltInAuxilliaryFunctions(example_function=True, block_sum=True, bf16=True, lerp=True)
+    src = aux.wrap("""
+    __global__ void k(const float* x, float* sums, int* ex, unsigned short* h, float* l) {
+        __shared__ float scratch[64];
+        long long i = get_global_id(0);
+        float s = cek_block_sum(x[i], scratch);
+        if (get_local_id(0) == 0) sums[cek_global_group_id()] = s;
+        ex[i] = exampleFunction((int)i, 1);
+        h[i] = cek_f32_to_bf16(x[i]);
+        l[i] = cek_lerp(0.f, x[i], 0.5f);
+    }""")
+    cr = ClNumberCruncher(cpu, src)
+    assert cr.error_code() == 0, cr.error_message()
+    n = 256
+    x = ClArray(np.linspace(-2, 2, n).astype(np.float32)); x.write = False
+    sums = ClArray(np.zeros(n // 64, np.float32)); sums.read = False
+    sums.elements_per_group = 1
+    ex = ClArray(np.zeros(n, np.int32)); ex.read = False
+    h = ClArray(np.zeros(n, np.uint16)); h.read = False
+    lv = ClArray(np.zeros(n, np.float32)); lv.read = False
+    x.next_param(sums, ex, h, lv).compute(cr, 1, "k", n, 64)
+    np.testing.assert_allclose(sums.array, x.array.reshape(-1, 64).sum(1), rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(ex.array, np.arange(n) + 1)
+    bits = x.array.view(np.uint32)
+    rne = ((bits + 0x7FFF + ((bits >> 16) & 1)) >> 16).astype(np.uint16)
+    np.testing.assert_array_equal(h.array, rne)
+    np.testing.assert_allclose(lv.array, x.array * 0.5)
+    cr.dispose()
