@@ -488,9 +488,12 @@ class ClArray:
         arr = self.array
         if self.zero_copy and self._fast is None and not self._registered:
             self._registered = bool(cek.host_register(arr.ctypes.data, arr.nbytes))
+        # zero-copy only when the GPU can map the memory (pinned FastArr or a
+        # successful registration); otherwise the array is copied as usual
+        zc = bool(self.zero_copy) and (self._fast is not None or self._registered)
         spec = cek.ArraySpec(self._uid, arr.ctypes.data, arr.nbytes, arr.itemsize,
                              self._read, self._partial, self._write, self._write_all,
-                             self._ro, self._wo, bool(self.zero_copy), int(self.elements_per_work_item),
+                             self._ro, self._wo, zc, int(self.elements_per_work_item),
                              int(self.elements_per_group))
         self._spec_cache = (key, spec)
         return spec

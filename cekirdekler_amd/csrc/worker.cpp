@@ -114,7 +114,11 @@ void Worker::set_device() const {
 void* Worker::buffer(const ArraySpec& a) {
   if (!gpu()) return a.host;
   if (a.zc) {
-    host_register(a.host, a.bytes);
+    // The array owns its registration (ClArray registers once, unregisters
+    // on dispose); registering here per launch would leak refcounts and leave
+    // a stale mapping behind once the host memory is freed.
+    if (!host_is_pinned(a.host))
+      throw Error("zero-copy array is neither pinned nor registered with HIP");
     std::lock_guard<std::mutex> g(buf_mu_);
     zc_[a.uid] = true;
     return host_device_ptr(a.host);

@@ -1,7 +1,9 @@
 """Mandelbrot renderer on the AOT CDNA4 kernel (BASELINE config
 "Mandelbrot 4096×4096, 1×MI355X, event-driven read/compute/write pipeline").
 
-The image is one 1-D range of quads (4 pixels per work item); with
+The image is one 1-D range of work items of ``ppw`` pixels each (4 fixed
+pixels for "quad"; 8 or 16 for the wave-pooled kernels, whose waves drain a
+pool of 64·ppw pixels with two pixels in flight per lane); with
 ``pipeline=True`` each device's slice is cut into ``blobs`` chunks whose
 kernel runs overlap the previous chunks' device→host copies (the reference's
 event-driven pipeline, Cores.cs:1197-1367).
@@ -16,12 +18,21 @@ from ..ops.library import library
 
 FLOP_PER_ITER = 8
 
+# kernel variants: name -> (library kernel, pixels per work item)
+KERNELS = {
+    "quad": ("cek_mandelbrot_f32", 4),          # 4 fixed pixels per work item
+    "pool8": ("cek_mandelbrot_pool8_f32", 8),    # wave-pooled, 512-pixel pools
+    "pool16": ("cek_mandelbrot_pool16_f32", 16),  # wave-pooled, 1024-pixel pools
+}
+
 
 class MandelbrotRenderer:
     def __init__(self, width: int = 4096, height: int = 4096, max_iter: int = 256,
-                 view=(-2.0, -1.5, 3.0, 3.0), devices=None, cruncher: ClNumberCruncher | None = None):
-        if (width * height) % 1024:
-            raise ValueError("width*height must be a multiple of 1024")
+                 view=(-2.0, -1.5, 3.0, 3.0), devices=None, cruncher: ClNumberCruncher | None = None,
+                 kernel: str = "pool16"):
+        self.kernel, self.ppw = KERNELS[kernel]
+        if (width * height) % (256 * self.ppw) or width * height >= 2 ** 31:
+            raise ValueError(f"width*height must be a multiple of {256 * self.ppw} and below 2^31")
         x0, y0, w, h = view
         self.width, self.height, self.max_iter = width, height, max_iter
         self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library("mandelbrot"))
@@ -31,14 +42,14 @@ class MandelbrotRenderer:
             a.write = False
         self.out = ClArray(width * height, np.int32)
         self.out.read = False
-        self.out.elements_per_work_item = 4
-        self.global_range = width * height // 4
+        self.out.elements_per_work_item = self.ppw
+        self.global_range = width * height // self.ppw
         self._last_id = None
 
     def render(self, compute_id: int = 1, pipeline: bool = True, blobs: int = 8,
                pipeline_type: bool = PIPELINE_EVENT) -> np.ndarray:
         self.view.next_param(self.size, self.out).compute(
-            self.cr, compute_id, "cek_mandelbrot_f32", self.global_range, 256, 0, pipeline,
+            self.cr, compute_id, self.kernel, self.global_range, 256, 0, pipeline,
             pipeline_type, blobs)
         self._last_id = compute_id
         return self.out.array.reshape(self.height, self.width)
@@ -48,8 +59,8 @@ class MandelbrotRenderer:
         refs, rng = self.cr.references(cid), self.cr.ranges(cid)
         base = self.cr._cores.global_base
         n = self.cr._cores.num_devices
-        lo = refs[base] * 4
-        hi = (refs[base + n - 1] + rng[base + n - 1]) * 4
+        lo = refs[base] * self.ppw
+        hi = (refs[base + n - 1] + rng[base + n - 1]) * self.ppw
         return slice(lo, hi)
 
     def flops(self) -> float:

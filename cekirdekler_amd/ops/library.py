@@ -17,7 +17,7 @@ LIBRARY = {
     "sgemm_bf16": ["cek_sgemm_bf16_256x256", "cek_sgemm_bf16_256x256p", "cek_sgemm_bf16_256x256pp", "cek_sgemm_bf16_256x256ps",
                    "cek_sgemm_bf16_256x128", "cek_sgemm_bf16_256x128p", "cek_sgemm_bf16_256x128pp", "cek_sgemm_bf16_256x128ps",
                    "cek_sgemm_bf16_128x128", "cek_sgemm_bf16_128x128p"],
-    "mandelbrot": ["cek_mandelbrot_f32"],
+    "mandelbrot": ["cek_mandelbrot_f32", "cek_mandelbrot_pool16_f32", "cek_mandelbrot_pool8_f32"],
     "nbody": ["cek_nbody_f32", "cek_nbody_integrate_f32", "cek_nbody_energy_f32"],
     "reduce": ["cek_reduce_sum_f32", "cek_reduce_sum_f32_final"],
     "stream": ["cek_saxpy_f32", "cek_copy_u8", "cek_vec_add_f32"],

@@ -79,10 +79,11 @@ def test_gemm_two_logical_devices_balanced():
     assert np.abs(c - ref).max() < 5e-3 * np.abs(ref).max()
 
 
-def test_mandelbrot_event_pipeline_matches_numpy():
+@pytest.mark.parametrize("kernel", ["quad", "pool8", "pool16"])
+def test_mandelbrot_event_pipeline_matches_numpy(kernel):
     from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
 
-    m = MandelbrotRenderer(512, 256, max_iter=64, devices=_gpu()[0])
+    m = MandelbrotRenderer(512, 256, max_iter=64, devices=_gpu()[0], kernel=kernel)
     img = m.render(pipeline=True, blobs=4)
     ref = m.reference()
     mism = np.mean(img != ref)

@@ -14,7 +14,7 @@ for spec in "$@"; do
   rc=$?
   echo "=== $name rc=$rc elapsed=$(( $(date +%s) - start ))s"
   tail -5 "gpurun_out/$name.log"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+  if [ $rc -ne 0 ] && { [ $rc -ne 1 ] || [ -n "$CEK_STOP_ON_FAIL" ]; }; then
     echo "=== stopping: $name exited with $rc"
     exit $rc
   fi
