@@ -88,6 +88,17 @@ def kernel_sources() -> list[str]:
     return sorted(os.path.join(KDIR, f) for f in os.listdir(KDIR) if f.endswith(".hip"))
 
 
+def _file_flags(src: str) -> list[str]:
+    """Per-file compiler flags from a ``// cek-flags: ...`` line in the source."""
+    flags: list[str] = []
+    with open(src) as f:
+        for line in f:
+            line = line.strip()
+            if line.startswith("// cek-flags:"):
+                flags += line.split(":", 1)[1].split()
+    return flags
+
+
 def build_kernels(force: bool = False, jobs: int = 8) -> list[str]:
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     if not os.path.exists(hipcc):
@@ -99,7 +110,7 @@ def build_kernels(force: bool = False, jobs: int = 8) -> list[str]:
         outs.append(out)
         if force or not _newer(out, [src] + inc_hdrs):
             todo.append([hipcc, "--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17",
-                         "-mcode-object-version=5", f"-I{KDIR}", src, "-o", out])
+                         "-mcode-object-version=5", f"-I{KDIR}", *_file_flags(src), src, "-o", out])
     if todo:
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
             list(ex.map(_run, todo))

@@ -504,6 +504,20 @@ void Cores::compute(const ComputeCall& c) {
     if (!workers_[0]->program().has(k)) throw Error("unknown kernel: " + k);
   if (!c.repeat_kernel.empty() && !workers_[0]->program().has(c.repeat_kernel))
     throw Error("unknown repeat kernel: " + c.repeat_kernel);
+  // Every kernel of a compute receives the same array list (Worker.cs:990-1021
+  // binds them positionally); a count mismatch would shift the hidden offset
+  // argument onto a pointer and make the kernel address wild memory.
+  {
+    const int nargs = static_cast<int>(c.arrays.size());
+    auto check = [&](const std::string& k) {
+      for (auto& sig : workers_[0]->program().kernels())
+        if (sig.name == k && sig.arity >= 0 && sig.arity != nargs)
+          throw Error("kernel " + k + " takes " + std::to_string(sig.arity) + " array parameter(s) but compute passes " +
+                      std::to_string(nargs));
+    };
+    for (auto& k : c.kernels) check(k);
+    if (!c.repeat_kernel.empty()) check(c.repeat_kernel);
+  }
   const int D = global_devices_;
   const int nloc = num_devices();
   const long long B = std::max(1, c.blobs);

@@ -516,10 +516,16 @@ std::shared_ptr<Program> Program::build(const DeviceInfo& dev, const std::string
       std::string n;
       while (std::getline(ss, n, ',')) {
         if (n.empty()) continue;
+        int arity = -1;  // "name:arity" declares the array-parameter count
+        auto colon = n.find(':');
+        if (colon != std::string::npos) {
+          arity = std::stoi(n.substr(colon + 1));
+          n = n.substr(0, colon);
+        }
         hipFunction_t f;
         CEK_HIP(hipModuleGetFunction(&f, m, n.c_str()));
         p->gpu_fns_[n] = f;
-        p->kernels_.push_back({n, -1});
+        p->kernels_.push_back({n, arity});
       }
     }
   } else {

@@ -2,108 +2,141 @@
 // particles"; the reference's test workload is the 2-D O(n²) force loop of
 // Tester.cs:7726-7743).
 //
-// pos  : float4 {x, y, z, m} per body     acc : float4 {ax, ay, az, 0}
-// params: {softening², G, n, 0}
+// cek-flags: -fno-slp-vectorize
 //
-// One work item = TWO bodies (i and i + half the group's span) so the inner
-// loop issues packed f32 ops (v_pk_fma_f32 / v_pk_mul_f32: 2 interactions
-// per VALU issue); the j loop streams the bodies through LDS in tiles of
-// blockDim bodies — every lane of a wave reads the same LDS address (a
-// broadcast, no bank conflicts) — and uses the hardware rsqrt.  20 FLOP per
-// interaction is the accounting convention.  Work items are absolute
-// (__cek_off), so the body range is load-balanced across devices like any
-// other compute().
+// pos  : float4 {x, y, z, m} per body     acc : float4 {ax, ay, az, 0}
+// params: {softening², G, n, dt}
+//
+// One work item = B bodies (B = 2 or 4): in workgroup g (256 work items) the
+// item with local id l owns bodies g·256·B + k·256 + l, k < B.  The j loop
+// streams all bodies through LDS in tiles of 256 (the next tile is fetched
+// into registers while the current one is consumed); every lane of a wave
+// reads the same LDS address (a broadcast, no bank conflicts) and applies it
+// to its B bodies.  The arithmetic is scalar on purpose (the file is built
+// with -fno-slp-vectorize): on CDNA4's SIMD-32 a wave64 v_fma_f32 issues in
+// 2 cycles, so v_pk_fma_f32 adds no FLOP rate, and the packed form forced
+// s_nop hazard padding around the (unpackable) v_rsq_f32.  Per interaction:
+// 3 sub, 3 fma (r²), rsq, 3 mul, 3 fma — 20 FLOP by the usual convention.
+// Work items are absolute (__cek_off), so the body range is load-balanced
+// across devices like any other compute().
 #include "cek_kernel.h"
 
-extern "C" __global__ __launch_bounds__(256) void cek_nbody_f32(const float4* __restrict__ pos,
-                                                              float4* __restrict__ vel,
-                                                              float4* __restrict__ acc,
-                                                              const float* __restrict__ params,
-                                                              CEK_HIDDEN) {
-  (void)vel;
+namespace {
+
+template <int B>
+__device__ __forceinline__ long long first_body(long long w) {
+  return (w >> 8) * (256LL * B) + (w & 255);
+}
+
+template <int B>
+__device__ __forceinline__ void nbody_force(const float4* __restrict__ pos, float4* __restrict__ acc,
+                                            const float* __restrict__ params, long long off) {
   __shared__ float4 tile[256];
+  if (blockDim.x != 256) return;  // body mapping assumes 256-item groups
   const float eps2 = params[0], gconst = params[1];
   const int n = (int)params[2];
-  // work item w handles bodies 2·(w - lane-group base) layout: i0 = base + l, i1 = base + l + L
-  const long long w = cek_global_id();
-  const int L = blockDim.x;
-  const long long grp = w / L, l = w % L;
-  const long long i0 = grp * 2 * L + l, i1 = i0 + L;
-  const float4 p0 = pos[i0], p1 = pos[i1];
-  f32x2 px = {p0.x, p1.x}, py = {p0.y, p1.y}, pz = {p0.z, p1.z};
-  f32x2 ax = {0.f, 0.f}, ay = {0.f, 0.f}, az = {0.f, 0.f};
-  const f32x2 e2 = {eps2, eps2};
-  for (int j0 = 0; j0 < n; j0 += L) {
+  const int l = threadIdx.x;
+  const long long i0 = first_body<B>((long long)blockIdx.x * 256 + l + off);
+  float px[B], py[B], pz[B], ax[B], ay[B], az[B];
+#pragma unroll
+  for (int k = 0; k < B; ++k) {
+    const float4 p = pos[i0 + k * 256];
+    px[k] = p.x;
+    py[k] = p.y;
+    pz[k] = p.z;
+    ax[k] = ay[k] = az[k] = 0.f;
+  }
+  float4 next = pos[l];
+  for (int j0 = 0; j0 < n; j0 += 256) {
     __syncthreads();
-    tile[threadIdx.x] = pos[j0 + threadIdx.x];
+    tile[l] = next;
     __syncthreads();
-#pragma unroll 8
-    for (int j = 0; j < L; ++j) {
+    if (j0 + 256 < n) next = pos[j0 + 256 + l];
+#pragma unroll 4
+    for (int j = 0; j < 256; ++j) {
       const float4 q = tile[j];
-      const f32x2 qx = {q.x, q.x}, qy = {q.y, q.y}, qz = {q.z, q.z}, qm = {q.w, q.w};
-      const f32x2 dx = qx - px, dy = qy - py, dz = qz - pz;
-      const f32x2 r2 = dx * dx + dy * dy + dz * dz + e2;
-      f32x2 inv = {__builtin_amdgcn_rsqf(r2.x), __builtin_amdgcn_rsqf(r2.y)};
-      const f32x2 s = qm * inv * inv * inv;
-      ax += dx * s;
-      ay += dy * s;
-      az += dz * s;
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        const float dx = q.x - px[k], dy = q.y - py[k], dz = q.z - pz[k];
+        const float r2 = fmaf(dx, dx, fmaf(dy, dy, fmaf(dz, dz, eps2)));
+        const float inv = __builtin_amdgcn_rsqf(r2);
+        const float s = (q.w * inv) * (inv * inv);
+        ax[k] = fmaf(dx, s, ax[k]);
+        ay[k] = fmaf(dy, s, ay[k]);
+        az[k] = fmaf(dz, s, az[k]);
+      }
     }
   }
-  acc[i0] = make_float4(gconst * ax.x, gconst * ay.x, gconst * az.x, 0.f);
-  acc[i1] = make_float4(gconst * ax.y, gconst * ay.y, gconst * az.y, 0.f);
+#pragma unroll
+  for (int k = 0; k < B; ++k) acc[i0 + k * 256] = make_float4(gconst * ax[k], gconst * ay[k], gconst * az[k], 0.f);
 }
 
-// Leapfrog kick-drift: v += a·dt; x += v·dt for the same two bodies per
-// work item as cek_nbody_f32, so both kernels run in one compute() on the
-// same balanced range (same argument list).  params: {softening², G, n, dt}
-__device__ __forceinline__ void kick_drift(float4* pos, float4* vel, const float4* acc, long long i,
-                                           float dt) {
-  float4 p = pos[i], v = vel[i];
-  const float4 a = acc[i];
-  v.x += a.x * dt;
-  v.y += a.y * dt;
-  v.z += a.z * dt;
-  p.x += v.x * dt;
-  p.y += v.y * dt;
-  p.z += v.z * dt;
-  pos[i] = p;
-  vel[i] = v;
-}
-
-extern "C" __global__ __launch_bounds__(256) void cek_nbody_integrate_f32(float4* __restrict__ pos,
-                                                                       float4* __restrict__ vel,
-                                                                       const float4* __restrict__ acc,
-                                                                       const float* __restrict__ params,
-                                                                       CEK_HIDDEN) {
-  const long long w = cek_global_id();
-  const int L = blockDim.x;
-  const long long i0 = (w / L) * 2 * L + (w % L);
+// Leapfrog kick-drift: v += a·dt; x += v·dt for the same bodies per work item
+// as the force kernel, so both run in one compute() on the same balanced range
+// (same argument list).
+template <int B>
+__device__ __forceinline__ void nbody_integrate(float4* __restrict__ pos, float4* __restrict__ vel,
+                                                const float4* __restrict__ acc, const float* __restrict__ params,
+                                                long long off) {
+  if (blockDim.x != 256) return;
+  const long long i0 = first_body<B>((long long)blockIdx.x * 256 + threadIdx.x + off);
   const float dt = params[3];
-  kick_drift(pos, vel, acc, i0, dt);
-  kick_drift(pos, vel, acc, i0 + L, dt);
+#pragma unroll
+  for (int k = 0; k < B; ++k) {
+    const long long i = i0 + k * 256;
+    float4 p = pos[i], v = vel[i];
+    const float4 a = acc[i];
+    v.x = fmaf(a.x, dt, v.x);
+    v.y = fmaf(a.y, dt, v.y);
+    v.z = fmaf(a.z, dt, v.z);
+    p.x = fmaf(v.x, dt, p.x);
+    p.y = fmaf(v.y, dt, p.y);
+    p.z = fmaf(v.z, dt, p.z);
+    pos[i] = p;
+    vel[i] = v;
+  }
 }
 
 // Per-group kinetic energy diagnostic: energy[g] = Σ ½ m |v|² over the
-// group's 2·L bodies (same work-item mapping as above).
-extern "C" __global__ __launch_bounds__(256) void cek_nbody_energy_f32(const float4* __restrict__ pos,
-                                                                     const float4* __restrict__ vel,
-                                                                     float* __restrict__ energy,
-                                                                     CEK_HIDDEN) {
+// group's 256·B bodies (same mapping).
+template <int B>
+__device__ __forceinline__ void nbody_energy(const float4* __restrict__ pos, const float4* __restrict__ vel,
+                                             float* __restrict__ energy, long long off) {
   __shared__ float ws[4];
-  const long long w = cek_global_id();
-  const int L = blockDim.x;
-  const long long i0 = (w / L) * 2 * L + (w % L), i1 = i0 + L;
-  const float4 p0 = pos[i0], v0 = vel[i0], p1 = pos[i1], v1 = vel[i1];
-  float e = 0.5f * p0.w * (v0.x * v0.x + v0.y * v0.y + v0.z * v0.z) +
-            0.5f * p1.w * (v1.x * v1.x + v1.y * v1.y + v1.z * v1.z);
+  if (blockDim.x != 256) return;
+  const long long i0 = first_body<B>((long long)blockIdx.x * 256 + threadIdx.x + off);
+  float e = 0.f;
+#pragma unroll
+  for (int k = 0; k < B; ++k) {
+    const float4 p = pos[i0 + k * 256], v = vel[i0 + k * 256];
+    e += 0.5f * p.w * (v.x * v.x + v.y * v.y + v.z * v.z);
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = e;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) s += ws[k];
-    energy[cek_global_group_id()] = s;
-  }
+  if (threadIdx.x == 0) energy[blockIdx.x + off / 256] = ws[0] + ws[1] + ws[2] + ws[3];
 }
+
+}  // namespace
+
+#define CEK_NBODY_KERNELS(B)                                                                          \
+  extern "C" __global__ __launch_bounds__(256) void cek_nbody_f32_b##B(                               \
+      const float4* __restrict__ pos, float4* __restrict__ vel, float4* __restrict__ acc,             \
+      const float* __restrict__ params, CEK_HIDDEN) {                                                 \
+    (void)vel;                                                                                        \
+    nbody_force<B>(pos, acc, params, __cek_off);                                                      \
+  }                                                                                                   \
+  extern "C" __global__ __launch_bounds__(256) void cek_nbody_integrate_f32_b##B(                     \
+      float4* __restrict__ pos, float4* __restrict__ vel, const float4* __restrict__ acc,             \
+      const float* __restrict__ params, CEK_HIDDEN) {                                                 \
+    nbody_integrate<B>(pos, vel, acc, params, __cek_off);                                             \
+  }                                                                                                   \
+  extern "C" __global__ __launch_bounds__(256) void cek_nbody_energy_f32_b##B(                        \
+      const float4* __restrict__ pos, const float4* __restrict__ vel, float* __restrict__ energy,     \
+      CEK_HIDDEN) {                                                                                   \
+    nbody_energy<B>(pos, vel, energy, __cek_off);                                                     \
+  }
+
+CEK_NBODY_KERNELS(2)
+CEK_NBODY_KERNELS(4)

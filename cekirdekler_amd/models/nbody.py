@@ -36,10 +36,19 @@ def nbody_accel_reference(pos: np.ndarray, eps2: float, g: float = 1.0, chunk: i
 
 class NBodySimulation:
     def __init__(self, n: int, devices=None, cruncher: ClNumberCruncher | None = None, eps: float = 0.01,
-                 dt: float = 1e-3, g: float = 1.0, seed: int = 0, resident: bool = True):
-        if n % (2 * L):
-            raise ValueError(f"n must be a multiple of {2 * L}")
+                 dt: float = 1e-3, g: float = 1.0, seed: int = 0, resident: bool = True,
+                 bodies_per_item: int | None = None):
+        # 4 bodies per work item once the grid still has >= 4 workgroups per
+        # CU (n >= 1M on 256 CUs); 2 below that, for occupancy
+        b = bodies_per_item or (4 if n >= 4 * L * 1024 else 2)
+        if b not in (2, 4):
+            raise ValueError("bodies_per_item must be 2 or 4")
+        if n % (b * L):
+            raise ValueError(f"n must be a multiple of {b * L}")
         self.n = n
+        self.bpw = b
+        self.k_force, self.k_integrate = f"cek_nbody_f32_b{b}", f"cek_nbody_integrate_f32_b{b}"
+        self.k_energy = f"cek_nbody_energy_f32_b{b}"
         self.resident = resident
         self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library("nbody"))
         rng = np.random.default_rng(seed)
@@ -64,7 +73,7 @@ class NBodySimulation:
     def _flags(self) -> None:
         first = self.steps == 0
         for a in (self.pos, self.vel, self.acc):
-            a.elements_per_work_item = 8  # 2 bodies × float4 per work item
+            a.elements_per_work_item = 4 * self.bpw  # bpw bodies × float4 per work item
             a.partial_read = False
         # positions: every device reads all of them
         self.pos.read = first or not self.resident
@@ -81,15 +90,15 @@ class NBodySimulation:
         self._flags()
         self.pos.write = False
         self.acc.write = True
-        self.pos.next_param(self.vel, self.acc, self.params).compute(self.cr, compute_id, "cek_nbody_f32",
-                                                                    self.n // 2, L)
+        self.pos.next_param(self.vel, self.acc, self.params).compute(self.cr, compute_id, self.k_force,
+                                                                    self.n // self.bpw, L)
 
     def step(self, compute_id: int = 1) -> None:
         """Forces + kick-drift for every body, range-partitioned; then the
         position slices are made coherent on every device."""
         self._flags()
         self.pos.next_param(self.vel, self.acc, self.params).compute(
-            self.cr, compute_id, "cek_nbody_f32 cek_nbody_integrate_f32", self.n // 2, L)
+            self.cr, compute_id, f"{self.k_force} {self.k_integrate}", self.n // self.bpw, L)
         if self.resident and self.cr.cores.num_devices > 1:
             self.cr.cores.share_slices(compute_id, self.pos._spec(), L)
         self.steps += 1
@@ -108,7 +117,7 @@ class NBodySimulation:
                 continue
             cid = 1
             refs, rng = self.cr.references(cid), self.cr.ranges(cid)
-            e = 8
+            e = 4 * self.bpw
             full = np.empty_like(arr.array)
             keep = arr.array.copy()
             for d in range(c.num_devices):

@@ -18,9 +18,22 @@ LIBRARY = {
                    "cek_sgemm_bf16_256x128", "cek_sgemm_bf16_256x128p", "cek_sgemm_bf16_256x128pp", "cek_sgemm_bf16_256x128ps",
                    "cek_sgemm_bf16_128x128", "cek_sgemm_bf16_128x128p"],
     "mandelbrot": ["cek_mandelbrot_f32", "cek_mandelbrot_pool16_f32", "cek_mandelbrot_pool8_f32"],
-    "nbody": ["cek_nbody_f32", "cek_nbody_integrate_f32", "cek_nbody_energy_f32"],
+    "nbody": ["cek_nbody_f32_b2", "cek_nbody_integrate_f32_b2", "cek_nbody_energy_f32_b2",
+              "cek_nbody_f32_b4", "cek_nbody_integrate_f32_b4", "cek_nbody_energy_f32_b4"],
     "reduce": ["cek_reduce_sum_f32", "cek_reduce_sum_f32_final"],
     "stream": ["cek_saxpy_f32", "cek_copy_u8", "cek_vec_add_f32"],
+}
+
+# Array-parameter count of every library kernel.  Passed to the runtime as
+# "name:arity" so a compute() whose array list does not match the kernel's
+# signature is rejected on the host instead of faulting on the device.
+ARITY = {
+    **{k: 4 for k in LIBRARY["sgemm_bf16"]},
+    **{k: 3 for k in LIBRARY["mandelbrot"]},
+    **{k: 4 for k in LIBRARY["nbody"] if "energy" not in k},
+    **{k: 3 for k in LIBRARY["nbody"] if "energy" in k},
+    "cek_reduce_sum_f32": 2, "cek_reduce_sum_f32_final": 3,
+    "cek_saxpy_f32": 3, "cek_copy_u8": 2, "cek_vec_add_f32": 3,
 }
 
 
@@ -39,4 +52,4 @@ def code_object(name: str) -> str:
 
 def library(*names: str):
     """``prebuilt`` entries for the given library names."""
-    return [(code_object(n), LIBRARY[n]) for n in names]
+    return [(code_object(n), [f"{k}:{ARITY[k]}" for k in LIBRARY[n]]) for n in names]

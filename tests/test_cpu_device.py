@@ -19,6 +19,7 @@ __global__ void copy2(const float* src, float* dst) {
 }
 __global__ void inc(float* x) { x[get_global_id(0)] += 1.0f; }
 __global__ void count(float* x, int* c) { if (get_global_id(0) == 0) c[0] += 1; }
+__global__ void incc(float* x, int* c) { x[get_global_id(0)] += 1.0f; }
 __global__ void groupsum(const float* x, float* out) {
   __shared__ float s[64];
   int l = (int)get_local_id(0);
@@ -89,7 +90,7 @@ def test_repeat_with_sync_kernel(cr):
     cr.repeat_count = 5
     cr.repeat_kernel_name = "count"
     try:
-        x.next_param(c).compute(cr, 4, "inc", 1024, 64)
+        x.next_param(c).compute(cr, 4, "incc", 1024, 64)
     finally:
         cr.repeat_count = 1
         cr.repeat_kernel_name = ""
@@ -152,3 +153,12 @@ def test_load_balancer_with_injected_imbalance(cpu):
     r = cr.ranges(9)
     assert r[0] > r[1] * 1.5
     assert cr.normalized_global_ranges_of_devices(9)[0] > 0.55
+
+
+def test_kernel_arity_mismatch_is_rejected(cr):
+    # inc takes one array; passing two would shift the hidden offset argument
+    x = ck.ClArray(np.zeros(256, np.float32))
+    c = ck.ClArray(np.zeros(1, np.int32))
+    c.write = False
+    with pytest.raises(Exception, match="array parameter"):
+        x.next_param(c).compute(cr, 40, "inc", 256, 64)

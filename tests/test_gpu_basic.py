@@ -107,10 +107,11 @@ def test_reduce_sum():
     np.testing.assert_allclose(part.array.sum(), x.array.astype(np.float64).sum(), rtol=1e-5)
 
 
-def test_nbody_forces_match_fp64():
+@pytest.mark.parametrize("bpw", [2, 4])
+def test_nbody_forces_match_fp64(bpw):
     from cekirdekler_amd.models.nbody import NBodySimulation, nbody_accel_reference
 
-    sim = NBodySimulation(4096, devices=_gpu()[0], resident=False)
+    sim = NBodySimulation(4096, devices=_gpu()[0], resident=False, bodies_per_item=bpw)
     sim.forces()
     sim.cr.sync()
     got = sim.acc.array.reshape(-1, 4)[:, :3]

@@ -15,6 +15,7 @@ pytestmark = pytest.mark.gpu
 SRC = """
 __global__ void inc(float* x) { x[get_global_id(0)] += 1.0f; }
 __global__ void count(float* x, int* c) { if (get_global_id(0) == 0) c[0] += 1; }
+__global__ void incc(float* x, int* c) { x[get_global_id(0)] += 1.0f; }
 __global__ void scale(const float* a, float* x) { long long i = get_global_id(0); x[i] = a[0] * x[i]; }
 """
 
@@ -111,7 +112,7 @@ def test_repeat_with_sync_kernel(cr):
     cr.repeat_count = 7
     cr.repeat_kernel_name = "count"
     try:
-        x.next_param(c).compute(cr, 14, "inc", 4096, 256)
+        x.next_param(c).compute(cr, 14, "incc", 4096, 256)
     finally:
         cr.repeat_count = 1
         cr.repeat_kernel_name = ""
