@@ -32,6 +32,9 @@ TILES = {
     "256x128ps": (256, 128, 512, "cek_sgemm_bf16_256x128ps"),
     "128x128": (128, 128, 256, "cek_sgemm_bf16_128x128"),
     "128x128p": (128, 128, 256, "cek_sgemm_bf16_128x128p"),
+    # 8-phase half-tile pipeline (kernels/sgemm8p_bf16.hip), ring of 8 / 10 slots
+    "256x256e8": (256, 256, 512, "cek_sgemm8p_bf16_r8"),
+    "256x256e10": (256, 256, 512, "cek_sgemm8p_bf16_r10"),
 }
 
 
@@ -77,7 +80,7 @@ class GemmBf16:
         self.M, self.N, self.K, self.BM, self.BN, self.L, self.kernel = M, N, K, BM, BN, L, kname
         self.tiles = (M // BM) * (N // BN)
         self.global_range = self.tiles * L
-        self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library("sgemm_bf16"))
+        self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library("sgemm_bf16", "sgemm8p_bf16"))
         self.group_m = group_m
         self.dims = ClArray(np.array([M, N, K, group_m], np.int32))
         self.dims.write = False

@@ -55,7 +55,7 @@ def test_logical_devices_pipelines(pipeline, ptype):
 
 
 @pytest.mark.parametrize("tile", ["256x256", "256x256p", "256x256pp", "256x256ps", "256x128", "256x128p", "256x128pp", "256x128ps",
-                                  "128x128", "128x128p"])
+                                  "128x128", "128x128p", "256x256e8", "256x256e10"])
 def test_gemm_bf16_matches_fp64(tile):
     from cekirdekler_amd.ops.gemm import GemmBf16
 
@@ -65,6 +65,24 @@ def test_gemm_bf16_matches_fp64(tile):
     ref = g.reference()
     err = np.abs(c - ref).max()
     assert err < 5e-3 * np.abs(ref).max(), err
+
+
+@pytest.mark.parametrize("tile", ["256x256e8", "256x256e10"])
+@pytest.mark.parametrize("shape", [(256, 256, 64), (512, 256, 128), (256, 512, 192), (1024, 768, 320),
+                                   (2048, 2048, 1024)])
+def test_gemm_8phase_pipeline_tails(tile, shape):
+    """The 8-phase ring pipeline at K-tile counts below, at and above its
+    prefetch depth (prologue/tail waits), on several grid shapes."""
+    from cekirdekler_amd.ops.gemm import GemmBf16
+
+    M, N, K = shape
+    g = GemmBf16(M, N, K, devices=_gpu()[0], tile=tile, group_m=2)
+    for _ in range(3):                       # repeated runs screen for LDS races
+        g.run(resident=False)
+        c = g.result(download=False)
+        ref = g.reference()
+        err = np.abs(c - ref).max()
+        assert err < 5e-3 * np.abs(ref).max(), (shape, err)
 
 
 def test_gemm_two_logical_devices_balanced():
