@@ -142,3 +142,132 @@ extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_pool8_f32(const
                                                                          int4* out, CEK_HIDDEN) {
   mandel_pool<8>(view, size, out, __cek_off);
 }
+
+// ---------------------------------------------------------------------------
+// Packed pool variant.  Same pool scheduling as above, but every operation of
+// the iteration is a packed-f32 instruction over a PAIR of pixels (on MI355X a
+// wave64 VALU instruction costs ~4 issue cycles packed or not, so packing
+// halves the cost per pixel), including the escape count: instead of a
+// per-pixel compare + carry-add, each iteration adds
+//     t = clamp(2^20 · (4 − |z|²), 0, 1)        (one v_pk_fma_f32 … clamp)
+// which is 1 while |z|² ≤ 4 − 2^-20 and 0 once the pixel escaped (±inf and NaN
+// clamp to 0), so the float sum is the escape iteration.  Only pixels whose
+// |z|² lands within 2^-20 of 4 can differ by one iteration from a strict
+// "|z|² > 4" test.  Per pixel-iteration: 4 packed instructions.
+// Two pairs (four pixels) in flight per lane.
+__device__ __forceinline__ f32x2 pk_fma_clamp(f32x2 a, f32x2 b, f32x2 c) {
+  f32x2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 clamp" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+template <int PPW>
+__device__ __forceinline__ void mandel_pool_pk(const float* view, const int* size, int4* out,
+                                               long long off) {
+  constexpr int P = 64 * PPW, NS = 4;  // pool pixels per wave, slots per lane
+  __shared__ int res[4][P];
+  if (blockDim.x != 256) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long long wi0 = (long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63) + off;
+  const int pbase = (int)(wi0 * PPW);
+  const int W = size[0], max_iter = size[2];
+  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
+  const float invW = 1.0f / (float)W;
+  const float iter_cap = (float)max_iter - 0.5f;
+  auto coords = [&](int p, float& cr, float& ci) {
+    const int g = pbase + p;
+    int y = (int)((float)g * invW);
+    int x = g - y * W;
+    if (x < 0) { --y; x += W; }
+    if (x >= W) { ++y; x -= W; }
+    cr = x0 + x * dx;
+    ci = y0 + y * dy;
+  };
+  // slot s of this lane: pair s/2, element s%2
+  f32x2 zr[2], zi[2], cr[2], ci[2], cnt[2], t[2];
+  int pix[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) pix[s] = lane + 64 * s;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    float a, b, c, d;
+    coords(pix[2 * q], a, b);
+    coords(pix[2 * q + 1], c, d);
+    cr[q] = f32x2{a, c};
+    ci[q] = f32x2{b, d};
+    zr[q] = zi[q] = cnt[q] = t[q] = f32x2{0.f, 0.f};
+  }
+  int next = 64 * NS;
+  const f32x2 nbig = {-1048576.f, -1048576.f}, cbig = {4194304.f, 4194304.f}, two = {2.f, 2.f};
+  const int chunk_cap = (P / (64 * NS) + 2) * ((max_iter + 7) / 8 + 1);
+  for (int chunk = 0; chunk < chunk_cap; ++chunk) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const f32x2 zi2 = zi[q] * zi[q];
+        const f32x2 m = __builtin_elementwise_fma(zr[q], zr[q], zi2);
+        t[q] = pk_fma_clamp(m, nbig, cbig);
+        cnt[q] += t[q];
+        const f32x2 tz = zr[q] * zi[q];
+        zr[q] = __builtin_elementwise_fma(zr[q], zr[q], -zi2) + cr[q];
+        zi[q] = __builtin_elementwise_fma(tz, two, ci[q]);
+      }
+    }
+    bool d[NS];
+    unsigned long long b[NS], any = 0ull;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const float ts = (s & 1) ? t[s >> 1].y : t[s >> 1].x;
+      const float cs = (s & 1) ? cnt[s >> 1].y : cnt[s >> 1].x;
+      d[s] = pix[s] < P && (ts < 0.5f || cs >= iter_cap);
+      b[s] = __ballot(d[s]);
+      any |= b[s];
+    }
+    if (any != 0ull) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        if (d[s]) {
+          const int q = s >> 1;
+          const float cs = (s & 1) ? cnt[q].y : cnt[q].x;
+          res[wv][pix[s]] = min((int)(cs + 0.5f), max_iter);
+          pix[s] = next + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(b[s] >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((unsigned)b[s], 0u));
+          float a = 0.f, c = 0.f;
+          if (pix[s] < P) coords(pix[s], a, c);
+          if (s & 1) {
+            zr[q].y = zi[q].y = cnt[q].y = 0.f;
+            t[q].y = 1.f;
+            cr[q].y = a;
+            ci[q].y = c;
+          } else {
+            zr[q].x = zi[q].x = cnt[q].x = 0.f;
+            t[q].x = 1.f;
+            cr[q].x = a;
+            ci[q].x = c;
+          }
+        }
+        next += __popcll(b[s]);
+      }
+    }
+    bool live = false;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) live |= pix[s] < P;
+    if (__ballot(live) == 0ull) break;
+  }
+  __syncthreads();
+  const int4* r4 = reinterpret_cast<const int4*>(res[wv]);
+  int4* o = out + pbase / 4;
+#pragma unroll
+  for (int k = 0; k < PPW / 4; ++k) o[k * 64 + lane] = r4[k * 64 + lane];
+}
+
+extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_pk16_f32(const float* view, const int* size,
+                                                                        int4* out, CEK_HIDDEN) {
+  mandel_pool_pk<16>(view, size, out, __cek_off);
+}
+
+extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_pk32_f32(const float* view, const int* size,
+                                                                        int4* out, CEK_HIDDEN) {
+  mandel_pool_pk<32>(view, size, out, __cek_off);
+}

@@ -12,11 +12,15 @@
 // streams all bodies through LDS in tiles of 256 (the next tile is fetched
 // into registers while the current one is consumed); every lane of a wave
 // reads the same LDS address (a broadcast, no bank conflicts) and applies it
-// to its B bodies.  The arithmetic is scalar on purpose (the file is built
-// with -fno-slp-vectorize): on CDNA4's SIMD-32 a wave64 v_fma_f32 issues in
-// 2 cycles, so v_pk_fma_f32 adds no FLOP rate, and the packed form forced
-// s_nop hazard padding around the (unpackable) v_rsq_f32.  Per interaction:
-// 3 sub, 3 fma (r²), rsq, 3 mul, 3 fma — 20 FLOP by the usual convention.
+// to its B bodies.  The bodies are processed as packed pairs: measured on
+// MI355X a wave64 VALU instruction costs ≈4 cycles of SIMD issue whether it
+// is v_fma_f32 or v_pk_fma_f32 (PMC: 4.2 cycles per VALU instruction at two
+// waves per SIMD), so FP32 peak needs the packed forms.  Per pair of
+// interactions: 3 pk_add, 3 pk_fma (r²), 2 v_rsq_f32, 3 pk_mul, 3 pk_fma =
+// 14 instructions for 40 FLOP (20 per interaction, the usual convention);
+// with two pairs per work item the rsq results are consumed by the other
+// pair's independent work instead of s_nop padding.  Auto-SLP is disabled
+// (cek-flags) so only these explicit vectors are packed.
 // Work items are absolute (__cek_off), so the body range is load-balanced
 // across devices like any other compute().
 #include "cek_kernel.h"
@@ -31,21 +35,25 @@ __device__ __forceinline__ long long first_body(long long w) {
 template <int B>
 __device__ __forceinline__ void nbody_force(const float4* __restrict__ pos, float4* __restrict__ acc,
                                             const float* __restrict__ params, long long off) {
+  static_assert(B % 2 == 0, "bodies are processed in packed pairs");
+  constexpr int NP = B / 2;  // packed pairs per work item
   __shared__ float4 tile[256];
   if (blockDim.x != 256) return;  // body mapping assumes 256-item groups
   const float eps2 = params[0], gconst = params[1];
   const int n = (int)params[2];
   const int l = threadIdx.x;
   const long long i0 = first_body<B>((long long)blockIdx.x * 256 + l + off);
-  float px[B], py[B], pz[B], ax[B], ay[B], az[B];
+  // pair p holds bodies k = 2p (.x) and 2p+1 (.y)
+  f32x2 px[NP], py[NP], pz[NP], ax[NP], ay[NP], az[NP];
 #pragma unroll
-  for (int k = 0; k < B; ++k) {
-    const float4 p = pos[i0 + k * 256];
-    px[k] = p.x;
-    py[k] = p.y;
-    pz[k] = p.z;
-    ax[k] = ay[k] = az[k] = 0.f;
+  for (int p = 0; p < NP; ++p) {
+    const float4 b0 = pos[i0 + (2 * p) * 256], b1 = pos[i0 + (2 * p + 1) * 256];
+    px[p] = f32x2{b0.x, b1.x};
+    py[p] = f32x2{b0.y, b1.y};
+    pz[p] = f32x2{b0.z, b1.z};
+    ax[p] = ay[p] = az[p] = f32x2{0.f, 0.f};
   }
+  const f32x2 e2 = {eps2, eps2};
   float4 next = pos[l];
   for (int j0 = 0; j0 < n; j0 += 256) {
     __syncthreads();
@@ -55,20 +63,24 @@ __device__ __forceinline__ void nbody_force(const float4* __restrict__ pos, floa
 #pragma unroll 4
     for (int j = 0; j < 256; ++j) {
       const float4 q = tile[j];
+      const f32x2 qx = {q.x, q.x}, qy = {q.y, q.y}, qz = {q.z, q.z}, qm = {q.w, q.w};
 #pragma unroll
-      for (int k = 0; k < B; ++k) {
-        const float dx = q.x - px[k], dy = q.y - py[k], dz = q.z - pz[k];
-        const float r2 = fmaf(dx, dx, fmaf(dy, dy, fmaf(dz, dz, eps2)));
-        const float inv = __builtin_amdgcn_rsqf(r2);
-        const float s = (q.w * inv) * (inv * inv);
-        ax[k] = fmaf(dx, s, ax[k]);
-        ay[k] = fmaf(dy, s, ay[k]);
-        az[k] = fmaf(dz, s, az[k]);
+      for (int p = 0; p < NP; ++p) {
+        const f32x2 dx = qx - px[p], dy = qy - py[p], dz = qz - pz[p];
+        const f32x2 r2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, __builtin_elementwise_fma(dz, dz, e2)));
+        const f32x2 inv = {__builtin_amdgcn_rsqf(r2.x), __builtin_amdgcn_rsqf(r2.y)};
+        const f32x2 s = (qm * inv) * (inv * inv);
+        ax[p] = __builtin_elementwise_fma(dx, s, ax[p]);
+        ay[p] = __builtin_elementwise_fma(dy, s, ay[p]);
+        az[p] = __builtin_elementwise_fma(dz, s, az[p]);
       }
     }
   }
 #pragma unroll
-  for (int k = 0; k < B; ++k) acc[i0 + k * 256] = make_float4(gconst * ax[k], gconst * ay[k], gconst * az[k], 0.f);
+  for (int p = 0; p < NP; ++p) {
+    acc[i0 + (2 * p) * 256] = make_float4(gconst * ax[p].x, gconst * ay[p].x, gconst * az[p].x, 0.f);
+    acc[i0 + (2 * p + 1) * 256] = make_float4(gconst * ax[p].y, gconst * ay[p].y, gconst * az[p].y, 0.f);
+  }
 }
 
 // Leapfrog kick-drift: v += a·dt; x += v·dt for the same bodies per work item

@@ -23,6 +23,8 @@ KERNELS = {
     "quad": ("cek_mandelbrot_f32", 4),          # 4 fixed pixels per work item
     "pool8": ("cek_mandelbrot_pool8_f32", 8),    # wave-pooled, 512-pixel pools
     "pool16": ("cek_mandelbrot_pool16_f32", 16),  # wave-pooled, 1024-pixel pools
+    "pk16": ("cek_mandelbrot_pk16_f32", 16),     # pooled, packed pairs + clamp count
+    "pk32": ("cek_mandelbrot_pk32_f32", 32),     # same, 2048-pixel pools
 }
 
 
