@@ -512,9 +512,10 @@ class ClArray:
 
     def compute(self, cruncher, compute_id: int, kernels: str, global_range: int, local_range: int = 256,
                 global_offset: int = 0, pipeline: bool = False, pipeline_type: bool = True,
-                pipeline_blobs: int = 4) -> None:
+                pipeline_blobs: int = 4, granularity: int = 0) -> None:
         ClParameterGroup([self]).compute(cruncher, compute_id, kernels, global_range, local_range,
-                                         global_offset, pipeline, pipeline_type, pipeline_blobs)
+                                         global_offset, pipeline, pipeline_type, pipeline_blobs,
+                                         granularity)
 
     def task(self, compute_id: int, kernels: str, global_range: int, local_range: int = 256,
              global_offset: int = 0, pipeline: bool = False, pipeline_type: bool = True,
@@ -607,9 +608,12 @@ class ClParameterGroup:
 
     def compute(self, cruncher, compute_id: int, kernels: str, global_range: int, local_range: int = 256,
                 global_offset: int = 0, pipeline: bool = False, pipeline_type: bool = True,
-                pipeline_blobs: int = 4) -> None:
+                pipeline_blobs: int = 4, granularity: int = 0) -> None:
+        """Run ``kernels`` over ``global_range`` work items split across the
+        cruncher's devices (ClArray.cs:543).  ``granularity`` (an extension)
+        makes every device range a multiple of that many work items."""
         cruncher._compute_group(self, compute_id, kernels, global_range, local_range, global_offset,
-                                pipeline, pipeline_type, pipeline_blobs)
+                                pipeline, pipeline_type, pipeline_blobs, granularity=granularity)
 
     def task(self, compute_id: int, kernels: str, global_range: int, local_range: int = 256,
              global_offset: int = 0, pipeline: bool = False, pipeline_type: bool = True,

@@ -317,7 +317,8 @@ class ClNumberCruncher:
 
     def _compute_group(self, group: ClParameterGroup, compute_id: int, kernels, global_range: int,
                        local_range: int = 256, global_offset: int = 0, pipeline: bool = False,
-                       pipeline_type: bool = PIPELINE_EVENT, pipeline_blobs: int = 4, specs=None) -> None:
+                       pipeline_type: bool = PIPELINE_EVENT, pipeline_blobs: int = 4, specs=None,
+                       granularity: int = 0) -> None:
         names = split_kernel_names(kernels)
         G, L = int(global_range), int(local_range)
         try:
@@ -338,17 +339,23 @@ class ClNumberCruncher:
         call.pipeline = bool(pipeline)
         call.pipeline_event = bool(pipeline_type)
         call.blobs = int(pipeline_blobs)
+        if granularity:
+            if granularity % L or G % granularity:
+                self.number_of_errors_happened += 1
+                raise ClComputeError(f"granularity({granularity}) must be a multiple of the local range({L}) "
+                                     f"and divide the global range({G})")
+            call.granularity = int(granularity)
         self._cores.compute(call)
         if self.performance_feed:
             self.performance_report(compute_id)
 
     def compute(self, arrays, compute_id: int, kernels, global_range: int, local_range: int = 256,
                 global_offset: int = 0, pipeline: bool = False, pipeline_type: bool = PIPELINE_EVENT,
-                pipeline_blobs: int = 4) -> None:
+                pipeline_blobs: int = 4, granularity: int = 0) -> None:
         """Functional form: ``cr.compute([a, b, c], 1, "k", G, L)``."""
         group = arrays if isinstance(arrays, ClParameterGroup) else ClParameterGroup(arrays)
         self._compute_group(group, compute_id, kernels, global_range, local_range, global_offset,
-                            pipeline, pipeline_type, pipeline_blobs)
+                            pipeline, pipeline_type, pipeline_blobs, granularity=granularity)
 
     # ------------------------------------------------------------ device data access
     def upload(self, array: ClArray, device: int = 0) -> None:

@@ -176,7 +176,8 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("compute_id", &ComputeCall::compute_id)
       .def_readwrite("pipeline", &ComputeCall::pipeline)
       .def_readwrite("pipeline_event", &ComputeCall::pipeline_event)
-      .def_readwrite("blobs", &ComputeCall::blobs);
+      .def_readwrite("blobs", &ComputeCall::blobs)
+      .def_readwrite("granularity", &ComputeCall::granularity);
 
   py::class_<CoresConfig>(m, "CoresConfig")
       .def(py::init<>())

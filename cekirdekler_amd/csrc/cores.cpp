@@ -522,6 +522,9 @@ void Cores::compute(const ComputeCall& c) {
   const int nloc = num_devices();
   const long long B = std::max(1, c.blobs);
   const bool pipe_req = c.pipeline && !cfg_.no_pipelining;
+  const long long U = c.granularity > 0 ? c.granularity : L;  // balancer unit
+  if (U % L != 0) throw Error("granularity must be a multiple of the local range");
+  if (G % U != 0) throw Error("global range must be a multiple of the granularity");
   TraceRange tr("cek.compute.id" + std::to_string(c.compute_id));
   double wall0 = now_ms();
 
@@ -548,12 +551,12 @@ void Cores::compute(const ComputeCall& c) {
       // Cores.cs:569-596
       std::vector<long long> eq(D, G / D);
       eq[0] += G - (G / D) * D;
-      bool b1 = std::all_of(eq.begin(), eq.end(), [&](long long r) { return r >= B * L; });
-      long long step = (b1 && pipe_req && G >= B * L) ? B * L : L;
+      bool b1 = std::all_of(eq.begin(), eq.end(), [&](long long r) { return r >= B * U; });
+      long long step = (b1 && pipe_req && G >= B * U) ? B * U : U;
       initial_split(D, smooth, st.history, G, st.ranges, step);
     } else {
-      bool b1 = std::all_of(st.ranges.begin(), st.ranges.end(), [&](long long r) { return r >= B * L; });
-      long long step = (b1 && pipe_req && G >= B * L) ? B * L : L;
+      bool b1 = std::all_of(st.ranges.begin(), st.ranges.end(), [&](long long r) { return r >= B * U; });
+      long long step = (b1 && pipe_req && G >= B * U) ? B * U : U;
       load_balance(st.bench, smooth, st.history, G, st.ranges, step);
     }
   }
@@ -566,7 +569,7 @@ void Cores::compute(const ComputeCall& c) {
   // Pipelining eligibility (Cores.cs:624-652), decided per call for all devices.
   bool pipelined = pipe_req && c.repeats <= 1 && !enqueue_mode_;
   for (int i = 0; i < D && pipelined; ++i)
-    if (st.ranges[i] % (B * L) != 0 || st.ranges[i] < B * L) pipelined = false;
+    if (st.ranges[i] % (B * U) != 0 || st.ranges[i] < B * U) pipelined = false;
   if (comm_ && (dist_gather_writes || dist_broadcast_reads)) pipelined = false;
 
   std::vector<double> ms(nloc, 0.0);

@@ -40,6 +40,10 @@ struct ComputeCall {
   bool pipeline = false;
   bool pipeline_event = true;  // PIPELINE_EVENT=true, PIPELINE_DRIVER=false
   int blobs = 4;
+  // Split granularity in work items (0 = local range): every device range is
+  // a multiple of it, e.g. to keep the K-split work-groups of one GEMM tile
+  // on the same device.  Must be a multiple of local_range.
+  long long granularity = 0;
 };
 
 struct CoresConfig {

@@ -25,11 +25,12 @@
 
 namespace {
 
-template <int WM, int WN, int FM, int FN, int MODE>
+template <int WM, int WN, int FM, int FN, int MODE, bool SK = false>
 __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
                                           const uint16_t* __restrict__ A,
                                           const uint16_t* __restrict__ Bt, float* __restrict__ C,
-                                          char* smem, long long off) {
+                                          char* smem, long long off, float* __restrict__ W = nullptr,
+                                          int* __restrict__ tile_cnt = nullptr) {
   constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN, BK = 64;
   constexpr int NWAVES = WM * WN, NT = 64 * NWAVES;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -50,7 +51,13 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave / WN, wc = wave % WN;
-  const long long t = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
+  // Split-K (SK): work-group u computes K-tiles [ks, ks + nk) of tile u / S;
+  // the S work-groups of a tile are consecutive ids, so the XCD remap keeps
+  // them on one XCD and the load balancer (granularity S·local) on one device.
+  const long long u = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
+  const int S = SK ? max(dims[4], 1) : 1;
+  const long long t = u / S;
+  const int ks = SK ? (int)(u % S) * (dims[2] / 64 / S) : 0;
   // Grouped tile order (dims[3] = GM row panels per group, tiles walk down
   // the group's rows first): the 32 work-groups an XCD runs at once cover a
   // GM × (32/GM) block of C, so A and B K-slices are shared through that
@@ -79,8 +86,8 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     char* base = smem + buf * STAGE;
 #pragma unroll
     for (int j = 0; j < A_INSTR; ++j) {
-      const char* u = a_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 2;
-      __builtin_amdgcn_global_load_lds((glb_cvoid*)(u + lane_off),
+      const char* src = a_wave + ((size_t)j * 8 * K + (size_t)(ks + kt) * BK) * 2;
+      __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
                                        (lds_void*)(base + (sw * A_INSTR + j) * 1024), 16, 0, 0);
     }
   };
@@ -88,8 +95,8 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     char* base = smem + buf * STAGE + A_BYTES;
 #pragma unroll
     for (int j = 0; j < B_INSTR; ++j) {
-      const char* u = b_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 2;
-      __builtin_amdgcn_global_load_lds((glb_cvoid*)(u + lane_off),
+      const char* src = b_wave + ((size_t)j * 8 * K + (size_t)(ks + kt) * BK) * 2;
+      __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
                                        (lds_void*)(base + (sw * B_INSTR + j) * 1024), 16, 0, 0);
     }
   };
@@ -115,7 +122,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / BK;
+  const int nk = K / BK / S;
   if constexpr (MODE == 0) {
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -282,6 +289,43 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   }
 
   // Epilogue: acc[i][j][r] is C(row = wr·16FM + i·16 + fq·4 + r, col = wc·16FN + j·16 + fr)
+  if constexpr (SK) {
+    if (S > 1) {
+      // Every split stores its partial tile; the last of the S to arrive
+      // (device-scope counter) adds the others' partials to its own and
+      // writes C, then re-arms the counter for the next call.
+      float* wt = W + (size_t)u * BM * BN;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            wt[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr] = acc[i][j][r];
+      __threadfence();
+      __syncthreads();
+      int* flag = reinterpret_cast<int*>(smem);
+      if (tid == 0) {
+        const int old = atomicAdd(&tile_cnt[t], 1);
+        *flag = old == S - 1;
+        if (old == S - 1) tile_cnt[t] = 0;
+      }
+      __syncthreads();
+      if (*flag == 0) return;
+      __threadfence();
+      for (int s2 = 0; s2 < S; ++s2) {
+        if (s2 == (int)(u % S)) continue;
+        const float* wp = W + (size_t)(t * S + s2) * BM * BN;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              acc[i][j][r] += wp[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr];
+      }
+    }
+  }
   float* ct = C + (size_t)t * BM * BN;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -300,6 +344,20 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     __shared__ __attribute__((aligned(16))) char smem[2 * (WM * 16 * FM + WN * 16 * FN) * 64 * 2]; \
     gemm_tile<WM, WN, FM, FN, MODE>(dims, A, Bt, C, smem, __cek_off);                              \
   }
+
+#define CEK_GEMM_SK_KERNEL(NAME, WM, WN, FM, FN, MODE)                                           \
+  extern "C" __global__ __launch_bounds__(64 * WM * WN) void NAME(                                \
+      const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt,    \
+      CEK_HIDDEN) {                                                                                \
+    __shared__ __attribute__((aligned(16))) char smem[2 * (WM * 16 * FM + WN * 16 * FN) * 64 * 2]; \
+    gemm_tile<WM, WN, FM, FN, MODE, true>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);           \
+  }
+
+// Split-K ping-pong variants (dims[4] = S splits; K/64 divisible by S):
+// strongly scaled slices keep one 256-row tile per CU busy instead of
+// leaving CUs idle (8 GPUs × 1024 rows of an 8192² problem = 128 tiles).
+CEK_GEMM_SK_KERNEL(cek_sgemm_bf16_256x256pp_sk, 2, 4, 8, 4, 2)
+CEK_GEMM_SK_KERNEL(cek_sgemm_bf16_256x128pp_sk, 4, 2, 4, 4, 2)
 
 // 256×256 tiles, 8 waves (2×4, 128×64 each), 128 KiB LDS, 1 block/CU.
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256, 2, 4, 8, 4, 0)

@@ -38,6 +38,10 @@ TILES = {
 }
 
 
+# tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
+SPLIT_K_TILES = {"256x256pp", "256x128pp"}
+
+
 def to_bf16_bits(x: np.ndarray) -> np.ndarray:
     """fp32 → bf16 bit patterns (round to nearest even), as uint16."""
     u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32)
@@ -73,16 +77,23 @@ def untile(c: np.ndarray, M: int, N: int, BM: int, BN: int, group_m: int = 1) ->
 class GemmBf16:
     def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256",
                  cruncher: ClNumberCruncher | None = None, fill: str = "random", seed: int = 0,
-                 group_m: int = 4):
+                 group_m: int = 4, split_k: int = 1):
         BM, BN, L, kname = TILES[tile]
         if M % BM or N % BN or K % 64:
             raise ValueError(f"M%{BM}, N%{BN} and K%64 must be 0 (got {M},{N},{K})")
+        if split_k > 1:
+            if tile not in SPLIT_K_TILES:
+                raise ValueError(f"split-K is available for tiles {sorted(SPLIT_K_TILES)}")
+            if (K // 64) % split_k:
+                raise ValueError(f"K/64 ({K // 64}) must be divisible by split_k ({split_k})")
+            kname = kname + "_sk"
         self.M, self.N, self.K, self.BM, self.BN, self.L, self.kernel = M, N, K, BM, BN, L, kname
+        self.split_k = max(1, int(split_k))
         self.tiles = (M // BM) * (N // BN)
-        self.global_range = self.tiles * L
+        self.global_range = self.tiles * self.split_k * L
         self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library("sgemm_bf16", "sgemm8p_bf16"))
         self.group_m = group_m
-        self.dims = ClArray(np.array([M, N, K, group_m], np.int32))
+        self.dims = ClArray(np.array([M, N, K, group_m, self.split_k, 0, 0, 0], np.int32))
         self.dims.write = False
         self.A = ClArray(M * K, "bfloat16")
         self.B = ClArray(N * K, "bfloat16")
@@ -90,7 +101,16 @@ class GemmBf16:
         for a in (self.A, self.B):
             a.write = False
         self.C.read = False
-        self.C.elements_per_work_item = BM * BN // L
+        self.C.elements_per_work_item = BM * BN // (L * self.split_k)
+        self.extra = []
+        if self.split_k > 1:
+            # per-work-group partial tiles (device-only scratch: never transferred;
+            # np.empty leaves the host pages untouched) and per-tile arrival counters
+            self.W = ClArray(np.empty(self.tiles * self.split_k * BM * BN, np.float32))
+            self.W.read = self.W.write = False
+            self.counters = ClArray(np.zeros(self.tiles, np.int32))
+            self.counters.write = False
+            self.extra = [self.W, self.counters]
         if fill == "random":
             rng = np.random.default_rng(seed)
             self.A.array[:] = to_bf16_bits(rng.uniform(-1, 1, M * K).astype(np.float32))
@@ -105,9 +125,12 @@ class GemmBf16:
         first = not self._uploaded
         for a in (self.dims, self.A, self.B):
             a.read = first or not resident
+        if self.split_k > 1:
+            self.counters.read = first  # zeroed once; the kernel re-arms them
         self.C.write = not resident
-        self.dims.next_param(self.A, self.B, self.C).compute(
-            self.cr, compute_id, self.kernel, self.global_range, self.L)
+        self.dims.next_param(self.A, self.B, self.C, *self.extra).compute(
+            self.cr, compute_id, self.kernel, self.global_range, self.L,
+            granularity=self.L * self.split_k)
         self._uploaded = True
 
     def result(self, download: bool = True) -> np.ndarray:

@@ -162,3 +162,17 @@ def test_kernel_arity_mismatch_is_rejected(cr):
     c.write = False
     with pytest.raises(Exception, match="array parameter"):
         x.next_param(c).compute(cr, 40, "inc", 256, 64)
+
+
+def test_granularity_quantizes_device_ranges(cpu):
+    c = ck.ClNumberCruncher(cpu + cpu, SRC)
+    c.set_time_scale(1, 3.0)
+    x = ck.ClArray(np.zeros(64 * 40, np.float32))
+    for _ in range(6):
+        x.compute(c, 1, "inc", 64 * 40, 64, granularity=64 * 4)
+        assert all(r % 256 == 0 for r in c.ranges(1)), c.ranges(1)
+    np.testing.assert_array_equal(x.array, 6.0)
+    assert c.ranges(1)[0] > c.ranges(1)[1]
+    with pytest.raises(ck.ClComputeError):
+        x.compute(c, 2, "inc", 64 * 40, 64, granularity=96)
+    c.dispose()

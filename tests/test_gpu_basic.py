@@ -85,6 +85,30 @@ def test_gemm_8phase_pipeline_tails(tile, shape):
         assert err < 5e-3 * np.abs(ref).max(), (shape, err)
 
 
+@pytest.mark.parametrize("tile", ["256x256pp", "256x128pp"])
+@pytest.mark.parametrize("split", [2, 4])
+def test_gemm_split_k(tile, split):
+    """Split-K: partial tiles + last-arrival reduction, counters re-armed
+    across calls, K-split work-groups kept on one device by the balancer
+    granularity (two logical devices, one made slower)."""
+    from cekirdekler_amd.ops.gemm import GemmBf16
+
+    g0 = _gpu()[0]
+    cr = ck.ClNumberCruncher(g0 + g0, "", prebuilt=__import__(
+        "cekirdekler_amd.ops.library", fromlist=["library"]).library("sgemm_bf16"))
+    cr.set_time_scale(1, 2.0)
+    g = GemmBf16(1024, 768, 1024, cruncher=cr, tile=tile, split_k=split, group_m=2)
+    ref = g.reference()
+    for _ in range(4):
+        g.run(resident=False)
+        c = g.result(download=False)
+        err = np.abs(c - ref).max()
+        assert err < 5e-3 * np.abs(ref).max(), err
+    unit = g.L * split
+    assert all(r % unit == 0 for r in cr.ranges(1)) and sum(cr.ranges(1)) == g.global_range
+    cr.dispose()
+
+
 def test_gemm_two_logical_devices_balanced():
     from cekirdekler_amd.ops.gemm import GemmBf16
 
