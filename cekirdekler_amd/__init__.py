@@ -10,7 +10,7 @@ from ._native import CekError, cek, gpu_available
 from .arrays import (BFLOAT16, ClArray, ClBf16Array, ClByteArray, ClCharArray, ClDoubleArray,
                      ClFloatArray, ClIntArray, ClLongArray, ClParameterGroup, ClUIntArray, FastArr)
 from .cruncher import (PIPELINE_DRIVER, PIPELINE_EVENT, AcceleratorType, ClComputeError,
-                       ClNumberCruncher, Cores)
+                       ClNumberCruncher, ClUserEvent, Cores)
 from .aux_functions import ClBuiltInAuxilliaryFunctions
 from .hardware import ClDevice, ClDevices, ClPlatform, ClPlatforms
 
@@ -19,6 +19,6 @@ __version__ = "0.1.0"
 __all__ = [
     "AcceleratorType", "BFLOAT16", "ClBuiltInAuxilliaryFunctions", "CekError", "ClArray", "ClBf16Array", "ClByteArray", "ClCharArray",
     "ClComputeError", "ClDevice", "ClDevices", "ClDoubleArray", "ClFloatArray", "ClIntArray",
-    "ClLongArray", "ClNumberCruncher", "ClParameterGroup", "ClPlatform", "ClPlatforms", "ClUIntArray",
+    "ClLongArray", "ClNumberCruncher", "ClParameterGroup", "ClPlatform", "ClPlatforms", "ClUIntArray", "ClUserEvent",
     "Cores", "FastArr", "PIPELINE_DRIVER", "PIPELINE_EVENT", "cek", "gpu_available",
 ]

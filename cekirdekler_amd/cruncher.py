@@ -30,6 +30,32 @@ class AcceleratorType(enum.IntFlag):
     ACC = 4
 
 
+class ClUserEvent:
+    """Host-triggered start gate for device streams (reference ClUserEvent,
+    ClUserEvent.cs:28-117; "development cancelled" there, Worker.cs:487-560).
+
+    ``add_cruncher(cr)`` makes every stream of the cruncher's devices wait
+    (``hipStreamWaitValue32`` on a pinned host word) until :meth:`trigger`;
+    work enqueued meanwhile — e.g. in enqueue mode — starts on all devices at
+    once when triggered.  An armed event left untriggered is triggered when it
+    is garbage collected, so no stream stays blocked."""
+
+    def __init__(self):
+        self._ev = cek.UserEvent()
+
+    def add_cruncher(self, cruncher: "ClNumberCruncher", device: int = -1) -> None:
+        cruncher.cores.gate(self._ev, int(device))
+
+    addCommandQueue = add_cruncher
+
+    def trigger(self) -> None:
+        self._ev.trigger()
+
+    @property
+    def armed(self) -> bool:
+        return bool(self._ev.armed)
+
+
 class ClComputeError(ValueError):
     """A compute() call was rejected by validation (work-size/array-size)."""
 
@@ -145,6 +171,17 @@ class ClNumberCruncher:
             if self._cores:
                 setattr(self._cores, name, bool(v))
         return property(get, set_)
+
+    @property
+    def repeat_graph_threshold(self) -> int:
+        """Repeat loops with at least this many kernel launches per device are
+        captured into a hipGraph and replayed (0 = never)."""
+        return int(self._cores.graph_min_launches) if self._cores else 0
+
+    @repeat_graph_threshold.setter
+    def repeat_graph_threshold(self, n: int) -> None:
+        if self._cores:
+            self._cores.graph_min_launches = int(n)
 
     no_compute_mode = _prop("no_compute")
     fine_grained_queue_control = _prop("fine_grained")

@@ -223,6 +223,11 @@ PYBIND11_MODULE(_cek, m) {
         c.allreduce_sum_f32(reinterpret_cast<void*>(p), n, reinterpret_cast<hipStream_t>(stream));
       }, py::call_guard<py::gil_scoped_release>());
 
+  py::class_<UserEvent>(m, "UserEvent")
+      .def(py::init<>())
+      .def("trigger", &UserEvent::trigger)
+      .def_property_readonly("armed", &UserEvent::armed);
+
   py::class_<Cores, std::shared_ptr<Cores>>(m, "Cores")
       .def(py::init<const std::vector<DeviceInfo>&, const std::string&, const CoresConfig&>(),
            py::call_guard<py::gil_scoped_release>())
@@ -245,6 +250,8 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("fine_grained", &Cores::fine_grained)
       .def_readwrite("smooth", &Cores::smooth)
       .def_readwrite("serial", &Cores::serial)
+      .def_readwrite("graph_min_launches", &Cores::graph_min_launches)
+      .def("gate", &Cores::gate, py::arg("event"), py::arg("device") = -1)
       .def_readwrite("dist_gather_writes", &Cores::dist_gather_writes)
       .def_readwrite("dist_broadcast_reads", &Cores::dist_broadcast_reads)
       .def("set_time_scale", &Cores::set_time_scale)

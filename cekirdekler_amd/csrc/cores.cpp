@@ -1,10 +1,13 @@
 #include "cores.h"
 
+#include <cstring>
+
 #include <algorithm>
 #include <map>
 #include <numeric>
 #include <sstream>
 
+#include "memory.h"
 #include "trace.h"
 
 namespace cek {
@@ -257,17 +260,74 @@ void Cores::share_slices(int id, const ArraySpec& a, long long local_range) {
 
 // ------------------------------------------------------------- compute --
 
+// ---------------------------------------------------------------- UserEvent --
+
+namespace {
+std::mutex g_ue_mu;
+uint32_t* g_ue_slab = nullptr;
+int g_ue_next = 0;
+constexpr int kUserEventSlots = 4096;
+}  // namespace
+
+UserEvent::UserEvent() {
+  std::lock_guard<std::mutex> g(g_ue_mu);
+  if (!g_ue_slab) {
+    bool pinned = false;
+    g_ue_slab = static_cast<uint32_t*>(host_alloc(kUserEventSlots * sizeof(uint32_t), 4096, &pinned));
+    std::memset(g_ue_slab, 0, kUserEventSlots * sizeof(uint32_t));
+  }
+  if (g_ue_next >= kUserEventSlots) throw Error("too many user events in this process");
+  word_ = &g_ue_slab[g_ue_next++];
+}
+
+UserEvent::~UserEvent() {
+  if (armed_) trigger();  // never leave a stream blocked on a dead event
+}
+
+uint32_t UserEvent::arm() {
+  armed_ = true;
+  return gen_ + 1;
+}
+
+void UserEvent::trigger() {
+  __atomic_store_n(word_, gen_ + 1, __ATOMIC_RELEASE);
+  ++gen_;
+  armed_ = false;
+}
+
+void Cores::gate(UserEvent& ev, int device) {
+  const uint32_t v = ev.arm();
+  for (int w = 0; w < num_devices(); ++w)
+    if (device < 0 || device == w) workers_[w]->gate_all_streams(ev.word(), v);
+}
+
 void Cores::launch_kernels(Worker& wk, hipStream_t s, const ComputeCall& c, long long ref,
                            long long range) {
   if (no_compute) return;
-  int reps = std::max(1, c.repeats);
-  for (int r = 0; r < reps; ++r) {
-    for (auto& k : c.kernels)
-      wk.launch(s, k, c.arrays, ref, range, static_cast<int>(c.local_range), c.global_range);
-    if (!c.repeat_kernel.empty())
-      wk.launch(s, c.repeat_kernel, c.arrays, 0, c.local_range, static_cast<int>(c.local_range),
-                c.local_range);
+  const int reps = std::max(1, c.repeats);
+  auto body = [&](hipStream_t st) {
+    for (int r = 0; r < reps; ++r) {
+      for (auto& k : c.kernels)
+        wk.launch(st, k, c.arrays, ref, range, static_cast<int>(c.local_range), c.global_range);
+      if (!c.repeat_kernel.empty())
+        wk.launch(st, c.repeat_kernel, c.arrays, 0, c.local_range, static_cast<int>(c.local_range),
+                  c.local_range);
+    }
+  };
+  const int launches = reps * (static_cast<int>(c.kernels.size()) + (c.repeat_kernel.empty() ? 0 : 1));
+  if (!wk.gpu() || graph_min_launches <= 0 || launches < graph_min_launches || range <= 0) {
+    body(s);
+    return;
   }
+  // A launch-bound repeat loop is captured once into a hipGraph and replayed;
+  // the key holds everything the captured launches bake in (kernels, ranges,
+  // device buffer addresses).
+  std::string key = std::to_string(reps) + "|" + c.repeat_kernel + "|" + std::to_string(ref) + "|" +
+                    std::to_string(range) + "|" + std::to_string(c.local_range) + "|" +
+                    std::to_string(c.global_range);
+  for (auto& k : c.kernels) key += "|" + k;
+  for (auto& a : c.arrays) key += "|" + std::to_string(reinterpret_cast<uintptr_t>(wk.buffer(a)));
+  wk.launch_graph(s, key, body);
 }
 
 void Cores::full_reads(Worker& wk, hipStream_t s, const ComputeCall& c, uint64_t* h2d) {

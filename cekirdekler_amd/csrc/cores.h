@@ -63,6 +63,26 @@ struct ComputeRecord {  // structured per-call record (observability)
   bool pipelined = false;
 };
 
+// Host-triggered event gating device streams (reference ClUserEvent, a
+// "development cancelled" feature there, Worker.cs:487-560): gated streams
+// execute hipStreamWaitValue32 on a pinned host word; trigger() stores the
+// awaited value.  Words come from a never-freed pinned slab, so a stream can
+// never poll released memory.
+class UserEvent {
+ public:
+  UserEvent();
+  ~UserEvent();
+  uint32_t arm();       // value the next gates wait for
+  void trigger();
+  bool armed() const { return armed_; }
+  const uint32_t* word() const { return word_; }
+
+ private:
+  uint32_t* word_ = nullptr;
+  uint32_t gen_ = 0;
+  bool armed_ = false;
+};
+
 class Cores {
  public:
   Cores(const std::vector<DeviceInfo>& devices, const std::string& source, const CoresConfig& cfg);
@@ -86,6 +106,12 @@ class Cores {
   bool fine_grained = false;
   bool smooth = true;
   bool serial = false;  // run devices one after another (isolated timings)
+  // Repeat loops with at least this many launches per device are captured
+  // into a hipGraph and replayed (0 disables graphs).
+  int graph_min_launches = 8;
+  // Gate every stream of local device `device` (-1: all) on `ev`: work
+  // enqueued afterwards starts only once ev.trigger() (ClUserEvent.cs:102-117).
+  void gate(class UserEvent& ev, int device);
   void set_time_scale(int device, double scale);  // injected heterogeneity (tests/bench)
   void set_dynamic_lds(unsigned bytes);
 

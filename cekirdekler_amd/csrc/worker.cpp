@@ -96,6 +96,7 @@ Worker::~Worker() {
     } catch (...) {
     }
     release_all();
+    for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
     for (auto e : events_) (void)hipEventDestroy(e);
     if (main_) (void)hipStreamDestroy(main_);
     for (auto s : cq_)
@@ -216,6 +217,46 @@ void Worker::sync_all() {
   for (auto& h : pq_)
     for (auto s : h)
       if (s) CEK_HIP(hipStreamSynchronize(s));
+}
+
+void Worker::gate_all_streams(const uint32_t* word, uint32_t value) {
+  if (!gpu()) return;
+  set_device();
+  void* dptr = host_device_ptr(const_cast<uint32_t*>(word));
+  auto gate = [&](hipStream_t s) {
+    CEK_HIP(hipStreamWaitValue32(s, dptr, value, hipStreamWaitValueGte, 0xffffffffu));
+  };
+  gate(main_stream());
+  for (int i = 0; i < qconc_; ++i) gate(compute_stream(i));
+  for (int h = 0; h < 2; ++h)
+    for (int r = 0; r < 3; ++r) gate(pipe_stream(h, r));
+}
+
+void Worker::launch_graph(hipStream_t s, const std::string& key,
+                          const std::function<void(hipStream_t)>& fn) {
+  auto it = graphs_.find(key);
+  if (it == graphs_.end()) {
+    hipGraph_t g = nullptr;
+    CEK_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    try {
+      fn(s);
+    } catch (...) {
+      (void)hipStreamEndCapture(s, &g);
+      if (g) (void)hipGraphDestroy(g);
+      throw;
+    }
+    CEK_HIP(hipStreamEndCapture(s, &g));
+    hipGraphExec_t ex = nullptr;
+    hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    CEK_HIP(e);
+    if (graphs_.size() >= 64) {  // bounded cache: drop everything, recapture on demand
+      for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+      graphs_.clear();
+    }
+    it = graphs_.emplace(key, ex).first;
+  }
+  CEK_HIP(hipGraphLaunch(it->second, s));
 }
 
 int Worker::stream_slot(hipStream_t s) {

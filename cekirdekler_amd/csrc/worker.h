@@ -113,6 +113,16 @@ class Worker {
   uint64_t marker_word(int slot) const;
   long long markers_issued() const { return markers_issued_; }
 
+  // --- user-event gating (ClUserEvent.cs:102-117) -------------------------
+  // Every stream of this worker (created on demand) waits until *word >= value.
+  void gate_all_streams(const uint32_t* word, uint32_t value);
+
+  // --- graph replay of a repeat loop (hipGraph instead of N launches) ------
+  // Launches `fn`'s stream work on `s`; the first call with `key` captures
+  // it into a hipGraph, later calls replay the instantiated graph.
+  void launch_graph(hipStream_t s, const std::string& key, const std::function<void(hipStream_t)>& fn);
+  size_t graphs_cached() const { return graphs_.size(); }
+
   // --- job thread --------------------------------------------------------
   void post(std::function<void()> fn);
   void wait();  // rethrows the first job exception
@@ -148,6 +158,7 @@ class Worker {
   uint64_t last_value_ = 0;
 
   std::unique_ptr<CpuPool> pool_;
+  std::unordered_map<std::string, hipGraphExec_t> graphs_;
 
   std::thread th_;
   std::mutex mu_;

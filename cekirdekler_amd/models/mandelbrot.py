@@ -18,13 +18,16 @@ from ..ops.library import library
 
 FLOP_PER_ITER = 8
 
-# kernel variants: name -> (library kernel, pixels per work item)
+# kernel variants: name -> (library kernel, pixels per work item); "blk16"
+# additionally needs ranges in whole 16-row bands (see kernels/mandelbrot.hip)
+BAND_KERNELS = {"blk16"}
 KERNELS = {
     "quad": ("cek_mandelbrot_f32", 4),          # 4 fixed pixels per work item
     "pool8": ("cek_mandelbrot_pool8_f32", 8),    # wave-pooled, 512-pixel pools
     "pool16": ("cek_mandelbrot_pool16_f32", 16),  # wave-pooled, 1024-pixel pools
     "pk16": ("cek_mandelbrot_pk16_f32", 16),     # pooled, packed pairs + clamp count
     "pk32": ("cek_mandelbrot_pk32_f32", 32),     # same, 2048-pixel pools
+    "blk16": ("cek_mandelbrot_blk16_f32", 4),    # 16×16 pixel block per wave, packed
 }
 
 
@@ -35,6 +38,12 @@ class MandelbrotRenderer:
         self.kernel, self.ppw = KERNELS[kernel]
         if (width * height) % (256 * self.ppw) or width * height >= 2 ** 31:
             raise ValueError(f"width*height must be a multiple of {256 * self.ppw} and below 2^31")
+        # band kernels: 16-row bands, whole bands per device / pipeline chunk
+        self.granularity = 0
+        if kernel in BAND_KERNELS:
+            if width % 64 or height % 16:
+                raise ValueError("blk16 needs width % 64 == 0 and height % 16 == 0")
+            self.granularity = 4 * width
         x0, y0, w, h = view
         self.width, self.height, self.max_iter = width, height, max_iter
         self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library("mandelbrot"))
@@ -52,7 +61,7 @@ class MandelbrotRenderer:
                pipeline_type: bool = PIPELINE_EVENT) -> np.ndarray:
         self.view.next_param(self.size, self.out).compute(
             self.cr, compute_id, self.kernel, self.global_range, 256, 0, pipeline,
-            pipeline_type, blobs)
+            pipeline_type, blobs, granularity=self.granularity)
         self._last_id = compute_id
         return self.out.array.reshape(self.height, self.width)
 

@@ -176,3 +176,14 @@ def test_granularity_quantizes_device_ranges(cpu):
     with pytest.raises(ck.ClComputeError):
         x.compute(c, 2, "inc", 64 * 40, 64, granularity=96)
     c.dispose()
+
+
+def test_user_event_on_cpu_device_is_a_no_op_gate(cr):
+    ev = ck.ClUserEvent()
+    ev.add_cruncher(cr)
+    assert ev.armed
+    x = ck.ClArray(np.zeros(256, np.float32))
+    x.compute(cr, 41, "inc", 256, 64)   # CPU streams are not gated
+    ev.trigger()
+    assert not ev.armed
+    np.testing.assert_array_equal(x.array, 1.0)

@@ -230,3 +230,39 @@ def test_type_matrix_gpu(gpu):
 
     total, fails = type_matrix(gpu[0] + gpu[0], verbose=True)
     assert total == 8 * 2 * 2 * 3 * 3 and fails == 0
+
+
+@pytest.mark.timeout(120, method="thread")
+def test_user_event_gates_enqueued_work(cr):
+    import time
+
+    x = ck.ClArray(1 << 16, np.float32)       # pinned: async copies never block the host
+    x.array[:] = 0
+    ev = ck.ClUserEvent()
+    cr.enqueue_mode = True
+    try:
+        ev.add_cruncher(cr)
+        for _ in range(3):
+            x.compute(cr, 31, "inc", 1 << 16, 256)
+        time.sleep(0.2)
+        gated = bool(np.all(x.array == 0.0))   # nothing may have run yet
+    finally:
+        ev.trigger()
+        cr.enqueue_mode = False               # drains every queue
+    assert gated
+    np.testing.assert_array_equal(x.array, 3.0)
+
+
+def test_repeat_loop_graph_replay(cr):
+    x = ck.ClArray(np.zeros(1 << 14, np.float32))
+    cr.repeat_count = 40
+    try:
+        for it in range(3):                   # capture once, then replay
+            x.compute(cr, 32, "inc", 1 << 14, 256)
+            np.testing.assert_array_equal(x.array, 40.0 * (it + 1))
+        cr.repeat_graph_threshold = 0         # plain launches give the same
+        x.compute(cr, 32, "inc", 1 << 14, 256)
+        np.testing.assert_array_equal(x.array, 160.0)
+    finally:
+        cr.repeat_count = 1
+        cr.repeat_graph_threshold = 8

@@ -14,7 +14,8 @@ from cekirdekler_amd.ops.gemm import TILES
 tiles = sys.argv[2].split(",") if len(sys.argv) > 2 else list(TILES)
 groups = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 4, 8]
 for (M, N, K), tile, gm in [(s, t, g) for s in shapes for t in tiles for g in groups]:
-    g = GemmBf16(M, N, K, devices=g0, tile=tile, group_m=gm)
+    tname, _, sk = tile.partition(":s")
+    g = GemmBf16(M, N, K, devices=g0, tile=tname, group_m=gm, split_k=int(sk or 1))
     for _ in range(3): g.run(resident=True)
     torch.cuda.synchronize()
     t = time.perf_counter(); REPS = 20
