@@ -12,6 +12,7 @@ from .arrays import (BFLOAT16, ClArray, ClBf16Array, ClByteArray, ClCharArray, C
 from .cruncher import (PIPELINE_DRIVER, PIPELINE_EVENT, AcceleratorType, ClComputeError,
                        ClNumberCruncher, ClUserEvent, Cores)
 from .aux_functions import ClBuiltInAuxilliaryFunctions
+from .license import license_text
 from .hardware import ClDevice, ClDevices, ClPlatform, ClPlatforms
 
 __version__ = "0.1.0"
@@ -20,5 +21,5 @@ __all__ = [
     "AcceleratorType", "BFLOAT16", "ClBuiltInAuxilliaryFunctions", "CekError", "ClArray", "ClBf16Array", "ClByteArray", "ClCharArray",
     "ClComputeError", "ClDevice", "ClDevices", "ClDoubleArray", "ClFloatArray", "ClIntArray",
     "ClLongArray", "ClNumberCruncher", "ClParameterGroup", "ClPlatform", "ClPlatforms", "ClUIntArray", "ClUserEvent",
-    "Cores", "FastArr", "PIPELINE_DRIVER", "PIPELINE_EVENT", "cek", "gpu_available",
+    "Cores", "FastArr", "PIPELINE_DRIVER", "PIPELINE_EVENT", "cek", "gpu_available", "license_text",
 ]
