@@ -302,17 +302,21 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             wt[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr] = acc[i][j][r];
-      __threadfence();
+      // Each wave waits for its stores to reach L2; ONE release fence (an L2
+      // write-back) then covers the whole block before the arrival counter —
+      // a fence per wave would write the L2 back eight times.
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       int* flag = reinterpret_cast<int*>(smem);
       if (tid == 0) {
-        const int old = atomicAdd(&tile_cnt[t], 1);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const int old = __hip_atomic_fetch_add(&tile_cnt[t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *flag = old == S - 1;
         if (old == S - 1) tile_cnt[t] = 0;
       }
       __syncthreads();
       if (*flag == 0) return;
-      __threadfence();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       for (int s2 = 0; s2 < S; ++s2) {
         if (s2 == (int)(u % S)) continue;
         const float* wp = W + (size_t)(t * S + s2) * BM * BN;

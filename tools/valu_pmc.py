@@ -10,11 +10,13 @@ from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer  # noqa: E402
 from cekirdekler_amd.models.nbody import NBodySimulation  # noqa: E402
 
 g0 = ck.ClPlatforms.all().gpus()[0]
-m = MandelbrotRenderer(4096, 4096, 256, devices=g0, kernel="pool16")
-m.out.write = False
-for _ in range(3):
-    m.render(1, pipeline=False)
-torch.cuda.synchronize()
+for kern in ("pool16", "blk16"):
+    m = MandelbrotRenderer(4096, 4096, 256, devices=g0, kernel=kern)
+    m.out.write = False
+    for _ in range(3):
+        m.render(1, pipeline=False)
+    torch.cuda.synchronize()
+    m.cr.dispose()
 for b in (2, 4):
     sim = NBodySimulation(262144, devices=g0, bodies_per_item=b)
     for _ in range(2):
