@@ -2,7 +2,7 @@
 double-buffered, stage transitions over xGMI (peer copies, no host bounce).
 
 An ensemble of independent N-body systems flows through
-  stage 1: all-pairs forces (LDS-tiled, rsqrt)       — dominant, O(n²)
+  stage 1: all-pairs forces (LDS-tiled, rsqrt, packed pairs) — dominant, O(n²)
   stage 2: leapfrog kick-drift                       — O(n)
   stage 3: kinetic-energy diagnostic (per-group sums) — O(n)
 Each push advances every stage by one system; after 2·3 pushes results flow
@@ -20,31 +20,50 @@ import cekirdekler_amd as ck
 from cekirdekler_amd.parallel.pipeline import ClPipelineStage
 
 FORCE = r"""
+// 4 bodies per work item as two packed f32x2 pairs (v_pk_* issue: see
+// kernels/nbody.hip) -- the same structure as the library force kernel,
+// written as a user kernel string and JIT-compiled by hiprtc.
+typedef float f2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void force(const float4* pos, const float4* vel, const float* prm,
                                              float4* pos_o, float4* vel_o, float4* acc_o) {
   __shared__ float4 tile[256];
   const int n = (int)prm[2];
-  const float e2 = prm[0];
-  long long i = get_global_id(0);
-  float4 p = pos[i];
-  float ax = 0.f, ay = 0.f, az = 0.f;
+  const f2 e2 = {prm[0], prm[0]};
+  const long long w = get_global_id(0);
+  const long long i0 = (w / 256) * 1024 + (w % 256);
+  f2 px[2], py[2], pz[2], ax[2], ay[2], az[2];
+  for (int p = 0; p < 2; ++p) {
+    float4 b0 = pos[i0 + 512 * p], b1 = pos[i0 + 512 * p + 256];
+    px[p] = (f2){b0.x, b1.x}; py[p] = (f2){b0.y, b1.y}; pz[p] = (f2){b0.z, b1.z};
+    ax[p] = ay[p] = az[p] = (f2){0.f, 0.f};
+  }
   for (int j0 = 0; j0 < n; j0 += 256) {
     __syncthreads();
     tile[threadIdx.x] = pos[j0 + threadIdx.x];
     __syncthreads();
-#pragma unroll 16
+#pragma unroll 4
     for (int j = 0; j < 256; ++j) {
-      float4 q = tile[j];
-      float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
-      float r2 = dx * dx + dy * dy + dz * dz + e2;
-      float inv = __builtin_amdgcn_rsqf(r2);
-      float s = q.w * inv * inv * inv;
-      ax += dx * s; ay += dy * s; az += dz * s;
+      const float4 q = tile[j];
+      const f2 qx = {q.x, q.x}, qy = {q.y, q.y}, qz = {q.z, q.z}, qm = {q.w, q.w};
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const f2 dx = qx - px[p], dy = qy - py[p], dz = qz - pz[p];
+        const f2 r2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, __builtin_elementwise_fma(dz, dz, e2)));
+        const f2 inv = {__builtin_amdgcn_rsqf(r2.x), __builtin_amdgcn_rsqf(r2.y)};
+        const f2 sc = (qm * inv) * (inv * inv);
+        ax[p] = __builtin_elementwise_fma(dx, sc, ax[p]);
+        ay[p] = __builtin_elementwise_fma(dy, sc, ay[p]);
+        az[p] = __builtin_elementwise_fma(dz, sc, az[p]);
+      }
     }
   }
-  acc_o[i] = make_float4(ax, ay, az, 0.f);
-  pos_o[i] = p;
-  vel_o[i] = vel[i];
+  for (int p = 0; p < 2; ++p) {
+    const long long a = i0 + 512 * p, b = a + 256;
+    acc_o[a] = make_float4(ax[p].x, ay[p].x, az[p].x, 0.f);
+    acc_o[b] = make_float4(ax[p].y, ay[p].y, az[p].y, 0.f);
+    pos_o[a] = pos[a]; pos_o[b] = pos[b];
+    vel_o[a] = vel[a]; vel_o[b] = vel[b];
+  }
 }
 """
 KICK = r"""
@@ -83,7 +102,7 @@ devs = [g[i % ng] for i in range(3)]
 f4 = lambda: np.zeros(4 * n, np.float32)  # noqa: E731
 prm = np.array([1e-4, 1.0, float(n), 1e-3], np.float32)
 s1, s2, s3 = ClPipelineStage(), ClPipelineStage(), ClPipelineStage()
-s1.add_devices(devs[0]); s1.add_kernels(FORCE, "force", [n], [256])
+s1.add_devices(devs[0]); s1.add_kernels(FORCE, "force", [n // 4], [256])
 s1.add_input_buffers(f4(), f4()); s1.add_hidden_buffers(prm.copy()); s1.add_output_buffers(f4(), f4(), f4())
 s2.add_devices(devs[1]); s2.add_kernels(KICK, "kick", [n], [256])
 s2.add_input_buffers(f4(), f4(), f4()); s2.add_hidden_buffers(prm.copy()); s2.add_output_buffers(f4(), f4())

@@ -281,39 +281,56 @@ extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_pk32_f32(const 
 // iterations, so a wave's lanes stay busy (85 % on the 4096² view vs 73 % for
 // 256×1 strips) without any refill bookkeeping; the count uses the packed
 // clamp of the pooled variant (4 packed instructions per pixel-iteration).
-extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_blk16_f32(const float* view, const int* size,
-                                                                         int4* out, CEK_HIDDEN) {
-  const long long w = cek_global_id();
+// NB blocks per wave, processed one after another (NB·4 pixels per work
+// item): longer-lived waves amortise workgroup dispatch, which capped the
+// one-block version at ~3.4 resident waves per SIMD (PMC).
+template <int NB>
+__device__ __forceinline__ void mandel_blk(const float* view, const int* size, int4* out, long long off) {
+  const long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x + off;
   const int W = size[0], max_iter = size[2];
-  const long long band_items = 4LL * W;  // 16 rows × W px / 4 px per work item
+  const long long band_items = 4LL * W / NB;  // 16 rows × W px / (4·NB px per work item)
   const long long band = w / band_items;
   const int q = (int)(w - band * band_items);
-  const int blk = q >> 6, l = q & 63;
-  const int row = (int)band * 16 + (l >> 2), col = blk * 16 + (l & 3) * 4;
+  const int wave_in_band = q >> 6, l = q & 63;
+  const int row = (int)band * 16 + (l >> 2);
   const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
   const float ci = y0 + row * dy;
-  f32x2 cr[2] = {{x0 + col * dx, x0 + (col + 1) * dx}, {x0 + (col + 2) * dx, x0 + (col + 3) * dx}};
   const f32x2 civ = {ci, ci};
-  f32x2 zr[2] = {{0.f, 0.f}, {0.f, 0.f}}, zi[2] = {{0.f, 0.f}, {0.f, 0.f}};
-  f32x2 cnt[2] = {{0.f, 0.f}, {0.f, 0.f}}, t[2] = {{1.f, 1.f}, {1.f, 1.f}};
   const f32x2 nbig = {-1048576.f, -1048576.f}, cbig = {4194304.f, 4194304.f}, two = {2.f, 2.f};
-  for (int it = 0; it < max_iter; it += 8) {
+  for (int b = 0; b < NB; ++b) {
+    const int col = (wave_in_band * NB + b) * 16 + (l & 3) * 4;
+    f32x2 cr[2] = {{x0 + col * dx, x0 + (col + 1) * dx}, {x0 + (col + 2) * dx, x0 + (col + 3) * dx}};
+    f32x2 zr[2] = {{0.f, 0.f}, {0.f, 0.f}}, zi[2] = {{0.f, 0.f}, {0.f, 0.f}};
+    f32x2 cnt[2] = {{0.f, 0.f}, {0.f, 0.f}}, t[2] = {{1.f, 1.f}, {1.f, 1.f}};
+    for (int it = 0; it < max_iter; it += 8) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 8; ++u) {
 #pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const f32x2 zi2 = zi[p] * zi[p];
-        const f32x2 m = __builtin_elementwise_fma(zr[p], zr[p], zi2);
-        t[p] = pk_fma_clamp(m, nbig, cbig);
-        cnt[p] += t[p];
-        const f32x2 tz = zr[p] * zi[p];
-        zr[p] = __builtin_elementwise_fma(zr[p], zr[p], -zi2) + cr[p];
-        zi[p] = __builtin_elementwise_fma(tz, two, civ);
+        for (int p = 0; p < 2; ++p) {
+          const f32x2 zi2 = zi[p] * zi[p];
+          const f32x2 m = __builtin_elementwise_fma(zr[p], zr[p], zi2);
+          t[p] = pk_fma_clamp(m, nbig, cbig);
+          cnt[p] += t[p];
+          const f32x2 tz = zr[p] * zi[p];
+          zr[p] = __builtin_elementwise_fma(zr[p], zr[p], -zi2) + cr[p];
+          zi[p] = __builtin_elementwise_fma(tz, two, civ);
+        }
       }
+      // a lane is done with this block once all four of its pixels escaped
+      const f32x2 tm = __builtin_elementwise_max(t[0], t[1]);
+      if (tm.x < 0.5f && tm.y < 0.5f) break;
     }
-    // a lane is done once all four of its pixels escaped
-    if (__builtin_elementwise_max(t[0], t[1]).x < 0.5f && __builtin_elementwise_max(t[0], t[1]).y < 0.5f) break;
+    auto fin = [&](float c) { return min((int)(c + 0.5f), max_iter); };
+    out[((long long)row * W + col) >> 2] = make_int4(fin(cnt[0].x), fin(cnt[0].y), fin(cnt[1].x), fin(cnt[1].y));
   }
-  auto fin = [&](float c) { return min((int)(c + 0.5f), max_iter); };
-  out[((long long)row * W + col) >> 2] = make_int4(fin(cnt[0].x), fin(cnt[0].y), fin(cnt[1].x), fin(cnt[1].y));
+}
+
+extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_blk16_f32(const float* view, const int* size,
+                                                                         int4* out, CEK_HIDDEN) {
+  mandel_blk<1>(view, size, out, __cek_off);
+}
+
+extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_blk64_f32(const float* view, const int* size,
+                                                                         int4* out, CEK_HIDDEN) {
+  mandel_blk<4>(view, size, out, __cek_off);
 }

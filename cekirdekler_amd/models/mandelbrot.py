@@ -20,7 +20,7 @@ FLOP_PER_ITER = 8
 
 # kernel variants: name -> (library kernel, pixels per work item); "blk16"
 # additionally needs ranges in whole 16-row bands (see kernels/mandelbrot.hip)
-BAND_KERNELS = {"blk16"}
+BAND_KERNELS = {"blk16", "blk64"}
 KERNELS = {
     "quad": ("cek_mandelbrot_f32", 4),          # 4 fixed pixels per work item
     "pool8": ("cek_mandelbrot_pool8_f32", 8),    # wave-pooled, 512-pixel pools
@@ -28,6 +28,7 @@ KERNELS = {
     "pk16": ("cek_mandelbrot_pk16_f32", 16),     # pooled, packed pairs + clamp count
     "pk32": ("cek_mandelbrot_pk32_f32", 32),     # same, 2048-pixel pools
     "blk16": ("cek_mandelbrot_blk16_f32", 4),    # 16×16 pixel block per wave, packed
+    "blk64": ("cek_mandelbrot_blk64_f32", 16),   # four 16×16 blocks per wave
 }
 
 
@@ -41,9 +42,9 @@ class MandelbrotRenderer:
         # band kernels: 16-row bands, whole bands per device / pipeline chunk
         self.granularity = 0
         if kernel in BAND_KERNELS:
-            if width % 64 or height % 16:
-                raise ValueError("blk16 needs width % 64 == 0 and height % 16 == 0")
-            self.granularity = 4 * width
+            if width % (16 * self.ppw) or height % 16:
+                raise ValueError(f"{kernel} needs width % {16 * self.ppw} == 0 and height % 16 == 0")
+            self.granularity = 16 * width // self.ppw  # one 16-row band in work items
         x0, y0, w, h = view
         self.width, self.height, self.max_iter = width, height, max_iter
         self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library("mandelbrot"))
