@@ -20,7 +20,20 @@ FLOP_PER_ITER = 8
 
 # kernel variants: name -> (library kernel, pixels per work item); "blk16"
 # additionally needs ranges in whole 16-row bands (see kernels/mandelbrot.hip)
-BAND_KERNELS = {"blk16", "blk64"}
+BAND_KERNELS = {
+    # name: (library kernel, pixels per work item, work-group size)
+    "quad": ("cek_mandelbrot_f32", 4, 256),           # 4 fixed pixels per work item
+    "pool8": ("cek_mandelbrot_pool8_f32", 8, 256),     # wave-pooled, 512-pixel pools
+    "pool16": ("cek_mandelbrot_pool16_f32", 16, 256),  # wave-pooled, 1024-pixel pools
+    "pk16": ("cek_mandelbrot_pk16_f32", 16, 256),      # pooled, packed pairs + clamp count
+    "pk32": ("cek_mandelbrot_pk32_f32", 32, 256),      # same, 2048-pixel pools
+    # 16×16 pixel block per wave, packed; one-wave work-groups so a finished
+    # wave's slot is refilled at once (a 4-wave group holds all four SIMD
+    # slots until its slowest block is done)
+    "blk16": ("cek_mandelbrot_blk16_f32", 4, 64),
+    "blk16w4": ("cek_mandelbrot_blk16_f32", 4, 256),
+    "blk64": ("cek_mandelbrot_blk64_f32", 16, 64),     # four 16×16 blocks per wave
+}
 KERNELS = {
     "quad": ("cek_mandelbrot_f32", 4),          # 4 fixed pixels per work item
     "pool8": ("cek_mandelbrot_pool8_f32", 8),    # wave-pooled, 512-pixel pools
@@ -36,9 +49,11 @@ class MandelbrotRenderer:
     def __init__(self, width: int = 4096, height: int = 4096, max_iter: int = 256,
                  view=(-2.0, -1.5, 3.0, 3.0), devices=None, cruncher: ClNumberCruncher | None = None,
                  kernel: str = "pool16"):
-        self.kernel, self.ppw = KERNELS[kernel]
+        self.kernel, self.ppw, self.local = KERNELS[kernel]
         if (width * height) % (256 * self.ppw) or width * height >= 2 ** 31:
             raise ValueError(f"width*height must be a multiple of {256 * self.ppw} and below 2^31")
+        if self.local != 256 and kernel not in BAND_KERNELS:
+            raise ValueError("only the band kernels take other work-group sizes")
         # band kernels: 16-row bands, whole bands per device / pipeline chunk
         self.granularity = 0
         if kernel in BAND_KERNELS:
@@ -61,7 +76,7 @@ class MandelbrotRenderer:
     def render(self, compute_id: int = 1, pipeline: bool = True, blobs: int = 8,
                pipeline_type: bool = PIPELINE_EVENT) -> np.ndarray:
         self.view.next_param(self.size, self.out).compute(
-            self.cr, compute_id, self.kernel, self.global_range, 256, 0, pipeline,
+            self.cr, compute_id, self.kernel, self.global_range, self.local, 0, pipeline,
             pipeline_type, blobs, granularity=self.granularity)
         self._last_id = compute_id
         return self.out.array.reshape(self.height, self.width)

@@ -28,7 +28,7 @@ for e in a.extra:
     path, rest = e.split("|")
     name, ppw = rest.split(",")
     key = f"{name}@{path.rsplit('/', 1)[-1]}"
-    mb.KERNELS[key] = (name, int(ppw))
+    mb.KERNELS[key] = (name, int(ppw), 256)
     variants.append((key, path + "|" + name))
 
 ref_img = None
