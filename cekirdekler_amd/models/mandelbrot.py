@@ -18,9 +18,10 @@ from ..ops.library import library
 
 FLOP_PER_ITER = 8
 
-# kernel variants: name -> (library kernel, pixels per work item); "blk16"
-# additionally needs ranges in whole 16-row bands (see kernels/mandelbrot.hip)
-BAND_KERNELS = {
+# kernel variants; the band kernels additionally need device and pipeline
+# chunk ranges made of whole 16-row bands (see kernels/mandelbrot.hip)
+BAND_KERNELS = {"blk16", "blk16w4", "blk64"}
+KERNELS = {
     # name: (library kernel, pixels per work item, work-group size)
     "quad": ("cek_mandelbrot_f32", 4, 256),           # 4 fixed pixels per work item
     "pool8": ("cek_mandelbrot_pool8_f32", 8, 256),     # wave-pooled, 512-pixel pools
@@ -33,15 +34,6 @@ BAND_KERNELS = {
     "blk16": ("cek_mandelbrot_blk16_f32", 4, 64),
     "blk16w4": ("cek_mandelbrot_blk16_f32", 4, 256),
     "blk64": ("cek_mandelbrot_blk64_f32", 16, 64),     # four 16×16 blocks per wave
-}
-KERNELS = {
-    "quad": ("cek_mandelbrot_f32", 4),          # 4 fixed pixels per work item
-    "pool8": ("cek_mandelbrot_pool8_f32", 8),    # wave-pooled, 512-pixel pools
-    "pool16": ("cek_mandelbrot_pool16_f32", 16),  # wave-pooled, 1024-pixel pools
-    "pk16": ("cek_mandelbrot_pk16_f32", 16),     # pooled, packed pairs + clamp count
-    "pk32": ("cek_mandelbrot_pk32_f32", 32),     # same, 2048-pixel pools
-    "blk16": ("cek_mandelbrot_blk16_f32", 4),    # 16×16 pixel block per wave, packed
-    "blk64": ("cek_mandelbrot_blk64_f32", 16),   # four 16×16 blocks per wave
 }
 
 

@@ -71,3 +71,28 @@ def test_aux_functions_run_on_cpu(cpu):
     np.testing.assert_array_equal(h.array, rne)
     np.testing.assert_allclose(lv.array, x.array * 0.5)
     cr.dispose()
+
+
+def test_mandelbrot_kernel_table_is_consistent():
+    """Every Mandelbrot variant maps to a library kernel with a valid range
+    decomposition (checked on the host; the kernels run in the GPU tier)."""
+    from cekirdekler_amd.models import mandelbrot as mb
+    from cekirdekler_amd.ops.library import ARITY, LIBRARY
+
+    for name, (kernel, ppw, local) in mb.KERNELS.items():
+        assert kernel in LIBRARY["mandelbrot"] and ARITY[kernel] == 3, name
+        assert local in (64, 256) and (local == 256 or name in mb.BAND_KERNELS)
+        W, H = 4096, 4096
+        G = W * H // ppw
+        assert G % local == 0
+        if name in mb.BAND_KERNELS:
+            band = 16 * W // ppw          # work items per 16-row band
+            assert band % local == 0 and G % band == 0 and (G // band) % 8 == 0
+
+
+def test_library_arity_covers_every_kernel():
+    from cekirdekler_amd.ops.library import ARITY, LIBRARY
+
+    for names in LIBRARY.values():
+        for k in names:
+            assert k in ARITY, k
