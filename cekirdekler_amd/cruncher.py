@@ -183,6 +183,20 @@ class ClNumberCruncher:
         if self._cores:
             self._cores.graph_min_launches = int(n)
 
+    # ------------------------------------------------------------ failure handling
+    def disable_device(self, device: int) -> None:
+        """Drop a local device: later computes re-balance over the others
+        (SURVEY §5.3 "drop device and re-balance")."""
+        self._cores.set_device_enabled(int(device), False)
+
+    def enable_device(self, device: int) -> None:
+        self._cores.set_device_enabled(int(device), True)
+
+    def device_enabled(self, device: int) -> bool:
+        return bool(self._cores.device_enabled(int(device)))
+
+    auto_failover = _prop("auto_failover")
+
     no_compute_mode = _prop("no_compute")
     fine_grained_queue_control = _prop("fine_grained")
     enqueue_mode_async_enable = _prop("async_enqueue")

@@ -251,6 +251,11 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("smooth", &Cores::smooth)
       .def_readwrite("serial", &Cores::serial)
       .def_readwrite("graph_min_launches", &Cores::graph_min_launches)
+      .def_readwrite("auto_failover", &Cores::auto_failover)
+      .def_property_readonly("failovers", &Cores::failovers)
+      .def("set_device_enabled", &Cores::set_device_enabled)
+      .def("device_enabled", &Cores::device_enabled)
+      .def("inject_failure", &Cores::inject_failure)
       .def("gate", &Cores::gate, py::arg("event"), py::arg("device") = -1)
       .def_readwrite("dist_gather_writes", &Cores::dist_gather_writes)
       .def_readwrite("dist_broadcast_reads", &Cores::dist_broadcast_reads)

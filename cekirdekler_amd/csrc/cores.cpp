@@ -43,6 +43,8 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
   }
   global_devices_ = static_cast<int>(workers_.size());
   time_scale_.assign(workers_.size(), 1.0);
+  enabled_.assign(workers_.size(), true);
+  inject_.assign(workers_.size(), 0);
   build_ms_ = now_ms() - t0;
 }
 
@@ -62,6 +64,53 @@ std::vector<KernelSig> Cores::kernels() const {
 void Cores::set_time_scale(int device, double scale) {
   if (device < 0 || device >= static_cast<int>(time_scale_.size())) throw Error("bad device index");
   time_scale_[device] = scale;
+}
+
+void Cores::set_device_enabled(int device, bool on) {
+  if (device < 0 || device >= static_cast<int>(enabled_.size())) throw Error("bad device index");
+  if (!on && ex_) throw Error("devices cannot be disabled in a distributed job");
+  enabled_[device] = on;
+}
+
+void Cores::inject_failure(int device, int count) {
+  if (device < 0 || device >= static_cast<int>(inject_.size())) throw Error("bad device index");
+  inject_[device] = count;
+}
+
+// Runs the reference law over the enabled devices only (all of them unless
+// some were disabled); disabled devices keep a zero range.
+void Cores::balance(BalancerState& st, bool first, long long G, long long step) {
+  const int D = global_devices_;
+  std::vector<int> on;
+  for (int i = 0; i < D; ++i)
+    if (i < global_base_ || i >= global_base_ + num_devices() || enabled_[i - global_base_]) on.push_back(i);
+  if (on.empty()) throw Error("every device is disabled");
+  if (static_cast<int>(on.size()) == D) {
+    if (first)
+      initial_split(D, smooth, st.history, G, st.ranges, step);
+    else
+      load_balance(st.bench, smooth, st.history, G, st.ranges, step);
+    return;
+  }
+  const size_t n = on.size();
+  std::vector<long long> r(n);
+  std::vector<double> b(n);
+  std::vector<std::vector<double>> h(st.history.size(), std::vector<double>(n));
+  for (size_t j = 0; j < n; ++j) {
+    r[j] = st.ranges.empty() ? 0 : st.ranges[on[j]];
+    b[j] = st.bench.empty() ? 0.0 : st.bench[on[j]];
+    for (size_t d = 0; d < st.history.size(); ++d) h[d][j] = st.history[d][on[j]];
+  }
+  const bool sub_first = first || std::all_of(r.begin(), r.end(), [](long long x) { return x == 0; });
+  if (sub_first)
+    initial_split(static_cast<int>(n), smooth, h, G, r, step);
+  else
+    load_balance(b, smooth, h, G, r, step);
+  st.ranges.assign(D, 0);
+  for (size_t j = 0; j < n; ++j) {
+    st.ranges[on[j]] = r[j];
+    for (size_t d = 0; d < st.history.size(); ++d) st.history[d][on[j]] = h[d][j];
+  }
 }
 
 void Cores::set_dynamic_lds(unsigned bytes) {
@@ -538,6 +587,10 @@ void Cores::run_device(int w, const ComputeCall& c, long long ref, long long ran
   Worker& wk = *workers_[w];
   const int gidx = global_base_ + w;
   TraceRange tr("cek.device" + std::to_string(gidx) + ".id" + std::to_string(c.compute_id));
+  if (range > 0 && inject_[w] > 0) {
+    --inject_[w];
+    throw Error("injected failure on device " + std::to_string(w));
+  }
   double t0 = now_ms();
   if (range > 0) {
     wk.set_device();
@@ -555,6 +608,28 @@ void Cores::run_device(int w, const ComputeCall& c, long long ref, long long ran
 }
 
 void Cores::compute(const ComputeCall& c) {
+  DeviceFailure f;
+  compute_once(c, (auto_failover && !ex_) ? &f : nullptr);
+  if (f.devices.empty()) return;
+  // Failover: the surviving devices' slices are complete; each failed
+  // device's slice is recomputed on a surviving device (from the same host
+  // inputs), and the failed device is dropped from later splits.
+  for (int w : f.devices) enabled_[w] = false;
+  int survivor = -1;
+  for (int w = 0; w < num_devices() && survivor < 0; ++w)
+    if (enabled_[w]) survivor = w;
+  if (survivor < 0) throw Error(std::string("every device failed: ") + f.what());
+  auto& st = state_[c.compute_id];
+  for (int w : f.devices) {
+    const int g = global_base_ + w;
+    double ms = 0;
+    uint64_t h = 0, d = 0;
+    run_device(survivor, c, st.references[g], st.ranges[g], false, &ms, &h, &d);
+  }
+  ++failovers_;
+}
+
+void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
   if (error_code_ != 0) throw Error("cannot compute, initialisation failed: " + error_);
   const long long G = c.global_range, L = c.local_range;
   if (G <= 0) throw Error("global range must be positive");
@@ -607,17 +682,22 @@ void Cores::compute(const ComputeCall& c) {
   if (st.bench.size() != static_cast<size_t>(D)) st.bench.assign(D, 0.0);
   const bool first = fresh || std::all_of(st.ranges.begin(), st.ranges.end(), [](long long r) { return r == 0; });
   if (!(enqueue_mode_ && !first)) {
+    int active = 0;
+    for (int i = 0; i < D; ++i)
+      if (i < global_base_ || i >= global_base_ + nloc || enabled_[i - global_base_]) ++active;
     if (first) {
       // Cores.cs:569-596
-      std::vector<long long> eq(D, G / D);
-      eq[0] += G - (G / D) * D;
+      std::vector<long long> eq(active, G / std::max(active, 1));
+      if (active) eq[0] += G - (G / active) * active;
       bool b1 = std::all_of(eq.begin(), eq.end(), [&](long long r) { return r >= B * U; });
       long long step = (b1 && pipe_req && G >= B * U) ? B * U : U;
-      initial_split(D, smooth, st.history, G, st.ranges, step);
+      balance(st, true, G, step);
     } else {
-      bool b1 = std::all_of(st.ranges.begin(), st.ranges.end(), [&](long long r) { return r >= B * U; });
+      bool b1 = true;
+      for (int i = 0; i < D; ++i)
+        if (st.ranges[i] != 0 && st.ranges[i] < B * U) b1 = false;
       long long step = (b1 && pipe_req && G >= B * U) ? B * U : U;
-      load_balance(st.bench, smooth, st.history, G, st.ranges, step);
+      balance(st, false, G, step);
     }
   }
   st.references.assign(D, 0);
@@ -629,15 +709,20 @@ void Cores::compute(const ComputeCall& c) {
   // Pipelining eligibility (Cores.cs:624-652), decided per call for all devices.
   bool pipelined = pipe_req && c.repeats <= 1 && !enqueue_mode_;
   for (int i = 0; i < D && pipelined; ++i)
-    if (st.ranges[i] % (B * U) != 0 || st.ranges[i] < B * U) pipelined = false;
+    if (st.ranges[i] != 0 && (st.ranges[i] % (B * U) != 0 || st.ranges[i] < B * U)) pipelined = false;
   if (comm_ && (dist_gather_writes || dist_broadcast_reads)) pipelined = false;
 
   std::vector<double> ms(nloc, 0.0);
   std::vector<uint64_t> h2d(nloc, 0), d2h(nloc, 0);
+  DeviceFailure failure;
   if (nloc == 1 || serial) {
     for (int w = 0; w < nloc; ++w) {
       int g = global_base_ + w;
-      run_device(w, c, st.references[g], st.ranges[g], pipelined, &ms[w], &h2d[w], &d2h[w]);
+      try {
+        run_device(w, c, st.references[g], st.ranges[g], pipelined, &ms[w], &h2d[w], &d2h[w]);
+      } catch (const std::exception& e) {
+        failure.add(w, e.what());
+      }
     }
   } else {
     for (int w = 0; w < nloc; ++w) {
@@ -647,7 +732,17 @@ void Cores::compute(const ComputeCall& c) {
         run_device(w, c, ref, rng, pipelined, &ms[w], &h2d[w], &d2h[w]);
       });
     }
-    for (auto& w : workers_) w->wait();
+    for (int w = 0; w < nloc; ++w) {
+      try {
+        workers_[w]->wait();
+      } catch (const std::exception& e) {
+        failure.add(w, e.what());
+      }
+    }
+  }
+  if (!failure.devices.empty()) {
+    if (!failed) throw Error(failure.what());
+    *failed = failure;
   }
   last_id_ = c.compute_id;
   if (!enqueue_mode_) {

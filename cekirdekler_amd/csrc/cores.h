@@ -83,6 +83,17 @@ class UserEvent {
   bool armed_ = false;
 };
 
+// A compute() in which one or more local devices raised.
+struct DeviceFailure : std::exception {
+  std::vector<int> devices;
+  std::string msg;
+  void add(int w, const std::string& m) {
+    devices.push_back(w);
+    msg += (msg.empty() ? "" : "; ") + ("device " + std::to_string(w) + ": " + m);
+  }
+  const char* what() const noexcept override { return msg.c_str(); }
+};
+
 class Cores {
  public:
   Cores(const std::vector<DeviceInfo>& devices, const std::string& source, const CoresConfig& cfg);
@@ -113,6 +124,16 @@ class Cores {
   // enqueued afterwards starts only once ev.trigger() (ClUserEvent.cs:102-117).
   void gate(class UserEvent& ev, int device);
   void set_time_scale(int device, double scale);  // injected heterogeneity (tests/bench)
+  // ---- failure handling ----
+  // A disabled device gets no range; the balancer runs over the others.
+  void set_device_enabled(int device, bool on);
+  bool device_enabled(int device) const { return enabled_.at(device); }
+  // Make the next `count` computes on local device `device` fail (tests).
+  void inject_failure(int device, int count);
+  // When a device fails during compute(): disable it and re-run the call on
+  // the remaining devices (single-process jobs only).
+  bool auto_failover = false;
+  int failovers() const { return failovers_; }
   void set_dynamic_lds(unsigned bytes);
 
   // ---- state ----
@@ -168,6 +189,11 @@ class Cores {
   std::vector<std::unique_ptr<Worker>> workers_;
   std::map<int, BalancerState> state_;
   std::vector<double> time_scale_;
+  std::vector<bool> enabled_;
+  std::vector<int> inject_;
+  int failovers_ = 0;
+  void compute_once(const ComputeCall& call, struct DeviceFailure* failed);
+  void balance(struct BalancerState& st, bool first, long long G, long long step);
   std::string error_;
   int error_code_ = 0;
   double build_ms_ = 0;

@@ -187,3 +187,38 @@ def test_user_event_on_cpu_device_is_a_no_op_gate(cr):
     ev.trigger()
     assert not ev.armed
     np.testing.assert_array_equal(x.array, 1.0)
+
+
+def test_disable_device_rebalances_over_the_others(cpu):
+    c = ck.ClNumberCruncher(cpu + cpu + cpu, SRC)
+    x = ck.ClArray(np.zeros(64 * 30, np.float32))
+    x.compute(c, 1, "inc", 64 * 30, 64)
+    c.disable_device(1)
+    x.compute(c, 1, "inc", 64 * 30, 64)
+    r = c.ranges(1)
+    assert r[1] == 0 and sum(r) == 64 * 30 and r[0] > 0 and r[2] > 0
+    c.enable_device(1)
+    for _ in range(3):
+        x.compute(c, 1, "inc", 64 * 30, 64)
+    assert c.ranges(1)[1] > 0
+    np.testing.assert_array_equal(x.array, 5.0)
+    c.dispose()
+
+
+def test_injected_failure_and_auto_failover(cpu):
+    c = ck.ClNumberCruncher(cpu + cpu, SRC)
+    x = ck.ClArray(np.zeros(64 * 16, np.float32))
+    c.cores.inject_failure(1, 1)
+    with pytest.raises(Exception, match="injected failure"):
+        x.compute(c, 1, "inc", 64 * 16, 64)
+    assert c.device_enabled(1)                 # without failover nothing changes
+    x.array[:] = 0
+    c.auto_failover = True
+    c.cores.inject_failure(1, 1)
+    x.compute(c, 2, "inc", 64 * 16, 64)        # device 1 fails; its slice reruns on device 0
+    assert not c.device_enabled(1) and c.cores.failovers == 1
+    np.testing.assert_array_equal(x.array, 1.0)
+    x.compute(c, 2, "inc", 64 * 16, 64)        # later calls skip the dropped device
+    assert c.ranges(2) == [64 * 16, 0]
+    np.testing.assert_array_equal(x.array, 2.0)
+    c.dispose()
