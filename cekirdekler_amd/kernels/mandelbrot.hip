@@ -334,3 +334,37 @@ extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_blk64_f32(const
                                                                          int4* out, CEK_HIDDEN) {
   mandel_blk<4>(view, size, out, __cek_off);
 }
+
+// 8×16 pixel block per wave, one packed pair (2 horizontally adjacent
+// pixels) per lane: a smaller block keeps the lanes' escape times closer
+// (87 % vs 85 % busy lanes on the 4096² view) at half the per-wave ILP,
+// which the one-wave work-groups make up with occupancy.  Bands of 8 rows.
+extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8_f32(const float* view, const int* size,
+                                                                       int2* out, CEK_HIDDEN) {
+  const long long w = cek_global_id();
+  const int W = size[0], max_iter = size[2];
+  const long long band_items = 4LL * W;  // 8 rows × W px / 2 px per work item
+  const long long band = w / band_items;
+  const int q = (int)(w - band * band_items);
+  const int blk = q >> 6, l = q & 63;
+  const int row = (int)band * 8 + (l >> 3), col = blk * 16 + (l & 7) * 2;
+  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
+  const float ci = y0 + row * dy;
+  const f32x2 cr = {x0 + col * dx, x0 + (col + 1) * dx}, civ = {ci, ci};
+  f32x2 zr = {0.f, 0.f}, zi = {0.f, 0.f}, cnt = {0.f, 0.f}, t = {1.f, 1.f};
+  const f32x2 nbig = {-1048576.f, -1048576.f}, cbig = {4194304.f, 4194304.f}, two = {2.f, 2.f};
+  for (int it = 0; it < max_iter; it += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const f32x2 zi2 = zi * zi;
+      const f32x2 m = __builtin_elementwise_fma(zr, zr, zi2);
+      t = pk_fma_clamp(m, nbig, cbig);
+      cnt += t;
+      const f32x2 tz = zr * zi;
+      zr = __builtin_elementwise_fma(zr, zr, -zi2) + cr;
+      zi = __builtin_elementwise_fma(tz, two, civ);
+    }
+    if (t.x < 0.5f && t.y < 0.5f) break;
+  }
+  out[((long long)row * W + col) >> 1] = make_int2(min((int)(cnt.x + 0.5f), max_iter), min((int)(cnt.y + 0.5f), max_iter));
+}

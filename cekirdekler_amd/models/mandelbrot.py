@@ -20,7 +20,8 @@ FLOP_PER_ITER = 8
 
 # kernel variants; the band kernels additionally need device and pipeline
 # chunk ranges made of whole 16-row bands (see kernels/mandelbrot.hip)
-BAND_KERNELS = {"blk16", "blk16w4", "blk64"}
+BAND_ROWS = {"blk16": 16, "blk16w4": 16, "blk64": 16, "blk8": 8}  # rows per band
+BAND_KERNELS = set(BAND_ROWS)
 KERNELS = {
     # name: (library kernel, pixels per work item, work-group size)
     "quad": ("cek_mandelbrot_f32", 4, 256),           # 4 fixed pixels per work item
@@ -34,6 +35,7 @@ KERNELS = {
     "blk16": ("cek_mandelbrot_blk16_f32", 4, 64),
     "blk16w4": ("cek_mandelbrot_blk16_f32", 4, 256),
     "blk64": ("cek_mandelbrot_blk64_f32", 16, 64),     # four 16×16 blocks per wave
+    "blk8": ("cek_mandelbrot_blk8_f32", 2, 64),        # 8×16 block per wave, one pair per lane
 }
 
 
@@ -49,9 +51,11 @@ class MandelbrotRenderer:
         # band kernels: 16-row bands, whole bands per device / pipeline chunk
         self.granularity = 0
         if kernel in BAND_KERNELS:
-            if width % (16 * self.ppw) or height % 16:
-                raise ValueError(f"{kernel} needs width % {16 * self.ppw} == 0 and height % 16 == 0")
-            self.granularity = 16 * width // self.ppw  # one 16-row band in work items
+            rows = BAND_ROWS[kernel]
+            block_w = 64 * self.ppw // rows  # pixels per wave row
+            if width % block_w or height % rows:
+                raise ValueError(f"{kernel} needs width % {block_w} == 0 and height % {rows} == 0")
+            self.granularity = rows * width // self.ppw  # one band in work items
         x0, y0, w, h = view
         self.width, self.height, self.max_iter = width, height, max_iter
         self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library("mandelbrot"))

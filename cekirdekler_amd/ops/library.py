@@ -21,7 +21,7 @@ LIBRARY = {
     "sgemm8p_bf16": ["cek_sgemm8p_bf16_r8", "cek_sgemm8p_bf16_r10"],
     "mandelbrot": ["cek_mandelbrot_f32", "cek_mandelbrot_pool16_f32", "cek_mandelbrot_pool8_f32",
                    "cek_mandelbrot_pk16_f32", "cek_mandelbrot_pk32_f32", "cek_mandelbrot_blk16_f32",
-                   "cek_mandelbrot_blk64_f32"],
+                   "cek_mandelbrot_blk64_f32", "cek_mandelbrot_blk8_f32"],
     "nbody": ["cek_nbody_f32_b2", "cek_nbody_integrate_f32_b2", "cek_nbody_energy_f32_b2",
               "cek_nbody_f32_b4", "cek_nbody_integrate_f32_b4", "cek_nbody_energy_f32_b4"],
     "reduce": ["cek_reduce_sum_f32", "cek_reduce_sum_f32_final"],

@@ -121,7 +121,7 @@ def test_gemm_two_logical_devices_balanced():
     assert np.abs(c - ref).max() < 5e-3 * np.abs(ref).max()
 
 
-@pytest.mark.parametrize("kernel", ["quad", "pool8", "pool16", "pk16", "pk32", "blk16", "blk64"])
+@pytest.mark.parametrize("kernel", ["quad", "pool8", "pool16", "pk16", "pk32", "blk16", "blk64", "blk8"])
 def test_mandelbrot_event_pipeline_matches_numpy(kernel):
     from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
 

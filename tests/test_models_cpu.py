@@ -86,7 +86,7 @@ def test_mandelbrot_kernel_table_is_consistent():
         G = W * H // ppw
         assert G % local == 0
         if name in mb.BAND_KERNELS:
-            band = 16 * W // ppw          # work items per 16-row band
+            band = mb.BAND_ROWS[name] * W // ppw   # work items per band
             assert band % local == 0 and G % band == 0 and (G // band) % 8 == 0
 
 
