@@ -252,6 +252,15 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("serial", &Cores::serial)
       .def_readwrite("graph_min_launches", &Cores::graph_min_launches)
       .def_readwrite("auto_failover", &Cores::auto_failover)
+      .def_readwrite("record_schedule", &Cores::record_schedule)
+      .def("schedule",
+           [](Cores& c) {
+             py::list out;
+             for (auto& o : c.schedule())
+               out.append(py::make_tuple(o.device, o.op, o.stream, o.begin, o.count, o.event));
+             return out;
+           })
+      .def("clear_schedule", &Cores::clear_schedule)
       .def_property_readonly("failovers", &Cores::failovers)
       .def("set_device_enabled", &Cores::set_device_enabled)
       .def("device_enabled", &Cores::device_enabled)

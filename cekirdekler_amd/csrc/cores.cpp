@@ -462,18 +462,23 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
   const long long per_half = B / halves;
   hipStream_t m = wk.main_stream();
   full_reads(wk, m, c, h2d);
+  log_op(gidx, "h2d", 0, -1, -1);  // full reads
   int slot = 0;
   hipEvent_t ev_full = nullptr;
   if (wk.gpu()) {
-    ev_full = wk.event(slot++);
+    ev_full = wk.event(slot);
     CEK_HIP(hipEventRecord(ev_full, m));
     for (int h = 0; h < halves; ++h) CEK_HIP(hipStreamWaitEvent(wk.pipe_stream(h, 1), ev_full, 0));
   }
+  log_op(gidx, "rec", 0, 0, 0, slot);
+  for (int h = 0; h < halves; ++h) log_op(gidx, "wait", 17 + 3 * h + 1, 0, 0, slot);
+  ++slot;
   // Interleave the two half-pipelines' chunks so both read streams start early.
   for (long long k = 0; k < per_half; ++k) {
     for (int h = 0; h < halves; ++h) {
       hipStream_t rs = wk.pipe_stream(h, 0), ks = wk.pipe_stream(h, 1), ws = wk.pipe_stream(h, 2);
       long long off = ref + h * (range / halves) + k * chunk;
+      const int rsid = 17 + 3 * h, ksid = rsid + 1, wsid = rsid + 2;
       for (auto& a : c.arrays) {
         if (a.zc || !a.partial) continue;
         uint64_t b, n;
@@ -481,17 +486,25 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
         wk.h2d(rs, a, b, n);
         *h2d += n * a.elem_size;
       }
+      log_op(gidx, "h2d", rsid, off, chunk);
       if (wk.gpu()) {
-        hipEvent_t er = wk.event(slot++);
+        hipEvent_t er = wk.event(slot);
         CEK_HIP(hipEventRecord(er, rs));
         CEK_HIP(hipStreamWaitEvent(ks, er, 0));
       }
+      log_op(gidx, "rec", rsid, off, chunk, slot);
+      log_op(gidx, "wait", ksid, off, chunk, slot);
+      ++slot;
       launch_kernels(wk, ks, c, off, chunk);
+      log_op(gidx, "kernel", ksid, off, chunk);
       if (wk.gpu()) {
-        hipEvent_t ek = wk.event(slot++);
+        hipEvent_t ek = wk.event(slot);
         CEK_HIP(hipEventRecord(ek, ks));
         CEK_HIP(hipStreamWaitEvent(ws, ek, 0));
       }
+      log_op(gidx, "rec", ksid, off, chunk, slot);
+      log_op(gidx, "wait", wsid, off, chunk, slot);
+      ++slot;
       for (auto& a : c.arrays) {
         if (a.zc || !a.write || a.write_all) continue;
         uint64_t b, n;
@@ -499,20 +512,26 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
         wk.d2h(ws, a, b, n);
         *d2h += n * a.elem_size;
       }
+      log_op(gidx, "d2h", wsid, off, chunk);
     }
   }
   // write-all owners download after every chunk's kernels
   bool any_all = false;
   for (auto& a : c.arrays) any_all |= (a.write && a.write_all && !a.zc);
-  if (wk.gpu()) {
-    for (int h = 0; h < halves; ++h) {
-      hipEvent_t e = wk.event(slot++);
+  for (int h = 0; h < halves; ++h) {
+    if (wk.gpu()) {
+      hipEvent_t e = wk.event(slot);
       CEK_HIP(hipEventRecord(e, wk.pipe_stream(h, 1)));
       CEK_HIP(hipStreamWaitEvent(m, e, 0));
-      hipEvent_t e2 = wk.event(slot++);
+      hipEvent_t e2 = wk.event(slot + 1);
       CEK_HIP(hipEventRecord(e2, wk.pipe_stream(h, 2)));
       CEK_HIP(hipStreamWaitEvent(m, e2, 0));
     }
+    log_op(gidx, "rec", 17 + 3 * h + 1, 0, 0, slot);
+    log_op(gidx, "wait", 0, 0, 0, slot);
+    log_op(gidx, "rec", 17 + 3 * h + 2, 0, 0, slot + 1);
+    log_op(gidx, "wait", 0, 0, 0, slot + 1);
+    slot += 2;
   }
   if (any_all) {
     for (size_t i = 0; i < c.arrays.size(); ++i) {
@@ -533,18 +552,24 @@ void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long
   const long long chunk = range / B;
   hipStream_t m = wk.main_stream();
   full_reads(wk, m, c, h2d);
+  log_op(gidx, "h2d", 0, -1, -1);  // full reads
   int slot = 0;
   hipEvent_t ev_full = nullptr;
   if (wk.gpu()) {
-    ev_full = wk.event(slot++);
+    ev_full = wk.event(slot);
     CEK_HIP(hipEventRecord(ev_full, m));
   }
+  log_op(gidx, "rec", 0, 0, 0, slot);
+  const int full_slot = slot++;
   const int nq = wk.queue_concurrency();
   std::vector<char> used(16, 0);
   for (long long k = 0; k < B; ++k) {
     int qi = static_cast<int>(k % nq);
     hipStream_t s = wk.compute_stream(qi);
-    if (wk.gpu() && !used[qi]) CEK_HIP(hipStreamWaitEvent(s, ev_full, 0));
+    if (!used[qi]) {
+      if (wk.gpu()) CEK_HIP(hipStreamWaitEvent(s, ev_full, 0));
+      log_op(gidx, "wait", 1 + qi, 0, 0, full_slot);
+    }
     used[qi] = 1;
     long long off = ref + k * chunk;
     for (auto& a : c.arrays) {
@@ -554,7 +579,9 @@ void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long
       wk.h2d(s, a, b, n);
       *h2d += n * a.elem_size;
     }
+    log_op(gidx, "h2d", 1 + qi, off, chunk);
     launch_kernels(wk, s, c, off, chunk);
+    log_op(gidx, "kernel", 1 + qi, off, chunk);
     for (auto& a : c.arrays) {
       if (a.zc || !a.write || a.write_all) continue;
       uint64_t b, n;
@@ -562,14 +589,18 @@ void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long
       wk.d2h(s, a, b, n);
       *d2h += n * a.elem_size;
     }
+    log_op(gidx, "d2h", 1 + qi, off, chunk);
   }
-  if (wk.gpu()) {
-    for (int q = 0; q < 16; ++q) {
-      if (!used[q]) continue;
-      hipEvent_t e = wk.event(slot++);
+  for (int q = 0; q < 16; ++q) {
+    if (!used[q]) continue;
+    if (wk.gpu()) {
+      hipEvent_t e = wk.event(slot);
       CEK_HIP(hipEventRecord(e, wk.compute_stream(q)));
       CEK_HIP(hipStreamWaitEvent(m, e, 0));
     }
+    log_op(gidx, "rec", 1 + q, 0, 0, slot);
+    log_op(gidx, "wait", 0, 0, 0, slot);
+    ++slot;
   }
   for (size_t i = 0; i < c.arrays.size(); ++i) {
     const auto& a = c.arrays[i];

@@ -133,6 +133,27 @@ class Cores {
   // When a device fails during compute(): disable it and re-run the call on
   // the remaining devices (single-process jobs only).
   bool auto_failover = false;
+  // ---- schedule recording (pipeline dependency checks) ----
+  // Every transfer / kernel / event edge the pipelines issue is appended as
+  // (device, op, logical stream, first work item, work items, event).
+  // Logical streams: 0 main, 1+k compute queue k, 17+3h+r pipeline half h
+  // role r (0 read, 1 compute, 2 write).
+  struct SchedOp {
+    int device;
+    std::string op;  // h2d | kernel | d2h | rec | wait
+    int stream;
+    long long begin, count;
+    int event;
+  };
+  bool record_schedule = false;
+  std::vector<SchedOp> schedule() {
+    std::lock_guard<std::mutex> g(sched_mu_);
+    return sched_;
+  }
+  void clear_schedule() {
+    std::lock_guard<std::mutex> g(sched_mu_);
+    sched_.clear();
+  }
   int failovers() const { return failovers_; }
   void set_dynamic_lds(unsigned bytes);
 
@@ -190,6 +211,13 @@ class Cores {
   std::map<int, BalancerState> state_;
   std::vector<double> time_scale_;
   std::vector<bool> enabled_;
+  std::mutex sched_mu_;
+  std::vector<SchedOp> sched_;
+  void log_op(int gidx, const char* op, int stream, long long begin, long long count, int event = -1) {
+    if (!record_schedule) return;
+    std::lock_guard<std::mutex> g(sched_mu_);
+    sched_.push_back({gidx, op, stream, begin, count, event});
+  }
   std::vector<int> inject_;
   int failovers_ = 0;
   void compute_once(const ComputeCall& call, struct DeviceFailure* failed);

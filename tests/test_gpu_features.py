@@ -266,3 +266,23 @@ def test_repeat_loop_graph_replay(cr):
     finally:
         cr.repeat_count = 1
         cr.repeat_graph_threshold = 8
+
+
+@pytest.mark.parametrize("ptype", [ck.PIPELINE_EVENT, ck.PIPELINE_DRIVER])
+def test_pipeline_schedule_on_gpu(gpu, ptype):
+    """The recorded GPU schedule (real streams and events) satisfies the
+    pipeline dependency DAG."""
+    from cekirdekler_amd.utils.schedule import check_pipeline_schedule
+
+    src = "__global__ void k(const float* x, float* y) { long long i = get_global_id(0); y[i] = x[i] * 2.0f; }"
+    c = ck.ClNumberCruncher(gpu[0] + gpu[0], src)
+    c.cores.record_schedule = True
+    n = 256 * 8 * 2 * 16
+    x = ck.ClArray(np.arange(n, dtype=np.float32)); x.partial_read = True; x.write = False
+    y = ck.ClArray(np.zeros(n, np.float32)); y.read = False
+    for _ in range(2):
+        c.cores.clear_schedule()
+        x.next_param(y).compute(c, 1, "k", n, 256, 0, True, ptype, 8)
+        np.testing.assert_array_equal(y.array, 2 * x.array)
+        assert check_pipeline_schedule(c.cores.schedule()) == 16
+    c.dispose()
