@@ -42,7 +42,7 @@ KERNELS = {
 class MandelbrotRenderer:
     def __init__(self, width: int = 4096, height: int = 4096, max_iter: int = 256,
                  view=(-2.0, -1.5, 3.0, 3.0), devices=None, cruncher: ClNumberCruncher | None = None,
-                 kernel: str = "pool16"):
+                 kernel: str = "blk8"):
         self.kernel, self.ppw, self.local = KERNELS[kernel]
         if (width * height) % (256 * self.ppw) or width * height >= 2 ** 31:
             raise ValueError(f"width*height must be a multiple of {256 * self.ppw} and below 2^31")
