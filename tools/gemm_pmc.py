@@ -1,12 +1,14 @@
-"""Few GEMM dispatches for counter collection under rocprofv3."""
+"""Few GEMM dispatches for counter collection under rocprofv3 --pmc.
+usage: python tools/gemm_pmc.py [tile,...]   (default 256x256pp)"""
 import sys
 sys.path.insert(0, '.')
 import torch
 import cekirdekler_amd as ck
 from cekirdekler_amd.ops.gemm import GemmBf16
 g0 = ck.ClPlatforms.all().gpus()[0]
-for tile, gm in [("256x256", 1), ("256x256", 4), ("256x256pp", 4)]:
-    g = GemmBf16(8192, 8192, 8192, devices=g0, tile=tile, group_m=gm)
+tiles = sys.argv[1].split(",") if len(sys.argv) > 1 else ["256x256pp"]
+for tile in tiles:
+    g = GemmBf16(8192, 8192, 8192, devices=g0, tile=tile, group_m=4)
     for _ in range(3):
         g.run(resident=True)
     torch.cuda.synchronize()
