@@ -90,7 +90,9 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
 
     if tile is None:
         tile = "256x256pp" if (size // 256) ** 2 // ctx.world >= 256 else "256x128pp"
-    cr = DistributedCruncher("", ctx=ctx, prebuilt=library("sgemm_bf16", "sgemm8p_bf16"))
+    from cekirdekler_amd.ops.gemm import GEMM_LIBS
+
+    cr = DistributedCruncher("", ctx=ctx, prebuilt=library(*GEMM_LIBS))
     g = GemmBf16(size, size, size, cruncher=cr, tile=tile)
     ms = timed(ctx, lambda: g.run(compute_id=1, resident=True), steps, warmup)
     host_steps = max(2, min(steps, 5))

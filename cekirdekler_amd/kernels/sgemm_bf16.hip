@@ -25,7 +25,7 @@
 
 namespace {
 
-template <int WM, int WN, int FM, int FN, int MODE, bool SK = false>
+template <int WM, int WN, int FM, int FN, int MODE, bool SK = false, bool NOSTORE = false>
 __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
                                           const uint16_t* __restrict__ A,
                                           const uint16_t* __restrict__ Bt, float* __restrict__ C,
@@ -331,6 +331,13 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     }
   }
   float* ct = C + (size_t)t * BM * BN;
+  if constexpr (NOSTORE) {  // probe build: measures the epilogue's share
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -356,6 +363,13 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     __shared__ __attribute__((aligned(16))) char smem[2 * (WM * 16 * FM + WN * 16 * FN) * 64 * 2]; \
     gemm_tile<WM, WN, FM, FN, MODE, true>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);           \
   }
+
+// Probe-only build without the C store (tools/gemm_probe.py epilogue share).
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pp_nostore(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * 16 * 8 + 4 * 16 * 4) * 64 * 2];
+  gemm_tile<2, 4, 8, 4, 2, false, true>(dims, A, Bt, C, smem, __cek_off);
+}
 
 // Split-K ping-pong variants (dims[4] = S splits; K/64 divisible by S):
 // strongly scaled slices keep one 256-row tile per CU busy instead of

@@ -32,11 +32,18 @@ TILES = {
     "256x128ps": (256, 128, 512, "cek_sgemm_bf16_256x128ps"),
     "128x128": (128, 128, 256, "cek_sgemm_bf16_128x128"),
     "128x128p": (128, 128, 256, "cek_sgemm_bf16_128x128p"),
+    # probe only: 256x256pp without the C store (epilogue share)
+    "256x256pp_nostore": (256, 256, 512, "cek_sgemm_bf16_256x256pp_nostore"),
+    # ping-pong with a 4-deep BK=32 LDS ring (kernels/sgemm_pp32_bf16.hip)
+    "256x256q": (256, 256, 512, "cek_sgemm_bf16_256x256q"),
+    "256x128q": (256, 128, 512, "cek_sgemm_bf16_256x128q"),
     # 8-phase half-tile pipeline (kernels/sgemm8p_bf16.hip), ring of 8 / 10 slots
     "256x256e8": (256, 256, 512, "cek_sgemm8p_bf16_r8"),
     "256x256e10": (256, 256, 512, "cek_sgemm8p_bf16_r10"),
 }
 
+
+GEMM_LIBS = ("sgemm_bf16", "sgemm8p_bf16", "sgemm_pp32_bf16")
 
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
 SPLIT_K_TILES = {"256x256pp", "256x128pp"}
@@ -91,7 +98,7 @@ class GemmBf16:
         self.split_k = max(1, int(split_k))
         self.tiles = (M // BM) * (N // BN)
         self.global_range = self.tiles * self.split_k * L
-        self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library("sgemm_bf16", "sgemm8p_bf16"))
+        self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library(*GEMM_LIBS))
         self.group_m = group_m
         self.dims = ClArray(np.array([M, N, K, group_m, self.split_k, 0, 0, 0], np.int32))
         self.dims.write = False
