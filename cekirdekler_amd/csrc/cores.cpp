@@ -309,6 +309,10 @@ void Cores::share_slices(int id, const ArraySpec& a, long long local_range) {
 
 // ------------------------------------------------------------- compute --
 
+// time the calling worker spent in the phase barrier of the current compute
+static thread_local double t_phase_wait = 0;
+static thread_local bool t_phase_arrived = false;
+
 // ---------------------------------------------------------------- UserEvent --
 
 namespace {
@@ -401,6 +405,7 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
   hipStream_t s = nullptr;
   if (wk.gpu())
     s = (enqueue_mode_ && async_enqueue) ? wk.compute_stream(wk.next_compute_queue()) : wk.main_stream();
+  const bool gather = comm_ && dist_gather_writes;
   // phase 1: host → device (partial slice wins over full read)
   for (auto& a : c.arrays) {
     if (a.zc) continue;
@@ -415,7 +420,6 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
   // phase 2: kernels
   launch_kernels(wk, s, c, ref, range);
   // optional device-side all-gather of written slices (distributed keep-resident)
-  const bool gather = comm_ && dist_gather_writes;
   if (gather) {
     auto& st = state_[c.compute_id];
     for (auto& a : c.arrays) {
@@ -430,6 +434,16 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
       }
       comm_->allgatherv(wk.buffer(a), offs, sizes, s);
     }
+  }
+  // Phase separation when an array is both read whole and written back:
+  // no device may write its slice into host memory another device is still
+  // reading (reference: all reads and computes finish before any write).
+  if (phase_) {
+    if (wk.gpu()) CEK_HIP(hipStreamSynchronize(s));
+    t_phase_arrived = true;
+    const double w0 = now_ms();
+    phase_->arrive_and_wait();
+    t_phase_wait = now_ms() - w0;  // not this device's work: kept out of its time
   }
   // phase 3: device → host
   for (size_t i = 0; i < c.arrays.size(); ++i) {
@@ -615,9 +629,22 @@ void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long
 
 void Cores::run_device(int w, const ComputeCall& c, long long ref, long long range, bool pipelined,
                        double* out_ms, uint64_t* h2d, uint64_t* d2h) {
+  t_phase_arrived = false;
+  try {
+    run_device_body(w, c, ref, range, pipelined, out_ms, h2d, d2h);
+  } catch (...) {
+    // a failing device must not leave the others waiting in the phase barrier
+    if (phase_ && !t_phase_arrived && range > 0) phase_->arrive_and_drop();
+    throw;
+  }
+}
+
+void Cores::run_device_body(int w, const ComputeCall& c, long long ref, long long range, bool pipelined,
+                       double* out_ms, uint64_t* h2d, uint64_t* d2h) {
   Worker& wk = *workers_[w];
   const int gidx = global_base_ + w;
   TraceRange tr("cek.device" + std::to_string(gidx) + ".id" + std::to_string(c.compute_id));
+  t_phase_wait = 0;
   if (range > 0 && inject_[w] > 0) {
     --inject_[w];
     throw Error("injected failure on device " + std::to_string(w));
@@ -635,7 +662,7 @@ void Cores::run_device(int w, const ComputeCall& c, long long ref, long long ran
     // still take part in the collectives
     run_3phase(wk, gidx, c, ref, 0, h2d, d2h);
   }
-  *out_ms = (now_ms() - t0) * time_scale_[w];
+  *out_ms = (now_ms() - t0 - t_phase_wait) * time_scale_[w];
 }
 
 void Cores::compute(const ComputeCall& c) {
@@ -737,8 +764,14 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
     st.references[i] = acc;
     acc += st.ranges[i];
   }
+  // Host-memory hazard: an array read whole by every device and written back
+  // by slices.  With several local devices the phases must be separated.
+  bool hazard = false;
+  if (nloc > 1)
+    for (auto& a : c.arrays)
+      if (!a.zc && a.read && !a.partial && a.write) hazard = true;
   // Pipelining eligibility (Cores.cs:624-652), decided per call for all devices.
-  bool pipelined = pipe_req && c.repeats <= 1 && !enqueue_mode_;
+  bool pipelined = pipe_req && c.repeats <= 1 && !enqueue_mode_ && !hazard;
   for (int i = 0; i < D && pipelined; ++i)
     if (st.ranges[i] != 0 && (st.ranges[i] % (B * U) != 0 || st.ranges[i] < B * U)) pipelined = false;
   if (comm_ && (dist_gather_writes || dist_broadcast_reads)) pipelined = false;
@@ -746,7 +779,16 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
   std::vector<double> ms(nloc, 0.0);
   std::vector<uint64_t> h2d(nloc, 0), d2h(nloc, 0);
   DeviceFailure failure;
-  if (nloc == 1 || serial) {
+  int participants = 0;
+  for (int w = 0; w < nloc; ++w)
+    if (st.ranges[global_base_ + w] > 0 || (comm_ && (dist_gather_writes || dist_broadcast_reads))) ++participants;
+  PhaseBarrier phase(participants);
+  if (hazard && !enqueue_mode_ && participants > 1) phase_ = &phase;
+  struct ResetPhase {
+    PhaseBarrier*& p;
+    ~ResetPhase() { p = nullptr; }
+  } reset_phase{phase_};
+  if (nloc == 1 || (serial && !phase_)) {
     for (int w = 0; w < nloc; ++w) {
       int g = global_base_ + w;
       try {

@@ -20,7 +20,9 @@
 // identical next split.  Optional RCCL data plane: broadcast `read` arrays
 // from rank 0 and all-gather written slices into every replica.
 #pragma once
+#include <condition_variable>
 #include <map>
+#include <mutex>
 
 #include "balancer.h"
 #include "dist.h"
@@ -81,6 +83,40 @@ class UserEvent {
   uint32_t* word_ = nullptr;
   uint32_t gen_ = 0;
   bool armed_ = false;
+};
+
+// Host rendezvous of the local devices inside one compute() (reference
+// phase separation: every device finishes reading and computing before any
+// device writes back, Cores.cs:751-831).
+class PhaseBarrier {
+ public:
+  explicit PhaseBarrier(int n) : n_(n) {}
+  void arrive_and_wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    const int gen = gen_;
+    if (++count_ == n_) {
+      count_ = 0;
+      ++gen_;
+      cv_.notify_all();
+    } else {
+      cv_.wait(lk, [&] { return gen_ != gen || broken_; });
+    }
+  }
+  void arrive_and_drop() {  // a failing device must not block the others
+    std::lock_guard<std::mutex> lk(mu_);
+    --n_;
+    if (count_ >= n_ && count_ > 0) {
+      count_ = 0;
+      ++gen_;
+      cv_.notify_all();
+    }
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int n_, count_ = 0, gen_ = 0;
+  bool broken_ = false;
 };
 
 // A compute() in which one or more local devices raised.
@@ -195,7 +231,10 @@ class Cores {
   int global_base() const { return global_base_; }
 
  private:
+  PhaseBarrier* phase_ = nullptr;  // set while a hazardous compute runs
   void run_device(int w, const ComputeCall& c, long long ref, long long range, bool pipelined,
+                  double* out_ms, uint64_t* h2d, uint64_t* d2h);
+  void run_device_body(int w, const ComputeCall& c, long long ref, long long range, bool pipelined,
                   double* out_ms, uint64_t* h2d, uint64_t* d2h);
   void run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref, long long range,
                   uint64_t* h2d, uint64_t* d2h);

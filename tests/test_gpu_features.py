@@ -286,3 +286,22 @@ def test_pipeline_schedule_on_gpu(gpu, ptype):
         np.testing.assert_array_equal(y.array, 2 * x.array)
         assert check_pipeline_schedule(c.cores.schedule()) == 16
     c.dispose()
+
+
+def test_phase_separation_for_read_whole_write_slices(gpu):
+    """An array read whole by every device and written back by slices: no
+    device may write its slice into host memory before every device has read
+    it (reference phase separation)."""
+    src = """__global__ void swap_halves(float* a, float* n) {
+        long long i = get_global_id(0); long long h = (long long)n[0] / 2;
+        a[i] = a[(i + h) % (2 * h)] + 1.0f; }"""
+    c = ck.ClNumberCruncher(gpu[0] + gpu[0], src)
+    m = 1 << 16
+    a = ck.ClArray(np.arange(m, dtype=np.float32))
+    nn = ck.ClArray(np.array([m], np.float32)); nn.write = False
+    for it in range(6):
+        c.set_time_scale(1, 1.0 + (it % 3))       # vary the split between calls
+        before = a.array.copy()
+        a.next_param(nn).compute(c, 1, "swap_halves", m, 256)
+        np.testing.assert_array_equal(a.array, np.roll(before, -m // 2) + 1.0)
+    c.dispose()
