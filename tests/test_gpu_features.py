@@ -300,8 +300,10 @@ def test_phase_separation_for_read_whole_write_slices(gpu):
     a = ck.ClArray(np.arange(m, dtype=np.float32))
     nn = ck.ClArray(np.array([m], np.float32)); nn.write = False
     for it in range(6):
-        c.set_time_scale(1, 1.0 + (it % 3))       # vary the split between calls
         before = a.array.copy()
-        a.next_param(nn).compute(c, 1, "swap_halves", m, 256)
+        # granularity m/2: each device owns exactly one half and reads only
+        # the other device's half (no overlap inside one device's kernel)
+        a.next_param(nn).compute(c, 1, "swap_halves", m, 256, granularity=m // 2)
+        assert c.ranges(1) == [m // 2, m // 2]
         np.testing.assert_array_equal(a.array, np.roll(before, -m // 2) + 1.0)
     c.dispose()
