@@ -9,7 +9,9 @@ from cekirdekler_amd.ops.gemm import GemmBf16
 res = {}
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 g0 = ck.ClPlatforms.all().gpus()[0]
-shapes = [(n, n, n)] + ([(n // 8, n, n)] if n >= 4096 else [])
+import os
+rows = [int(x) for x in os.environ.get("GEMM_PROBE_ROWS", "").split(",") if x]
+shapes = [(r, n, n) for r in rows] if rows else [(n, n, n)] + ([(n // 8, n, n)] if n >= 4096 else [])
 from cekirdekler_amd.ops.gemm import TILES
 tiles = sys.argv[2].split(",") if len(sys.argv) > 2 else list(TILES)
 groups = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 4, 8]
