@@ -235,6 +235,100 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       bar();
     }
     if (!g1) bar();  // equal barrier counts for both groups
+  } else if constexpr (MODE == 4) {
+    // Ping-pong with balanced DMA: G0 stages the A tile of K-tile k+1 and G1
+    // the Bt tile of K-tile k+2, each during its own LDS-read section, so both
+    // groups' read sections carry the same DMA issue cost (~60-100 cycles per
+    // 1 KiB glds) and stay shorter than the partner's MFMA section.  Bt gets
+    // three LDS buffers (A 2 × BM·64·2 B, Bt 3 × BN·64·2 B = 160 KiB at 256²).
+    //   WAR: both targets were last read in the previous read sections.
+    //   RAW: G0's vmcnt(0) closes its MFMA section (A k+1 before G0 reads it);
+    //        G1 ends its read section k with B k+1 retired (only k+2 in flight).
+    const bool g1 = wave >= NWAVES / 2;
+    char* const a_base = smem;
+    char* const b_base = smem + 2 * A_BYTES;
+    auto stage_a4 = [&](int kt) {
+      char* base = a_base + (kt & 1) * A_BYTES;
+#pragma unroll
+      for (int j = 0; j < A_INSTR; ++j) {
+        const char* src = a_wave + ((size_t)j * 8 * K + (size_t)(ks + kt) * BK) * 2;
+        __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off), (lds_void*)(base + (sw * A_INSTR + j) * 1024),
+                                         16, 0, 0);
+      }
+    };
+    auto stage_b4 = [&](int kt) {
+      char* base = b_base + (kt % 3) * B_BYTES;
+#pragma unroll
+      for (int j = 0; j < B_INSTR; ++j) {
+        const char* src = b_wave + ((size_t)j * 8 * K + (size_t)(ks + kt) * BK) * 2;
+        __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off), (lds_void*)(base + (sw * B_INSTR + j) * 1024),
+                                         16, 0, 0);
+      }
+    };
+    bf16x8 fa[2][FM], fb[2][FN];
+    auto ldall = [&](int kt) {
+      const char* ab = a_base + (kt & 1) * A_BYTES;
+      const char* bb = b_base + (kt % 3) * B_BYTES - A_BYTES;  // b_off includes A_BYTES
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[s][j] = *(const bf16x8*)(bb + b_off[s] + j * 2048);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[s][i] = *(const bf16x8*)(ab + a_off[s] + i * 2048);
+      }
+    };
+    auto mmaall = [&]() {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][i], fb[s][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    auto bar = [] {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    if (!g1) {
+      stage_a4(0);
+    } else {
+      stage_b4(0);
+      if (nk > 1) stage_b4(1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (g1) bar();  // G1 runs one section behind
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool b_issued = g1 && kt + 2 < nk;
+      if (!g1) {
+        if (kt + 1 < nk) stage_a4(kt + 1);
+      } else if (b_issued) {
+        stage_b4(kt + 2);
+      }
+      ldall(kt);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (g1) {
+        if (b_issued) {
+          if constexpr (B_INSTR == 8)
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else if constexpr (B_INSTR == 4)
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+      bar();
+      mmaall();
+      if (!g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+    }
+    if (!g1) bar();  // equal barrier counts for both groups
   } else {
     // Ping-pong with split DMA (see MODE comment above).
     const bool g1 = wave >= NWAVES / 2;
@@ -376,6 +470,17 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pp_nosto
 // leaving CUs idle (8 GPUs × 1024 rows of an 8192² problem = 128 tiles).
 CEK_GEMM_SK_KERNEL(cek_sgemm_bf16_256x256pp_sk, 2, 4, 8, 4, 2)
 CEK_GEMM_SK_KERNEL(cek_sgemm_bf16_256x128pp_sk, 4, 2, 4, 4, 2)
+
+#define CEK_GEMM_B3_KERNEL(NAME, WM, WN, FM, FN)                                                    \
+  extern "C" __global__ __launch_bounds__(64 * WM * WN) void NAME(                                    \
+      const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {                  \
+    __shared__ __attribute__((aligned(16))) char smem[(2 * WM * 16 * FM + 3 * WN * 16 * FN) * 64 * 2]; \
+    gemm_tile<WM, WN, FM, FN, 4>(dims, A, Bt, C, smem, __cek_off);                                     \
+  }
+
+// Balanced-DMA ping-pong (MODE 4): 160 KiB LDS at 256², 128 KiB at 256×128.
+CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x256pb, 2, 4, 8, 4)
+CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x128pb, 4, 2, 4, 4)
 
 // 256×256 tiles, 8 waves (2×4, 128×64 each), 128 KiB LDS, 1 block/CU.
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256, 2, 4, 8, 4, 0)

@@ -32,6 +32,9 @@ TILES = {
     "256x128ps": (256, 128, 512, "cek_sgemm_bf16_256x128ps"),
     "128x128": (128, 128, 256, "cek_sgemm_bf16_128x128"),
     "128x128p": (128, 128, 256, "cek_sgemm_bf16_128x128p"),
+    # balanced-DMA ping-pong: G0 stages A, G1 stages Bt two K-tiles ahead
+    "256x256pb": (256, 256, 512, "cek_sgemm_bf16_256x256pb"),
+    "256x128pb": (256, 128, 512, "cek_sgemm_bf16_256x128pb"),
     # probe only: 256x256pp without the C store (epilogue share)
     "256x256pp_nostore": (256, 256, 512, "cek_sgemm_bf16_256x256pp_nostore"),
     # ping-pong with a 4-deep BK=32 LDS ring (kernels/sgemm_pp32_bf16.hip)
