@@ -235,7 +235,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       bar();
     }
     if (!g1) bar();  // equal barrier counts for both groups
-  } else if constexpr (MODE == 4) {
+  } else if constexpr (MODE == 4 || MODE == 5) {
     // Ping-pong with balanced DMA: G0 stages the A tile of K-tile k+1 and G1
     // the Bt tile of K-tile k+2, each during its own LDS-read section, so both
     // groups' read sections carry the same DMA issue cost (~60-100 cycles per
@@ -304,12 +304,13 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     if (g1) bar();  // G1 runs one section behind
     for (int kt = 0; kt < nk; ++kt) {
       const bool b_issued = g1 && kt + 2 < nk;
+      if constexpr (MODE == 5) ldall(kt);  // reads first: their latency hides under the DMA issue
       if (!g1) {
         if (kt + 1 < nk) stage_a4(kt + 1);
       } else if (b_issued) {
         stage_b4(kt + 2);
       }
-      ldall(kt);
+      if constexpr (MODE == 4) ldall(kt);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (g1) {
         if (b_issued) {
@@ -471,16 +472,19 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pp_nosto
 CEK_GEMM_SK_KERNEL(cek_sgemm_bf16_256x256pp_sk, 2, 4, 8, 4, 2)
 CEK_GEMM_SK_KERNEL(cek_sgemm_bf16_256x128pp_sk, 4, 2, 4, 4, 2)
 
-#define CEK_GEMM_B3_KERNEL(NAME, WM, WN, FM, FN)                                                    \
+#define CEK_GEMM_B3_KERNEL(NAME, WM, WN, FM, FN, MODE)                                              \
   extern "C" __global__ __launch_bounds__(64 * WM * WN) void NAME(                                    \
       const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {                  \
     __shared__ __attribute__((aligned(16))) char smem[(2 * WM * 16 * FM + 3 * WN * 16 * FN) * 64 * 2]; \
-    gemm_tile<WM, WN, FM, FN, 4>(dims, A, Bt, C, smem, __cek_off);                                     \
+    gemm_tile<WM, WN, FM, FN, MODE>(dims, A, Bt, C, smem, __cek_off);                                  \
   }
 
-// Balanced-DMA ping-pong (MODE 4): 160 KiB LDS at 256², 128 KiB at 256×128.
-CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x256pb, 2, 4, 8, 4)
-CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x128pb, 4, 2, 4, 4)
+// Balanced-DMA ping-pong (MODE 4; MODE 5 issues the LDS reads before the
+// DMA): 160 KiB LDS at 256², 128 KiB at 256×128.
+CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x256pb, 2, 4, 8, 4, 4)
+CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x128pb, 4, 2, 4, 4, 4)
+CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x256pc, 2, 4, 8, 4, 5)
+CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x128pc, 4, 2, 4, 4, 5)
 
 // 256×256 tiles, 8 waves (2×4, 128×64 each), 128 KiB LDS, 1 block/CU.
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256, 2, 4, 8, 4, 0)
