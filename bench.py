@@ -89,7 +89,10 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     from cekirdekler_amd.parallel.distributed import DistributedCruncher
 
     if tile is None:
-        tile = "256x256pp" if (size // 256) ** 2 // ctx.world >= 256 else "256x128pp"
+        # 256² tiles while every CU still gets one (balanced-DMA ping-pong,
+        # 1.35 PF at 8192³); 256×128 once a GPU's slice has fewer 256² tiles
+        # than CUs (8 GPUs × 1024 rows: 128 tiles)
+        tile = "256x256pb" if (size // 256) ** 2 // ctx.world >= 256 else "256x128pp"
     from cekirdekler_amd.ops.gemm import GEMM_LIBS
 
     cr = DistributedCruncher("", ctx=ctx, prebuilt=library(*GEMM_LIBS))
