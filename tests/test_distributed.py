@@ -49,22 +49,23 @@ def _worker(rank, world, port, exch, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("exch", ["shm", "torch"])
-def test_two_rank_balancing(exch):
+@pytest.mark.parametrize("exch,world", [("shm", 2), ("torch", 2), ("shm", 4)])
+def test_two_rank_balancing(exch, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, exch, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, exch, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
-    for _ in range(2):
+    for _ in range(world):
         r, splits, ok = q.get(timeout=240)
         res[r] = (splits, ok)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    assert res[0][0] == res[1][0]          # identical splits on both ranks, every call
-    assert res[0][1] and res[1][1]         # each rank computed its own slice correctly
+    for r in range(1, world):
+        assert res[r][0] == res[0][0]      # identical splits on every rank, every call
+    assert all(res[r][1] for r in range(world))  # each rank computed its own slice correctly
     last = res[0][0][-1]
     assert sum(last) == 64 * 512 and last[0] > last[1]  # faster rank 0 got more work
