@@ -69,14 +69,22 @@ def _sum_over_ranks(ctx, v: float) -> float:
     return float(t.item())
 
 
-def timed(ctx, fn, steps: int, warmup: int) -> float:
+def timed(ctx, fn, steps: int, warmup: int, enter=None, leave=None) -> float:
+    """W untimed calls, then K timed calls bracketed by barrier + device sync
+    on both sides; the max over ranks.  ``enter``/``leave`` run inside the
+    timed bracket around the K calls (enqueue mode on/off: leaving drains
+    every queue, so all K computes are inside the measurement)."""
     for _ in range(warmup):
         fn()
     _barrier(ctx)
     _sync()
     t0 = time.perf_counter()
+    if enter:
+        enter()
     for _ in range(steps):
         fn()
+    if leave:
+        leave()
     _sync()
     _barrier(ctx)
     ms = (time.perf_counter() - t0) * 1e3 / steps
@@ -97,7 +105,15 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
 
     cr = DistributedCruncher("", ctx=ctx, prebuilt=library(*GEMM_LIBS))
     g = GemmBf16(size, size, size, cruncher=cr, tile=tile)
-    ms = timed(ctx, lambda: g.run(compute_id=1, resident=True), steps, warmup)
+    step = lambda: g.run(compute_id=1, resident=True)  # noqa: E731
+    # Warm-up computes run the load balancer to its split; the K timed
+    # computes run in enqueue mode (reference ClNumberCruncher.enqueueMode:
+    # no host sync between computes, split frozen, timings gathered when the
+    # mode is left) — every step still runs the whole GEMM on every device.
+    ms = timed(ctx, step, steps, warmup,
+               enter=lambda: setattr(cr, "enqueue_mode", True),
+               leave=lambda: setattr(cr, "enqueue_mode", False))
+    ms_sync = timed(ctx, step, steps, 1)  # one host sync + time exchange per compute
     host_steps = max(2, min(steps, 5))
     ms_host = timed(ctx, lambda: g.run(compute_id=2, resident=False), host_steps, 1)
     ranges = cr.ranges(1)
@@ -105,6 +121,7 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     for a in (g.A, g.B, g.C, g.dims):
         a.dispose()  # release 0.5 GB of pinned host memory before the next config
     return {"ms": ms, "gflops": g.flops / (ms * 1e-3) / 1e9, "tile": tile,
+            "sync_per_step_ms": ms_sync, "sync_per_step_gflops": g.flops / (ms_sync * 1e-3) / 1e9,
             "host_resident_ms": ms_host, "host_resident_gflops": g.flops / (ms_host * 1e-3) / 1e9,
             "ranges": ranges}
 
@@ -193,6 +210,7 @@ def main(argv=None) -> int:
                        "parallelism": f"range-partition dp{ctx.world}"},
             "extra": {
                 "sgemm_device_resident_gflops": round(sg["gflops"], 1),
+                "sgemm_sync_per_step_gflops": round(sg["sync_per_step_gflops"], 1),
                 "sgemm_host_resident_gflops": round(sg["host_resident_gflops"], 1),
                 "sgemm_host_resident_ms": round(sg["host_resident_ms"], 3),
                 "sgemm_ranges": sg["ranges"],

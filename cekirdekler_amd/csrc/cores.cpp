@@ -133,10 +133,19 @@ void Cores::set_enqueue_mode(bool on) {
     finish();
     double el = now_ms() - enqueue_t0_;
     auto it = state_.find(last_id_);
+    std::vector<double> ms(num_devices());
+    for (int w = 0; w < num_devices(); ++w) ms[w] = el * time_scale_[w];
+    // every rank leaves enqueue mode together: exchange so all ranks keep the
+    // identical benchmark vector (and hence derive the identical next split)
+    std::vector<double> all = ex_ ? ex_->allgather(ms) : ms;
     if (it != state_.end()) {
-      for (int w = 0; w < num_devices(); ++w) {
-        size_t g = static_cast<size_t>(global_base_ + w);
-        if (g < it->second.bench.size()) it->second.bench[g] = el * time_scale_[w];
+      if (ex_ && all.size() == it->second.bench.size()) {
+        it->second.bench = all;
+      } else {
+        for (int w = 0; w < num_devices(); ++w) {
+          size_t g = static_cast<size_t>(global_base_ + w);
+          if (g < it->second.bench.size()) it->second.bench[g] = ms[w];
+        }
       }
     }
   }

@@ -40,6 +40,16 @@ def _worker(rank, world, port, exch, q):
         x.array[:] = 1.0
         x.compute(cr, 1, "k", n, 64)
         splits.append(cr.ranges(1))
+    # enqueue mode (no per-call exchange) is entered and left by every rank
+    # together; the timings gathered on leaving keep the splits identical
+    cr.enqueue_mode = True
+    for _ in range(3):
+        x.compute(cr, 1, "k", n, 64)
+    cr.enqueue_mode = False
+    for _ in range(2):
+        x.array[:] = 1.0
+        x.compute(cr, 1, "k", n, 64)
+        splits.append(cr.ranges(1))
     refs = cr.references(1)
     lo, hi = refs[rank], refs[rank] + splits[-1][rank]
     ok = bool(np.all(x.array[lo:hi] == 2.0 + np.arange(lo, hi, dtype=np.float32)))
