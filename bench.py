@@ -128,10 +128,10 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     # computes run in enqueue mode (reference ClNumberCruncher.enqueueMode:
     # no host sync between computes, split frozen, timings gathered when the
     # mode is left) — every step still runs the whole GEMM on every device.
-    ms = timed(ctx, step, steps, warmup,
+    ms_sync = timed(ctx, step, steps, warmup)  # one host sync + time exchange per compute
+    ms = timed(ctx, step, steps, 1,
                enter=lambda: setattr(cr, "enqueue_mode", True),
                leave=lambda: setattr(cr, "enqueue_mode", False))
-    ms_sync = timed(ctx, step, steps, 1)  # one host sync + time exchange per compute
     host_steps = max(2, min(steps, 5))
     ms_host = timed(ctx, lambda: g.run(compute_id=2, resident=False), host_steps, 1)
     ranges = cr.ranges(1)
