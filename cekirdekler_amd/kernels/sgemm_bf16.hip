@@ -471,6 +471,12 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pp_nosto
 // leaving CUs idle (8 GPUs × 1024 rows of an 8192² problem = 128 tiles).
 CEK_GEMM_SK_KERNEL(cek_sgemm_bf16_256x256pp_sk, 2, 4, 8, 4, 2)
 CEK_GEMM_SK_KERNEL(cek_sgemm_bf16_256x128pp_sk, 4, 2, 4, 4, 2)
+// balanced-DMA split-K (three Bt buffers: 160 KiB LDS)
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sk(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
+  gemm_tile<2, 4, 8, 4, 4, true>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
+}
 
 #define CEK_GEMM_B3_KERNEL(NAME, WM, WN, FM, FN, MODE)                                              \
   extern "C" __global__ __launch_bounds__(64 * WM * WN) void NAME(                                    \

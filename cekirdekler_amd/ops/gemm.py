@@ -51,7 +51,7 @@ TILES = {
 GEMM_LIBS = ("sgemm_bf16", "sgemm8p_bf16", "sgemm_pp32_bf16")
 
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
-SPLIT_K_TILES = {"256x256pp", "256x128pp"}
+SPLIT_K_TILES = {"256x256pp", "256x128pp", "256x256pb"}
 
 
 def to_bf16_bits(x: np.ndarray) -> np.ndarray:

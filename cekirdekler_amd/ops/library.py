@@ -17,7 +17,7 @@ LIBRARY = {
     "sgemm_bf16": ["cek_sgemm_bf16_256x256", "cek_sgemm_bf16_256x256p", "cek_sgemm_bf16_256x256pp", "cek_sgemm_bf16_256x256ps",
                    "cek_sgemm_bf16_256x128", "cek_sgemm_bf16_256x128p", "cek_sgemm_bf16_256x128pp", "cek_sgemm_bf16_256x128ps",
                    "cek_sgemm_bf16_128x128", "cek_sgemm_bf16_128x128p",
-                   "cek_sgemm_bf16_256x256pp_sk", "cek_sgemm_bf16_256x128pp_sk",
+                   "cek_sgemm_bf16_256x256pp_sk", "cek_sgemm_bf16_256x128pp_sk", "cek_sgemm_bf16_256x256pb_sk",
                    "cek_sgemm_bf16_256x256pp_nostore", "cek_sgemm_bf16_256x256pb", "cek_sgemm_bf16_256x128pb",
                    "cek_sgemm_bf16_256x256pc", "cek_sgemm_bf16_256x128pc"],
     "sgemm8p_bf16": ["cek_sgemm8p_bf16_r8", "cek_sgemm8p_bf16_r10"],

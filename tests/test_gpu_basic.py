@@ -87,7 +87,7 @@ def test_gemm_8phase_pipeline_tails(tile, shape):
         assert err < 5e-3 * np.abs(ref).max(), (shape, err)
 
 
-@pytest.mark.parametrize("tile", ["256x256pp", "256x128pp"])
+@pytest.mark.parametrize("tile", ["256x256pp", "256x128pp", "256x256pb"])
 @pytest.mark.parametrize("split", [2, 4])
 def test_gemm_split_k(tile, split):
     """Split-K: partial tiles + last-arrival reduction, counters re-armed
