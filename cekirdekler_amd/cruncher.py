@@ -10,7 +10,12 @@ across devices by the iterative load balancer per compute id.
 from __future__ import annotations
 
 import enum
+import json
+import logging
+import os
 import re
+import threading
+import time
 from typing import List, Optional, Sequence
 
 from ._native import cek, kernel_dir
@@ -28,6 +33,24 @@ class AcceleratorType(enum.IntFlag):
     CPU = 1
     GPU = 2
     ACC = 4
+
+
+# Structured observability: with CEK_RECORD_LOG=<path> every
+# compute() appends one JSON line {time, devices, compute_id, kernels, ranges,
+# device_ms, bytes, pipelined, wall_ms}; the "cekirdekler_amd" logger gets the
+# same record at DEBUG level.
+_logger = logging.getLogger("cekirdekler_amd")
+_RECORD_LOG = os.environ.get("CEK_RECORD_LOG") or None
+_record_lock = threading.Lock()
+
+
+def _log_record(cr, kernels) -> None:
+    rec = cr.last_record()
+    rec.update(time=time.time(), kernels=list(kernels), devices=cr.device_names())
+    line = json.dumps(rec)
+    _logger.debug(line)
+    with _record_lock, open(_RECORD_LOG, "a") as f:
+        f.write(line + "\n")
 
 
 class ClUserEvent:
@@ -399,6 +422,8 @@ class ClNumberCruncher:
         self._cores.compute(call)
         if self.performance_feed:
             self.performance_report(compute_id)
+        if _RECORD_LOG is not None:
+            _log_record(self, kernels=names)
 
     def compute(self, arrays, compute_id: int, kernels, global_range: int, local_range: int = 256,
                 global_offset: int = 0, pipeline: bool = False, pipeline_type: bool = PIPELINE_EVENT,

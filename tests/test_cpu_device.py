@@ -222,3 +222,20 @@ def test_injected_failure_and_auto_failover(cpu):
     assert c.ranges(2) == [64 * 16, 0]
     np.testing.assert_array_equal(x.array, 2.0)
     c.dispose()
+
+
+def test_record_log_json_lines(cpu, tmp_path, monkeypatch):
+    import json
+
+    import cekirdekler_amd.cruncher as crm
+
+    path = tmp_path / "records.jsonl"
+    monkeypatch.setattr(crm, "_RECORD_LOG", str(path))
+    c = ck.ClNumberCruncher(cpu, SRC)
+    x = ck.ClArray(np.zeros(256, np.float32))
+    for _ in range(3):
+        x.compute(c, 5, "inc", 256, 64)
+    lines = [json.loads(l) for l in path.read_text().splitlines()]
+    assert len(lines) == 3 and lines[-1]["compute_id"] == 5 and lines[-1]["kernels"] == ["inc"]
+    assert sum(lines[-1]["ranges"]) == 256 and lines[-1]["h2d_bytes"] == 1024
+    c.dispose()
