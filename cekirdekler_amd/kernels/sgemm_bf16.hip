@@ -235,6 +235,94 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       bar();
     }
     if (!g1) bar();  // equal barrier counts for both groups
+  } else if constexpr (MODE == 6) {
+    // Ping-pong with the K-tile's DMA split evenly by 1 KiB chunk: the A and
+    // Bt rows of a K-tile are NCH chunks (A first, then Bt, contiguous in a
+    // stage); G0 issues the first half for K-tile k+1 in its read section of
+    // k, G1 the second half for K-tile k+2 in its own.  Three whole stages.
+    //   WAR: a stage is refilled ≥ 2 read sections after its last read.
+    //   RAW: G0 retires its half of k+1 (vmcnt(0)) before the barrier ending
+    //        its MFMA section; G1 ends its read section k with only its half
+    //        of k+2 in flight, so k+1 is complete before G0 reads it.
+    constexpr int NCH = (A_BYTES + B_BYTES) / 1024, HALF = NCH / 2, PER_WAVE = HALF / (NWAVES / 2);
+    constexpr int A_CH = A_BYTES / 1024;
+    static_assert(PER_WAVE * (NWAVES / 2) * 2 == NCH, "even chunk split");
+    const bool g1 = wave >= NWAVES / 2;
+    const int first_chunk = (g1 ? HALF : 0) + sw * PER_WAVE;
+    auto stage6 = [&](int kt) {
+      char* base = smem + (kt % 3) * STAGE;
+#pragma unroll
+      for (int j = 0; j < PER_WAVE; ++j) {
+        const int c = first_chunk + j;  // wave-uniform
+        const char* src = c < A_CH ? (const char*)(A + (size_t)(m0 + c * 8) * K)
+                                   : (const char*)(Bt + (size_t)(n0 + (c - A_CH) * 8) * K);
+        src += (size_t)(ks + kt) * BK * 2;
+        __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off), (lds_void*)(base + c * 1024), 16, 0, 0);
+      }
+    };
+    bf16x8 fa[2][FM], fb[2][FN];
+    auto ldall = [&](int kt) {
+      const char* base = smem + (kt % 3) * STAGE;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[s][j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[s][i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
+      }
+    };
+    auto mmaall = [&]() {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][i], fb[s][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    auto bar = [] {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    if (!g1) {
+      stage6(0);
+    } else {
+      stage6(0);
+      if (nk > 1) stage6(1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (g1) bar();  // G1 runs one section behind
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool g1_issued = g1 && kt + 2 < nk;
+      if (!g1) {
+        if (kt + 1 < nk) stage6(kt + 1);
+      } else if (g1_issued) {
+        stage6(kt + 2);
+      }
+      ldall(kt);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (g1) {
+        if (g1_issued) {
+          if constexpr (PER_WAVE == 6)
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+          else if constexpr (PER_WAVE == 8)
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+      bar();
+      mmaall();
+      if (!g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+    }
+    if (!g1) bar();  // equal barrier counts for both groups
   } else if constexpr (MODE == 4 || MODE == 5) {
     // Ping-pong with balanced DMA: G0 stages the A tile of K-tile k+1 and G1
     // the Bt tile of K-tile k+2, each during its own LDS-read section, so both
@@ -491,6 +579,13 @@ CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x256pb, 2, 4, 8, 4, 4)
 CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x128pb, 4, 2, 4, 4, 4)
 CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x256pc, 2, 4, 8, 4, 5)
 CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x128pc, 4, 2, 4, 4, 5)
+
+// Even chunk-split DMA with three whole stages (MODE 6): 144 KiB at 256×128.
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x128pe(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * (256 + 128) * 64 * 2];
+  gemm_tile<4, 2, 4, 4, 6>(dims, A, Bt, C, smem, __cek_off);
+}
 
 // 256×256 tiles, 8 waves (2×4, 128×64 each), 128 KiB LDS, 1 block/CU.
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256, 2, 4, 8, 4, 0)
