@@ -114,8 +114,9 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     if tile is None:
         # 256² tiles while every CU still gets one (balanced-DMA ping-pong,
         # 1.35 PF at 8192³); 256×128 once a GPU's slice has fewer 256² tiles
-        # than CUs (8 GPUs × 1024 rows: 128 tiles)
-        tile = "256x256pb" if (size // 256) ** 2 // ctx.world >= 256 else "256x128pp"
+        # than CUs (8 GPUs × 1024 rows: 128 tiles) — even chunk-split DMA
+        # ping-pong with three stages, 0.95 PF at 1024×8192×8192
+        tile = "256x256pb" if (size // 256) ** 2 // ctx.world >= 256 else "256x128pe"
     from cekirdekler_amd.ops.gemm import GEMM_LIBS
 
     cr = DistributedCruncher("", ctx=ctx, prebuilt=library(*GEMM_LIBS))
