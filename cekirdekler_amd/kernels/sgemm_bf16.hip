@@ -323,7 +323,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       bar();
     }
     if (!g1) bar();  // equal barrier counts for both groups
-  } else if constexpr (MODE == 4 || MODE == 5 || MODE == 7) {
+  } else if constexpr (MODE == 4 || MODE == 5) {
     // Ping-pong with balanced DMA: G0 stages the A tile of K-tile k+1 and G1
     // the Bt tile of K-tile k+2, each during its own LDS-read section, so both
     // groups' read sections carry the same DMA issue cost (~60-100 cycles per
@@ -392,17 +392,13 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     if (g1) bar();  // G1 runs one section behind
     for (int kt = 0; kt < nk; ++kt) {
       const bool b_issued = g1 && kt + 2 < nk;
-      // MODE 7: G0 retires A(kt) here, at the start of its read section
-      // (overlapped with G1's MFMAs), instead of at the end of its MFMA section
-      if constexpr (MODE == 7)
-        if (!g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if constexpr (MODE == 5) ldall(kt);  // reads first: their latency hides under the DMA issue
       if (!g1) {
         if (kt + 1 < nk) stage_a4(kt + 1);
       } else if (b_issued) {
         stage_b4(kt + 2);
       }
-      if constexpr (MODE == 4 || MODE == 7) ldall(kt);
+      if constexpr (MODE == 4) ldall(kt);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (g1) {
         if (b_issued) {
@@ -418,8 +414,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       }
       bar();
       mmaall();
-      if constexpr (MODE != 7)
-        if (!g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       bar();
     }
     if (!g1) bar();  // equal barrier counts for both groups
@@ -584,7 +579,6 @@ CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x256pb, 2, 4, 8, 4, 4)
 CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x128pb, 4, 2, 4, 4, 4)
 CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x256pc, 2, 4, 8, 4, 5)
 CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x128pc, 4, 2, 4, 4, 5)
-CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x256pd, 2, 4, 8, 4, 7)
 
 // Even chunk-split DMA with three whole stages (MODE 6): 144 KiB at 256×128.
 extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x128pe(

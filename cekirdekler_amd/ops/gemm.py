@@ -38,7 +38,6 @@ TILES = {
     "256x256pc": (256, 256, 512, "cek_sgemm_bf16_256x256pc"),  # same, LDS reads before the DMA
     "256x128pc": (256, 128, 512, "cek_sgemm_bf16_256x128pc"),
     "256x128pe": (256, 128, 512, "cek_sgemm_bf16_256x128pe"),  # even chunk-split DMA, 3 stages
-    "256x256pd": (256, 256, 512, "cek_sgemm_bf16_256x256pd"),  # pb, A retired at G0's read section
     # probe only: 256x256pp without the C store (epilogue share)
     "256x256pp_nostore": (256, 256, 512, "cek_sgemm_bf16_256x256pp_nostore"),
     # ping-pong with a 4-deep BK=32 LDS ring (kernels/sgemm_pp32_bf16.hip)

@@ -20,7 +20,7 @@ LIBRARY = {
                    "cek_sgemm_bf16_256x256pp_sk", "cek_sgemm_bf16_256x128pp_sk", "cek_sgemm_bf16_256x256pb_sk",
                    "cek_sgemm_bf16_256x256pp_nostore", "cek_sgemm_bf16_256x256pb", "cek_sgemm_bf16_256x128pb",
                    "cek_sgemm_bf16_256x256pc", "cek_sgemm_bf16_256x128pc",
-                   "cek_sgemm_bf16_256x128pe", "cek_sgemm_bf16_256x256pd"],
+                   "cek_sgemm_bf16_256x128pe"],
     "sgemm8p_bf16": ["cek_sgemm8p_bf16_r8", "cek_sgemm8p_bf16_r10"],
     "sgemm_pp32_bf16": ["cek_sgemm_bf16_256x256q", "cek_sgemm_bf16_256x128q"],
     "mandelbrot": ["cek_mandelbrot_f32", "cek_mandelbrot_pool16_f32", "cek_mandelbrot_pool8_f32",
