@@ -10,14 +10,15 @@ from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer  # noqa: E402
 from cekirdekler_amd.models.nbody import NBodySimulation  # noqa: E402
 
 g0 = ck.ClPlatforms.all().gpus()[0]
-for kern in ("pool16", "blk16"):
+import os
+for kern in os.environ.get("MANDEL_KERNELS", "pool16,blk16").split(","):
     m = MandelbrotRenderer(4096, 4096, 256, devices=g0, kernel=kern)
     m.out.write = False
     for _ in range(3):
         m.render(1, pipeline=False)
     torch.cuda.synchronize()
     m.cr.dispose()
-for b in (2, 4):
+for b in ((2, 4) if os.environ.get("NBODY", "1") == "1" else ()):
     sim = NBodySimulation(262144, devices=g0, bodies_per_item=b)
     for _ in range(2):
         sim.forces()
