@@ -127,6 +127,7 @@ void Cores::set_distributed(std::shared_ptr<Exchanger> ex, std::shared_ptr<Comm>
 }
 
 void Cores::set_enqueue_mode(bool on) {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   if (on && !enqueue_mode_) {
     enqueue_t0_ = now_ms();
   } else if (!on && enqueue_mode_) {
@@ -153,22 +154,27 @@ void Cores::set_enqueue_mode(bool on) {
 }
 
 std::vector<long long> Cores::ranges(int id) const {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   auto it = state_.find(id);
   return it == state_.end() ? std::vector<long long>{} : it->second.ranges;
 }
 std::vector<long long> Cores::references(int id) const {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   auto it = state_.find(id);
   return it == state_.end() ? std::vector<long long>{} : it->second.references;
 }
 std::vector<double> Cores::benchmarks(int id) const {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   auto it = state_.find(id);
   return it == state_.end() ? std::vector<double>{} : it->second.bench;
 }
 std::vector<std::vector<double>> Cores::history(int id) const {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   auto it = state_.find(id);
   return it == state_.end() ? std::vector<std::vector<double>>{} : it->second.history;
 }
 std::vector<int> Cores::compute_ids() const {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   std::vector<int> out;
   for (auto& kv : state_) out.push_back(kv.first);
   return out;
@@ -176,6 +182,7 @@ std::vector<int> Cores::compute_ids() const {
 
 void Cores::set_state(int id, const std::vector<long long>& ranges,
                       const std::vector<std::vector<double>>& history, const std::vector<double>& bench) {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   auto& st = state_[id];
   st.ranges = ranges;
   st.history = history;
@@ -202,6 +209,7 @@ long long Cores::markers_issued() {
 }
 
 void Cores::finish() {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   for (auto& w : workers_) {
     w->wait();
     w->sync_all();
@@ -675,6 +683,7 @@ void Cores::run_device_body(int w, const ComputeCall& c, long long ref, long lon
 }
 
 void Cores::compute(const ComputeCall& c) {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   DeviceFailure f;
   compute_once(c, (auto_failover && !ex_) ? &f : nullptr);
   if (f.devices.empty()) return;

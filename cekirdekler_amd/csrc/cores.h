@@ -250,6 +250,9 @@ class Cores {
   std::map<int, BalancerState> state_;
   std::vector<double> time_scale_;
   std::vector<bool> enabled_;
+  // one compute()/state access at a time per Cores (Python releases the GIL
+  // during compute, so two threads may call into the same cruncher)
+  mutable std::recursive_mutex call_mu_;
   std::mutex sched_mu_;
   std::vector<SchedOp> sched_;
   void log_op(int gidx, const char* op, int stream, long long begin, long long count, int event = -1) {
