@@ -307,3 +307,17 @@ def test_phase_separation_for_read_whole_write_slices(gpu):
         assert c.ranges(1) == [m // 2, m // 2]
         np.testing.assert_array_equal(a.array, np.roll(before, -m // 2) + 1.0)
     c.dispose()
+
+
+def test_device_printf(gpu, capfd):
+    """Reference README example: printf from every work item."""
+    src = '__kernel void hello(__global char* arr) { printf("hello world %d\\n", (int)get_global_id(0)); }'
+    c = ck.ClNumberCruncher(gpu[0], src)
+    assert c.error_code() == 0, c.error_message()
+    arr = ck.ClArray(np.zeros(1000, np.uint8))
+    arr.read = arr.write = False
+    arr.compute(c, 1, "hello", 1000, 100)
+    c.sync()
+    c.dispose()
+    out = capfd.readouterr().out
+    assert out.count("hello world") == 1000
