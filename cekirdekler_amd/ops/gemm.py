@@ -90,7 +90,7 @@ def untile(c: np.ndarray, M: int, N: int, BM: int, BN: int, group_m: int = 1) ->
 class GemmBf16:
     def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256",
                  cruncher: ClNumberCruncher | None = None, fill: str = "random", seed: int = 0,
-                 group_m: int = 4, split_k: int = 1):
+                 group_m: int = 4, split_k: int = 1, wave_granularity: bool | None = None):
         BM, BN, L, kname = TILES[tile]
         if M % BM or N % BN or K % 64:
             raise ValueError(f"M%{BM}, N%{BN} and K%64 must be 0 (got {M},{N},{K})")
@@ -129,6 +129,32 @@ class GemmBf16:
             self.A.array[:] = to_bf16_bits(rng.uniform(-1, 1, M * K).astype(np.float32))
             self.B.array[:] = to_bf16_bits(rng.uniform(-1, 1, N * K).astype(np.float32))
         self._uploaded = False
+        self.wave_granularity = wave_granularity
+
+    def granularity(self) -> int:
+        """Balancer unit in work items.  One tile (all its K-splits) by
+        default.  On identical GPUs whose slices are whole waves of tiles
+        (``work-groups % CUs == 0`` and at least one wave per device), the unit
+        is one wave: one work-group per CU.  With 256 CUs and exactly one
+        wave of tiles per device (8192² at 4 or 8 GPUs), a one-tile step would
+        let timing noise hand a device 257 tiles, which costs it a second
+        round of tiles and doubles its time.  A split in whole waves cannot do
+        that.  ``wave_granularity`` forces the choice (None = auto)."""
+        tile_unit = self.L * self.split_k
+        devs = [d for d in self.cr.devices]
+        if self.wave_granularity is False or not devs:
+            return tile_unit
+        cus = {d.compute_units for d in devs}
+        gpus = all(d.is_gpu for d in devs)
+        if self.wave_granularity is None and not (gpus and len(cus) == 1):
+            return tile_unit
+        cu = min(cus)
+        groups = self.tiles * self.split_k
+        ndev = self.cr.number_of_devices or len(devs)
+        if cu <= 0 or groups % cu or groups // cu < ndev:
+            return tile_unit
+        # a wave of tiles must keep a tile's K-splits together
+        return cu * self.L if cu % self.split_k == 0 else tile_unit
 
     @property
     def flops(self) -> float:
@@ -143,7 +169,7 @@ class GemmBf16:
         self.C.write = not resident
         self.dims.next_param(self.A, self.B, self.C, *self.extra).compute(
             self.cr, compute_id, self.kernel, self.global_range, self.L,
-            granularity=self.L * self.split_k)
+            granularity=self.granularity())
         self._uploaded = True
 
     def result(self, download: bool = True) -> np.ndarray:

@@ -123,7 +123,27 @@ def test_gemm_two_logical_devices_balanced():
     assert np.abs(c - ref).max() < 5e-3 * np.abs(ref).max()
 
 
-@pytest.mark.parametrize("kernel", ["quad", "pool8", "pool16", "pk16", "pk32", "blk16", "blk64", "blk8"])
+def test_gemm_wave_granularity_two_logical_devices():
+    """Whole waves of tiles per device (one work-group per CU): 512 tiles of
+    256² over two logical devices of one 256-CU GPU split 256/256 and stay
+    in whole waves under re-balancing; every slice is correct."""
+    from cekirdekler_amd.ops.gemm import GemmBf16
+
+    g0 = _gpu()[0]
+    cu = g0.device(0).compute_units
+    g = GemmBf16(2048, (2 * cu // 8) * 256, 128, devices=g0 + g0, tile="256x256pb")
+    unit = g.granularity()
+    assert unit == cu * g.L
+    for _ in range(4):
+        g.run(resident=False)
+        assert all(r % unit == 0 for r in g.cr.ranges(1)) and sum(g.cr.ranges(1)) == g.global_range
+    c = g.result(download=False)
+    ref = g.reference()
+    assert np.abs(c - ref).max() < 5e-3 * np.abs(ref).max()
+    assert GemmBf16(256, 256, 64, devices=g0, tile="256x256pb").granularity() == 512  # < 1 wave: per tile
+
+
+@pytest.mark.parametrize("kernel", ["quad","pool8", "pool16", "pk16", "pk32", "blk16", "blk64", "blk8"])
 def test_mandelbrot_event_pipeline_matches_numpy(kernel):
     from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
 
