@@ -393,6 +393,19 @@ class ClNumberCruncher:
                        local_range: int = 256, global_offset: int = 0, pipeline: bool = False,
                        pipeline_type: bool = PIPELINE_EVENT, pipeline_blobs: int = 4, specs=None,
                        granularity: int = 0) -> None:
+        call = self._build_call(group, compute_id, kernels, global_range, local_range, global_offset,
+                                pipeline, pipeline_type, pipeline_blobs, specs, granularity)
+        self._cores.compute(call)
+        if self.performance_feed:
+            self.performance_report(compute_id)
+        if _RECORD_LOG is not None:
+            _log_record(self, kernels=list(call.kernels))
+
+    def _build_call(self, group: ClParameterGroup, compute_id: int, kernels, global_range: int,
+                    local_range: int = 256, global_offset: int = 0, pipeline: bool = False,
+                    pipeline_type: bool = PIPELINE_EVENT, pipeline_blobs: int = 4, specs=None,
+                    granularity: int = 0):
+        """Validate a compute and freeze it into a native ComputeCall."""
         names = split_kernel_names(kernels)
         G, L = int(global_range), int(local_range)
         try:
@@ -419,11 +432,7 @@ class ClNumberCruncher:
                 raise ClComputeError(f"granularity({granularity}) must be a multiple of the local range({L}) "
                                      f"and divide the global range({G})")
             call.granularity = int(granularity)
-        self._cores.compute(call)
-        if self.performance_feed:
-            self.performance_report(compute_id)
-        if _RECORD_LOG is not None:
-            _log_record(self, kernels=names)
+        return call
 
     def compute(self, arrays, compute_id: int, kernels, global_range: int, local_range: int = 256,
                 global_offset: int = 0, pipeline: bool = False, pipeline_type: bool = PIPELINE_EVENT,

@@ -10,6 +10,7 @@
 #include "dist.h"
 #include "jit.h"
 #include "memory.h"
+#include "pool.h"
 
 namespace py = pybind11;
 using namespace cek;
@@ -292,4 +293,29 @@ PYBIND11_MODULE(_cek, m) {
       .def("copy_between", &Cores::copy_between, py::call_guard<py::gil_scoped_release>())
       .def("share_slices", &Cores::share_slices, py::call_guard<py::gil_scoped_release>())
       .def("set_distributed", &Cores::set_distributed);
+
+  py::class_<PoolTask>(m, "PoolTask")
+      .def(py::init<>())
+      .def_readwrite("call", &PoolTask::call)
+      .def_readwrite("type", &PoolTask::type)
+      .def_readwrite("id", &PoolTask::id);
+
+  py::class_<PoolCompletion>(m, "PoolCompletion")
+      .def_readonly("id", &PoolCompletion::id)
+      .def_readonly("device", &PoolCompletion::device)
+      .def_readonly("ms", &PoolCompletion::ms)
+      .def_readonly("error", &PoolCompletion::error);
+
+  py::class_<DevicePool, std::shared_ptr<DevicePool>>(m, "DevicePool")
+      .def(py::init<std::vector<std::shared_ptr<Cores>>, int>(), py::call_guard<py::gil_scoped_release>())
+      .def("enqueue", &DevicePool::enqueue, py::call_guard<py::gil_scoped_release>())
+      .def("finish", &DevicePool::finish, py::call_guard<py::gil_scoped_release>())
+      .def("completions", &DevicePool::completions, py::arg("timeout_ms") = 0.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("outstanding", &DevicePool::outstanding)
+      .def("device_task_counts", &DevicePool::device_task_counts)
+      .def("device_busy_ms", &DevicePool::device_busy_ms)
+      .def_property_readonly("num_devices", &DevicePool::num_devices)
+      .def_property_readonly("max_in_flight", &DevicePool::max_in_flight)
+      .def("close", &DevicePool::close, py::call_guard<py::gil_scoped_release>());
 }

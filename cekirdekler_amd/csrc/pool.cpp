@@ -1,0 +1,216 @@
+// Native device pool (see pool.h).  Reference: ClDevicePool producer /
+// DevicePoolThread consumer loops, ClPipeline.cs:4132-4312 and :4841-5047.
+#include "pool.h"
+
+#include <chrono>
+
+namespace cek {
+
+DevicePool::DevicePool(std::vector<std::shared_ptr<Cores>> devices, int max_in_flight)
+    : devs_(std::move(devices)), max_in_flight_(std::max(1, std::min(16, max_in_flight))) {
+  if (devs_.empty()) throw Error("device pool needs at least one device");
+  for (auto& d : devs_) {
+    if (!d) throw Error("device pool: null cruncher");
+    if (d->num_devices() != 1) throw Error("device pool: every entry must be a single-device cruncher");
+  }
+  counts_.assign(devs_.size(), 0);
+  busy_ms_.assign(devs_.size(), 0.0);
+  for (int i = 0; i < num_devices(); ++i) threads_.emplace_back([this, i] { consumer(i); });
+}
+
+DevicePool::~DevicePool() {
+  try {
+    close();
+  } catch (...) {
+  }
+}
+
+void DevicePool::close() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (closed_ && threads_.empty()) return;
+    closed_ = true;
+  }
+  work_cv_.notify_all();
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  threads_.clear();
+}
+
+void DevicePool::enqueue(const std::vector<PoolTask>& tasks) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (closed_) throw Error("device pool is closed");
+    bool sync_next = false;
+    for (const auto& t : tasks) {
+      Item it;
+      it.task = t;
+      // GLOBAL_SYNC_LAST of the previous task = a barrier before this one
+      if (sync_next) it.task.type |= kTaskSyncFirst;
+      sync_next = (t.type & kTaskSyncLast) != 0;
+      if (t.type & kTaskBroadcast) {
+        for (int d = 0; d < num_devices(); ++d) {
+          Item c = it;
+          c.target = d;
+          queue_.push_back(std::move(c));
+          ++outstanding_;
+        }
+      } else {
+        queue_.push_back(std::move(it));
+        ++outstanding_;
+      }
+    }
+  }
+  work_cv_.notify_all();
+}
+
+bool DevicePool::take_locked(int dev, Item& out) {
+  for (size_t j = 0; j < queue_.size(); ++j) {
+    Item& u = queue_[j];
+    if (u.target >= 0 && u.target != dev) continue;  // another device's broadcast copy
+    if (u.target < 0 && owner_ >= 0 && owner_ != dev) return false;  // group pinned elsewhere
+    if (u.task.type & kTaskSyncFirst) {
+      // a barrier: every earlier task has retired and nothing precedes it
+      if (j != 0 || running_ > 0) return false;
+    }
+    out = std::move(u);
+    queue_.erase(queue_.begin() + static_cast<long>(j));
+    const uint32_t ty = out.task.type;
+    if (ty & (kTaskSelectBegin | kTaskSerialBegin)) owner_ = dev;
+    out.serial = (ty & (kTaskSerialBegin | kTaskSerialEnd)) != 0 || (owner_ == dev && serial_owner_);
+    if (ty & kTaskSerialBegin) serial_owner_ = true;
+    if (ty & (kTaskSelectEnd | kTaskSerialEnd)) {
+      if (owner_ == dev) owner_ = -1;
+      serial_owner_ = false;
+    }
+    ++running_;
+    return true;
+  }
+  return false;
+}
+
+void DevicePool::complete(int dev, long long id, double ms, const std::string& err) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    done_.push_back({id, dev, ms, err});
+    ++counts_[dev];
+    busy_ms_[dev] += ms;
+    --outstanding_;
+    --running_;
+  }
+  comp_cv_.notify_all();
+  done_cv_.notify_all();
+  work_cv_.notify_all();
+}
+
+int DevicePool::retire(int dev, std::vector<Inflight>& inflight) {
+  Cores& cr = *devs_[dev];
+  int n = 0;
+  for (size_t i = 0; i < inflight.size();) {
+    if (cr.marker_word(0, inflight[i].slot) >= inflight[i].value) {
+      complete(dev, inflight[i].id, now_ms() - inflight[i].t0, "");
+      inflight[i] = inflight.back();
+      inflight.pop_back();
+      ++n;
+    } else {
+      ++i;
+    }
+  }
+  return n;
+}
+
+void DevicePool::consumer(int dev) {
+  Cores& cr = *devs_[dev];
+  const bool async = max_in_flight_ > 1;
+  if (async) cr.fine_grained = true;  // a marker word after every compute
+  std::vector<Inflight> inflight;
+  for (;;) {
+    if (!inflight.empty()) retire(dev, inflight);
+    Item it;
+    bool got = false, idle = false, stop = false;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      if (static_cast<int>(inflight.size()) < max_in_flight_) got = take_locked(dev, it);
+      if (!got && inflight.empty()) {
+        if (closed_ && queue_.empty())
+          stop = true;
+        else
+          idle = true;
+      }
+    }
+    if (stop) break;
+    if (idle) {
+      // nothing in flight here: leave enqueue mode (syncs this device's
+      // streams) and sleep until new work, a retirement elsewhere (a barrier
+      // or a pinned group may be waiting on it) or close()
+      try {
+        if (cr.enqueue_mode()) cr.set_enqueue_mode(false);
+      } catch (...) {
+      }
+      std::unique_lock<std::mutex> lk(mu_);
+      work_cv_.wait_for(lk, std::chrono::milliseconds(5));
+      continue;
+    }
+    if (!got) {  // only in-flight tasks: poll their marker words
+      std::this_thread::sleep_for(std::chrono::microseconds(10));
+      continue;
+    }
+    const double t0 = now_ms();
+    const PoolTask& t = it.task;
+    if (t.call.kernels.empty()) {  // a pure barrier / message task
+      complete(dev, t.id, 0.0, "");
+      continue;
+    }
+    try {
+      cr.no_compute = (t.type & kTaskNoCompute) != 0;
+      if (async) {
+        if (!cr.enqueue_mode()) cr.set_enqueue_mode(true);
+        cr.async_enqueue = !it.serial;  // serial groups stay on one in-order stream
+        cr.compute(t.call);
+        auto m = cr.last_marker(0);
+        inflight.push_back({t.id, m.first, m.second, t0});
+      } else {
+        cr.compute(t.call);
+        complete(dev, t.id, now_ms() - t0, "");
+      }
+    } catch (const std::exception& e) {
+      complete(dev, t.id, now_ms() - t0, e.what());
+    }
+  }
+  try {
+    if (cr.enqueue_mode()) cr.set_enqueue_mode(false);
+  } catch (...) {
+  }
+}
+
+void DevicePool::finish() {
+  std::unique_lock<std::mutex> lk(mu_);
+  done_cv_.wait(lk, [&] { return outstanding_ == 0; });
+}
+
+std::vector<PoolCompletion> DevicePool::completions(double timeout_ms) {
+  std::unique_lock<std::mutex> lk(mu_);
+  if (done_.empty() && timeout_ms > 0)
+    comp_cv_.wait_for(lk, std::chrono::microseconds(static_cast<long long>(timeout_ms * 1e3)),
+                      [&] { return !done_.empty(); });
+  std::vector<PoolCompletion> out(std::make_move_iterator(done_.begin()), std::make_move_iterator(done_.end()));
+  done_.clear();
+  return out;
+}
+
+long long DevicePool::outstanding() {
+  std::lock_guard<std::mutex> g(mu_);
+  return outstanding_;
+}
+
+std::vector<long long> DevicePool::device_task_counts() {
+  std::lock_guard<std::mutex> g(mu_);
+  return counts_;
+}
+
+std::vector<double> DevicePool::device_busy_ms() {
+  std::lock_guard<std::mutex> g(mu_);
+  return busy_ms_;
+}
+
+}  // namespace cek

@@ -1,0 +1,115 @@
+// Native task pool × device pool: the MI355X-native counterpart of the
+// reference's ClDevicePool / DevicePoolThread (ClPipeline.cs:3891-5077).
+//
+// The reference runs one producer thread plus one C# consumer thread per
+// device; consumers pop frozen compute() calls (ClTask, :3331-3520) from a
+// shared FIFO and run them on the device's own cruncher ("compute at will",
+// :4841-5047).  Here every consumer is a C++ thread that owns one
+// single-device `Cores`; it takes the next task under one mutex, issues it in
+// enqueue mode on the device's round-robin HIP streams, and retires it when
+// the device writes the task's marker word (hipStreamWriteValue64 into pinned
+// memory) — no host callback, no GIL, no Python per task.  Up to
+// `max_in_flight` tasks per device are outstanding at once.
+//
+// Task type flags (ClTaskType, ClPipeline.cs:3247-3321):
+//   SELECT_BEGIN/END, SERIAL_BEGIN/END  pin the group to the device that took
+//                                       its first task (serial groups also run
+//                                       in issue order on one stream)
+//   SYNC_FIRST                          barrier: taken only when no task is
+//                                       running anywhere
+//   SYNC_LAST                           barrier after the task (becomes
+//                                       SYNC_FIRST of the next one)
+//   BROADCAST                           duplicated onto every device
+//   NO_COMPUTE                          transfers only
+// Completions (task id, device, ms, error) are queued for the caller, which
+// runs user callbacks off the device threads.
+#pragma once
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <thread>
+
+#include "cores.h"
+
+namespace cek {
+
+enum PoolTaskFlags : uint32_t {
+  kTaskSelectBegin = 1,
+  kTaskSelectEnd = 2,
+  kTaskSyncFirst = 4,
+  kTaskSyncLast = 8,
+  kTaskBroadcast = 16,
+  kTaskNoCompute = 32,
+  kTaskSerialBegin = 64,
+  kTaskSerialEnd = 128,
+};
+
+struct PoolTask {
+  ComputeCall call;
+  uint32_t type = 0;
+  long long id = 0;  // caller's handle, reported back on completion
+};
+
+struct PoolCompletion {
+  long long id = 0;
+  int device = -1;
+  double ms = 0;  // issue → retirement (host clock)
+  std::string error;
+};
+
+class DevicePool {
+ public:
+  // One consumer thread per entry of `devices` (the same physical device may
+  // appear several times, ClPipeline.cs:4337, as separate Cores).
+  DevicePool(std::vector<std::shared_ptr<Cores>> devices, int max_in_flight);
+  ~DevicePool();
+
+  // Appends one task pool (FIFO order kept); broadcast tasks are duplicated
+  // per device, SYNC_LAST turns into SYNC_FIRST of the next task.
+  void enqueue(const std::vector<PoolTask>& tasks);
+  // Blocks until every enqueued task has retired.
+  void finish();
+  // Completions since the last call; waits up to timeout_ms for one (0: poll).
+  std::vector<PoolCompletion> completions(double timeout_ms);
+  long long outstanding();
+  std::vector<long long> device_task_counts();
+  std::vector<double> device_busy_ms();
+  int num_devices() const { return static_cast<int>(devs_.size()); }
+  int max_in_flight() const { return max_in_flight_; }
+  void close();  // drain, stop and join the consumer threads
+
+ private:
+  struct Item {
+    PoolTask task;
+    int target = -1;  // broadcast copy: only this device may take it
+    bool serial = false;
+  };
+  struct Inflight {
+    long long id;
+    int slot;
+    uint64_t value;
+    double t0;
+  };
+  bool take_locked(int dev, Item& out);
+  void consumer(int dev);
+  void complete(int dev, long long id, double ms, const std::string& err);
+  int retire(int dev, std::vector<Inflight>& inflight);
+
+  std::vector<std::shared_ptr<Cores>> devs_;
+  int max_in_flight_;
+  std::mutex mu_;
+  std::condition_variable work_cv_, done_cv_, comp_cv_;
+  std::deque<Item> queue_;
+  std::deque<PoolCompletion> done_;
+  long long outstanding_ = 0;
+  int running_ = 0;  // taken and not yet retired
+  int owner_ = -1;   // device holding a select/serial group
+  bool serial_owner_ = false;  // that group is a serial-mode group
+  bool closed_ = false;
+  std::vector<long long> counts_;
+  std::vector<double> busy_ms_;
+  std::vector<std::thread> threads_;
+};
+
+}  // namespace cek

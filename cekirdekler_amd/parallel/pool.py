@@ -4,13 +4,15 @@
 A :class:`ClTask` freezes one ``compute()`` call — the arrays, their flags at
 freeze time and the launch parameters (ClArray.cs:1552-1583).  Tasks are fed
 to a :class:`ClTaskPool` (FIFO); pools are enqueued into a
-:class:`ClDevicePool`, which runs one consumer thread per device: an idle
-device takes the next task immediately ("compute at will", the reference's
-greedy default).  Each device keeps up to ``max_queues_per_device`` tasks in
-flight on its own HIP streams (enqueue mode + round-robin queues) and tracks
-completion with stream-written marker words (``hipStreamWriteValue64``), the
-µs-cheap counterpart of the reference's 150–300 µs marker callbacks
-(Cores.cs:447).
+:class:`ClDevicePool`, whose scheduler is native (``cek.DevicePool``,
+``csrc/pool.cpp``): one C++ consumer thread per device takes the next task
+the moment its device has room ("compute at will", the reference's greedy
+default), with no Python and no GIL per task.  Each device keeps up to
+``max_queues_per_device`` tasks in flight on its own HIP streams (enqueue
+mode + round-robin queues) and retires them through stream-written marker
+words (``hipStreamWriteValue64``), the µs-cheap counterpart of the
+reference's 150–300 µs marker callbacks (Cores.cs:447).  User callbacks run
+on a dispatcher thread as completions arrive.
 
 Task type flags (ClTaskType, :3247-3321): DEVICE_SELECT_BEGIN/END and
 SERIAL_MODE_BEGIN/END pin a group of tasks to one device (in order),
@@ -22,12 +24,11 @@ from __future__ import annotations
 import collections
 import enum
 import threading
-import time
 from typing import Callable, Deque, List, Optional
 
 from .._native import cek
 from ..arrays import ClParameterGroup
-from ..cruncher import PIPELINE_EVENT, ClNumberCruncher
+from ..cruncher import PIPELINE_EVENT, ClComputeError, ClNumberCruncher
 from ..hardware import ClDevices
 
 
@@ -132,6 +133,8 @@ class ClTaskPool:
     def feed(self, task) -> None:
         if isinstance(task, ClTaskGroup):
             ts = [t.duplicate() for t in task.tasks]
+            for d, o in zip(ts, task.tasks):
+                d._origin = o
             if ts:
                 ts[0].type |= ClTaskType.TASK_MESSAGE_DEVICE_SELECT_BEGIN
                 ts[-1].type |= ClTaskType.TASK_MESSAGE_DEVICE_SELECT_END
@@ -139,7 +142,9 @@ class ClTaskPool:
                 self.tasks.append(t)
             self.total += len(ts)
             return
-        self.tasks.append(task.duplicate())
+        d = task.duplicate()
+        d._origin = task  # the caller's object learns where (and how long) it ran
+        self.tasks.append(d)
         self.total += 1
 
     def reset(self) -> None:
@@ -157,87 +162,11 @@ class ClTaskPool:
     nextTask = next_task
 
 
-class _DeviceWorker(threading.Thread):
-    """Consumer thread of one device.  Keeps up to ``max_queues`` tasks in
-    flight; each issued task carries a marker ticket (stream slot, value)
-    written by the device when the task's commands complete, so completion
-    is detected per task, in any order, without host callbacks."""
-
-    def __init__(self, pool: "ClDevicePool", index: int, cruncher: ClNumberCruncher):
-        super().__init__(daemon=True)
-        self.pool, self.index, self.cruncher = pool, index, cruncher
-        self.inflight: List[tuple] = []  # (task, slot, value)
-        self.completed = 0
-        self.busy_ms = 0.0
-
-    def _retire(self) -> int:
-        cores = self.cruncher.cores
-        keep, done = [], 0
-        for t, slot, val in self.inflight:
-            if cores.marker_word(0, slot) >= val:
-                self.completed += 1
-                done += 1
-                self.pool._task_done(self, t)
-            else:
-                keep.append((t, slot, val))
-        self.inflight = keep
-        return done
-
-    def _wait_one(self) -> None:
-        while self.inflight and self._retire() == 0:
-            time.sleep(0.00002)
-
-    def _drain(self) -> None:
-        cr = self.cruncher
-        if cr.enqueue_mode:
-            cr.enqueue_mode = False  # synchronises every stream of the device
-        self._retire()
-        for t, _, _ in self.inflight:  # (defensive) all commands are complete now
-            self.completed += 1
-            self.pool._task_done(self, t)
-        self.inflight = []
-
-    def run(self) -> None:
-        cr = self.cruncher
-        asynchronous = self.pool.max_queues > 1
-        if asynchronous:
-            cr.fine_grained_queue_control = True
-        while True:
-            t = self.pool._take(self)
-            if t is None:
-                if self.inflight:
-                    if asynchronous:
-                        self._wait_one()
-                    continue
-                if cr.enqueue_mode:
-                    cr.enqueue_mode = False
-                if self.pool._closed:
-                    break
-                self.pool._wait_for_work(self)
-                continue
-            t.device_index = self.index
-            t0 = time.perf_counter()
-            if asynchronous:
-                if not cr.enqueue_mode:
-                    cr.enqueue_mode = True
-                cr.enqueue_mode_async_enable = not t._serial
-                t.compute(cr)
-                slot, val = cr.cores.last_marker(0)
-                self.inflight.append((t, slot, val))
-                self._retire()
-                while len(self.inflight) >= self.pool.max_queues:
-                    self._wait_one()
-            else:
-                t.compute(cr)
-                self.completed += 1
-                self.pool._task_done(self, t)
-            self.busy_ms += (time.perf_counter() - t0) * 1e3
-        if cr.enqueue_mode:
-            cr.enqueue_mode = False
-
-
 class ClDevicePool:
-    """Greedy device pool (reference ``ClDevicePool``)."""
+    """Greedy device pool (reference ``ClDevicePool``, ClPipeline.cs:3891).
+
+    Devices are fixed per native pool: :meth:`add_device` after tasks were
+    enqueued first waits for them (``finish``) and then rebuilds the pool."""
 
     def __init__(self, pool_type: ClDevicePoolType = ClDevicePoolType.DEVICE_COMPUTE_AT_WILL,
                  kernel_source: str = "", fine_grained_queue_control: bool = False,
@@ -246,13 +175,17 @@ class ClDevicePool:
         self.kernel_source = kernel_source
         self.prebuilt = prebuilt
         self.max_queues = max(1, min(16, int(max_queues_per_device))) if fine_grained_queue_control else 1
-        self.workers: List[_DeviceWorker] = []
-        self._lock = threading.Condition()
-        self._queue: Deque[ClTask] = collections.deque()
-        self._outstanding = 0
+        self.crunchers: List[ClNumberCruncher] = []
+        self._native = None
+        self._counts_base: List[int] = []
+        self._cv = threading.Condition()
+        self._tasks = {}  # id -> [task, completions still expected]; keeps arrays alive
+        self._next_id = 0
+        self._expected = 0
+        self._handled = 0
+        self._errors: List[str] = []
         self._closed = False
-        self._owner: Optional[_DeviceWorker] = None  # device-select group owner
-        self._blocked = False
+        self._dispatcher: Optional[threading.Thread] = None
 
     def add_device(self, devices: ClDevices) -> None:
         """Adds each device (the same device may be added several times)."""
@@ -261,104 +194,127 @@ class ClDevicePool:
                                   queue_concurrency=max(1, self.max_queues))
             if cr.error_code():
                 raise RuntimeError(cr.error_message())
-            w = _DeviceWorker(self, len(self.workers), cr)
-            self.workers.append(w)
-            w.start()
+            self.crunchers.append(cr)
+        self._rebuild()
 
     addDevice = add_device
 
+    def _rebuild(self) -> None:
+        counts = [0] * len(self.crunchers)
+        if self._native is not None:
+            self.finish()
+            for i, c in enumerate(self.device_task_counts()):
+                counts[i] = c
+            self._native.close()
+        self._counts_base = counts
+        self._native = cek.DevicePool([c.cores for c in self.crunchers], self.max_queues)
+        if self._dispatcher is None:
+            self._dispatcher = threading.Thread(target=self._dispatch_loop, daemon=True)
+            self._dispatcher.start()
+
+    # ---- completions / callbacks -------------------------------------------
+    def _dispatch_loop(self) -> None:
+        while not self._closed:
+            nat = self._native
+            if nat is None:
+                break
+            self._handle(nat.completions(20.0))
+
+    def _handle(self, comps) -> None:
+        if not comps:
+            return
+        for c in comps:
+            with self._cv:
+                entry = self._tasks.get(c.id)
+            err = c.error
+            if entry is not None:
+                t = entry[0]
+                for u in (t, getattr(t, "_origin", None)):
+                    if u is not None:
+                        u.device_index = c.device
+                        u.elapsed_ms = c.ms
+                if not err and t.callback is not None:
+                    try:
+                        t.callback()
+                    except Exception as e:  # reported by finish()
+                        err = f"callback: {e!r}"
+            with self._cv:
+                if err:
+                    self._errors.append(f"task {c.id} on device {c.device}: {err}")
+                if entry is not None:
+                    entry[1] -= 1
+                    if entry[1] <= 0:
+                        self._tasks.pop(c.id, None)
+                self._handled += 1
+                self._cv.notify_all()
+
+    # ---- producer -------------------------------------------------------------
     def enqueue_task_pool(self, pool: ClTaskPool) -> None:
-        with self._lock:
-            sync_next = False
-            while pool.tasks:
-                t = pool.tasks.popleft()
-                if sync_next:  # GLOBAL_SYNC_LAST of the previous task = barrier before this one
-                    t.type |= ClTaskType.TASK_MESSAGE_GLOBAL_SYNCHRONIZATION_FIRST
-                sync_next = bool(t.type & ClTaskType.TASK_MESSAGE_GLOBAL_SYNCHRONIZATION_LAST)
-                t._serial = bool(t.type & (ClTaskType.TASK_MESSAGE_SERIAL_MODE_BEGIN |
-                                           ClTaskType.TASK_MESSAGE_SERIAL_MODE_END))
-                if t.type & ClTaskType.TASK_MESSAGE_BROADCAST:
-                    for w in self.workers:
-                        d = t.duplicate()
-                        d._serial = t._serial
-                        d._broadcast_target = w
-                        self._queue.append(d)
-                        self._outstanding += 1
-                else:
-                    self._queue.append(t)
-                    self._outstanding += 1
-            self._lock.notify_all()
+        if self._native is None:
+            raise RuntimeError("device pool has no devices (add_device first)")
+        cr0 = self.crunchers[0]
+        ndev = len(self.crunchers)
+        batch = []
+        while pool.tasks:
+            t = pool.tasks.popleft()
+            pt = cek.PoolTask()
+            pt.type = int(t.type)
+            with self._cv:
+                pt.id = self._next_id
+                self._next_id += 1
+            if t.group is not None and t.kernels and not (t.type & ClTaskType.TASK_MESSAGE_NO_COMPUTE
+                                                          and not t.kernels):
+                try:
+                    pt.call = cr0._build_call(ClParameterGroup(), t.compute_id, t.kernels, t.global_range,
+                                              t.local_range, t.global_offset, t.pipeline, t.pipeline_type,
+                                              t.pipeline_blobs, specs=t.specs)
+                except ClComputeError as e:
+                    raise ClComputeError(f"task {pt.id}: {e}") from None
+            copies = ndev if t.type & ClTaskType.TASK_MESSAGE_BROADCAST else 1
+            with self._cv:
+                self._tasks[pt.id] = [t, copies]
+                self._expected += copies
+            batch.append(pt)
+        if batch:
+            self._native.enqueue(batch)
 
     enqueueTaskPool = enqueue_task_pool
 
-    # ---- consumer protocol --------------------------------------------------
-    def _take(self, w: _DeviceWorker) -> Optional[ClTask]:
-        with self._lock:
-            while True:
-                if not self._queue:
-                    return None
-                t = self._queue[0]
-                target = getattr(t, "_broadcast_target", None)
-                if target is not None and target is not w:
-                    # find a task this worker may take; broadcast copies wait for their device
-                    for j, u in enumerate(self._queue):
-                        if getattr(u, "_broadcast_target", None) in (None, w):
-                            if self._owner is not None and self._owner is not w and getattr(u, "_broadcast_target", None) is None:
-                                return None
-                            del self._queue[j]
-                            return self._after_take(w, u)
-                    return None
-                if self._owner is not None and self._owner is not w and target is None:
-                    return None  # a device-select group is pinned to another device
-                if t.type & ClTaskType.TASK_MESSAGE_GLOBAL_SYNCHRONIZATION_FIRST:
-                    if self._running > 0:
-                        self._blocked = True
-                        return None
-                self._queue.popleft()
-                return self._after_take(w, t)
-
-    _running = 0
-
-    def _after_take(self, w: _DeviceWorker, t: ClTask) -> ClTask:
-        if t.type & (ClTaskType.TASK_MESSAGE_DEVICE_SELECT_BEGIN | ClTaskType.TASK_MESSAGE_SERIAL_MODE_BEGIN):
-            self._owner = w
-        if t.type & (ClTaskType.TASK_MESSAGE_DEVICE_SELECT_END | ClTaskType.TASK_MESSAGE_SERIAL_MODE_END):
-            if self._owner is w:
-                self._owner = None
-        self._running += 1
-        return t
-
-    def _wait_for_work(self, w: _DeviceWorker) -> None:
-        with self._lock:
-            if not self._queue and not self._closed:
-                self._lock.wait(0.01)
-            elif self._queue:
-                self._lock.wait(0.0005)
-
-    def _task_done(self, w: _DeviceWorker, t: ClTask) -> None:
-        try:
-            t._run_callback()
-        finally:
-            with self._lock:
-                self._outstanding -= 1
-                self._running -= 1
-                self._lock.notify_all()
-
     def finish(self) -> int:
-        """Block until every enqueued task has completed; returns 0."""
-        with self._lock:
-            while self._outstanding > 0:
-                self._lock.wait(0.01)
+        """Block until every enqueued task has completed and its callback has
+        run; raises if a task failed.  Returns 0."""
+        if self._native is None:
+            return 0
+        self._native.finish()
+        while True:
+            self._handle(self._native.completions(0.0))
+            with self._cv:
+                if self._handled >= self._expected:
+                    break
+                self._cv.wait(0.005)
+        with self._cv:
+            errs, self._errors = self._errors, []
+        if errs:
+            raise ClComputeError("device pool: " + "; ".join(errs))
         return 0
 
     def device_task_counts(self) -> List[int]:
-        return [w.completed for w in self.workers]
+        if self._native is None:
+            return []
+        return [int(b + c) for b, c in zip(self._counts_base, self._native.device_task_counts())]
+
+    def device_busy_ms(self) -> List[float]:
+        return list(self._native.device_busy_ms()) if self._native is not None else []
 
     def dispose(self) -> None:
-        self.finish()
-        with self._lock:
-            self._closed = True
-            self._lock.notify_all()
-        for w in self.workers:
-            w.join(5.0)
-            w.cruncher.dispose()
+        if self._native is not None:
+            try:
+                self.finish()
+            finally:
+                self._closed = True
+                self._native.close()
+                if self._dispatcher is not None:
+                    self._dispatcher.join(5.0)
+        for cr in self.crunchers:
+            cr.dispose()
+        self.crunchers = []

@@ -81,3 +81,49 @@ def test_global_sync_orders_phases():
     assert sorted(order) == list(range(12))
     assert set(order[:6]) == set(range(6))  # everything before the barrier finished first
     pool.dispose()
+
+
+def test_broadcast_runs_on_every_device_and_select_group_pins():
+    cpu = ck.ClPlatforms.all().cpus(True)
+    pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, True, 3)
+    pool.add_device(cpu + cpu + cpu)
+    tp = ClTaskPool()
+    seen = []
+    lock = threading.Lock()
+    _, b = _task("fill", 256, 7.0)
+    b.type = ClTaskType.TASK_MESSAGE_BROADCAST
+    b.set_callback(lambda: (lock.acquire(), seen.append("b"), lock.release()))
+    tp.feed(b)
+    # a device-select group: every task of it runs on one device
+    group = []
+    for k in range(6):
+        _, t = _task("fill", 256, float(k))
+        if k == 0:
+            t.type = ClTaskType.TASK_MESSAGE_DEVICE_SELECT_BEGIN
+        if k == 5:
+            t.type = ClTaskType.TASK_MESSAGE_DEVICE_SELECT_END
+        group.append(t)
+        tp.feed(t)
+    pool.enqueue_task_pool(tp)
+    pool.finish()
+    assert seen == ["b"] * 3  # one callback per device copy
+    assert len({t.device_index for t in group}) == 1 and group[0].device_index is not None
+    assert sum(pool.device_task_counts()) == 3 + 6
+    pool.dispose()
+
+
+def test_task_error_is_reported_by_finish():
+    cpu = ck.ClPlatforms.all().cpus(True)
+    pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, True, 2)
+    pool.add_device(cpu)
+    tp = ClTaskPool()
+    _, t = _task("fill", 256, 1.0)
+    t.kernels = "no_such_kernel"
+    tp.feed(t)
+    _, ok = _task("fill", 256, 2.0)
+    tp.feed(ok)
+    pool.enqueue_task_pool(tp)
+    with pytest.raises(ck.ClComputeError, match="no_such_kernel"):
+        pool.finish()
+    assert sum(pool.device_task_counts()) == 2  # the failing task retired too
+    pool.dispose()
