@@ -213,8 +213,12 @@ PYBIND11_MODULE(_cek, m) {
   py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
       .def_static("unique_id", []() { return py::bytes(Comm::unique_id()); })
       .def(py::init([](py::bytes uid, int rank, int world, int device) {
-             return std::make_shared<Comm>(std::string(uid), rank, world, device);
-           }), py::call_guard<py::gil_scoped_release>())
+        // copy the id while holding the GIL; only the RCCL rendezvous runs
+        // without it (the bytes object is released by pybind11, GIL held)
+        std::string id(uid);
+        py::gil_scoped_release r;
+        return std::make_shared<Comm>(id, rank, world, device);
+      }))
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("world", &Comm::world)
       .def("broadcast", [](Comm& c, uint64_t p, uint64_t bytes, int root, uint64_t stream) {

@@ -125,7 +125,14 @@ class DistributedCruncher(ClNumberCruncher):
         super().__init__(devices, kernel_source, **kwargs)
         self._exchanger = None
         self._comm = None
-        if not self.ctx.is_distributed or self._cores is None:
+        if self._cores is None:
+            return
+        if not self.ctx.is_distributed:
+            if comm and self._cores.num_devices == 1 and self.devices.device(0).is_gpu:
+                # a one-rank RCCL communicator: the data-plane code path (broadcast
+                # of reads, all-gather of written slices) runs exactly as at N ranks
+                self._comm = cek.Comm(cek.Comm.unique_id(), 0, 1, self.devices.device(0).info.ordinal)
+                self._cores.set_distributed(None, self._comm, 1, 0)
             return
         import torch.distributed as dist
 

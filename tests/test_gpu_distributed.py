@@ -84,3 +84,39 @@ def test_two_ranks_share_gpu0():
     assert res[0][1] and res[1][1], (res[0][2], res[1][2])
     assert res[0][0] == res[1][0]
     assert all(sum(s) == 2 * 4 * 512 for s in res[0][0])
+
+
+def test_rccl_data_plane_one_rank():
+    """The RCCL data plane of DistributedCruncher (rank-0 upload + broadcast of
+    ``read`` arrays, in-place all-gather-v of written slices into the device
+    replica) on a one-rank communicator, plus the raw Comm collectives on
+    torch device memory.  Multi-rank RCCL needs one GPU per rank."""
+    import cekirdekler_amd as ck
+    from cekirdekler_amd._native import cek
+    from cekirdekler_amd.parallel.distributed import DistContext, DistributedCruncher
+
+    gpu = ck.ClPlatforms.all().gpus()[0]
+    src = """__global__ void k(const float* a, float* y) {
+        long long i = get_global_id(0); y[i] = a[i] * 3.0f + 1.0f; }"""
+    cr = DistributedCruncher(src, ctx=DistContext(), devices=gpu, comm=True)
+    cr.broadcast_reads = True
+    cr.gather_writes = True
+    n = 256 * 64
+    a = ck.ClArray(np.arange(n, dtype=np.float32))
+    a.write = False
+    y = ck.ClArray(np.zeros(n, np.float32))
+    y.read = False
+    for _ in range(3):
+        a.next_param(y).compute(cr, 1, "k", n, 256)
+    np.testing.assert_allclose(y.array, np.arange(n, dtype=np.float32) * 3 + 1)
+    cr.download(y, 0)  # the gathered device replica holds every slice
+    np.testing.assert_allclose(y.array, np.arange(n, dtype=np.float32) * 3 + 1)
+    cr.dispose()
+
+    comm = cek.Comm(cek.Comm.unique_id(), 0, 1, gpu.device(0).info.ordinal)
+    t = torch.arange(1024, dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    comm.allreduce_sum_f32(t.data_ptr(), t.numel(), s)
+    comm.broadcast(t.data_ptr(), t.numel() * 4, 0, s)
+    torch.cuda.synchronize()
+    assert torch.equal(t.cpu(), torch.arange(1024, dtype=torch.float32))
