@@ -21,6 +21,7 @@ from __future__ import annotations
 import os
 import socket
 import uuid
+import warnings
 from dataclasses import dataclass
 from typing import Optional
 
@@ -125,6 +126,7 @@ class DistributedCruncher(ClNumberCruncher):
         super().__init__(devices, kernel_source, **kwargs)
         self._exchanger = None
         self._comm = None
+        self._warned_incoherent = False
         if self._cores is None:
             return
         if not self.ctx.is_distributed:
@@ -177,6 +179,22 @@ class DistributedCruncher(ClNumberCruncher):
         if v and self._comm is None and self.ctx.is_distributed:
             raise RuntimeError("broadcast_reads needs DistributedCruncher(comm=True)")
         self._cores.dist_broadcast_reads = bool(v)
+
+    def _build_call(self, *args, **kwargs):
+        call = super()._build_call(*args, **kwargs)
+        if self.ctx.is_distributed and not self._warned_incoherent and not (
+                self._comm is not None and self._cores.dist_gather_writes):
+            for a in call.arrays:
+                if a.read and not a.partial and a.write and not a.write_all and not a.zc:
+                    self._warned_incoherent = True
+                    warnings.warn(
+                        "DistributedCruncher: an array is read whole and written by slices. Each rank's "
+                        "host copy receives only that rank's slices, and re-balancing moves work items "
+                        "between ranks, so later reads see stale values from the other ranks. Use "
+                        "comm=True with gather_writes (RCCL all-gather over xGMI), partial_read, or read=False.",
+                        RuntimeWarning, stacklevel=4)
+                    break
+        return call
 
     def barrier(self) -> None:
         if self._exchanger is not None:

@@ -20,6 +20,7 @@
 from __future__ import annotations
 
 import itertools
+import time
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
@@ -136,8 +137,10 @@ def buffers() -> int:
 
 
 def nbody(n: int = 8 * 1024, devices: Optional[ClDevices] = None, stream: bool = False, log: bool = True,
-          iterations: int = 150, check: bool = True) -> int:
-    """2-D all-pairs forces (softening 1e-4), host reference vs device."""
+          iterations: int = 150, check: bool = True, timing: Optional[list] = None) -> int:
+    """2-D all-pairs forces (softening 1e-4), host reference vs device.
+    With ``timing`` (a list), one untimed warm-up compute runs first and the
+    wall time of the ``iterations`` computes (ms) is appended to it."""
     rng = np.random.default_rng(1234)
     x = (rng.random(n, dtype=np.float64) * 30 - 15).astype(np.float32)
     y = (rng.random(n, dtype=np.float64) * 30 - 15).astype(np.float32)
@@ -167,8 +170,13 @@ def nbody(n: int = 8 * 1024, devices: Optional[ClDevices] = None, stream: bool =
     xa.write = ya.write = False
     fx, fy = ClArray(np.zeros(n, np.float32)), ClArray(np.zeros(n, np.float32))
     fx.read = fy.read = False
+    if timing is not None:
+        xa.next_param(ya, fx, fy).compute(cr, 1, "nBody", n, 64)  # build buffers, first upload
+        t0 = time.perf_counter()
     for _ in range(iterations):
         xa.next_param(ya, fx, fy).compute(cr, 1, "nBody", n, 64)
+    if timing is not None:
+        timing.append((time.perf_counter() - t0) * 1e3)
     if not check:
         cr.dispose()
         return 0

@@ -239,3 +239,12 @@ def test_record_log_json_lines(cpu, tmp_path, monkeypatch):
     assert len(lines) == 3 and lines[-1]["compute_id"] == 5 and lines[-1]["kernels"] == ["inc"]
     assert sum(lines[-1]["ranges"]) == 256 and lines[-1]["h2d_bytes"] == 1024
     c.dispose()
+
+
+def test_devices_ranked_by_nbody_time(cpu):
+    """ClDevices.devicesWithHighestDirectNbodyPerformance (ClObjectApi.cs:1222-1244):
+    every device runs the N-body test alone; the list comes back fastest first
+    (here: two copies of the CPU device, so only the shape is checked)."""
+    plats = ck.ClPlatforms.all()
+    ranked = (plats.cpus(True) + plats.cpus(True)).devices_with_highest_direct_nbody_performance(n=1024)
+    assert len(ranked) == 2 and all(d.is_cpu for d in ranked)

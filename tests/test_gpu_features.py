@@ -321,3 +321,11 @@ def test_device_printf(gpu, capfd):
     c.dispose()
     out = capfd.readouterr().out
     assert out.count("hello world") == 1000
+
+
+def test_devices_ranked_by_nbody_time_gpu_first(gpu):
+    """N-body-timed ranking (ClObjectApi.cs:1222-1244): the MI355X beats the
+    host CPU device."""
+    plats = ck.ClPlatforms.all()
+    ranked = (plats.cpus(True) + gpu[0]).devices_with_highest_direct_nbody_performance(n=4096)
+    assert ranked.device(0).is_gpu and ranked.device(1).is_cpu
