@@ -21,6 +21,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -193,6 +194,33 @@ def bench_lb_iters():
     return {"iters": it + 1, "steady_share_dev0": steady}
 
 
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def bench_node_configs(world: int) -> dict:
+    """BASELINE configs 4 and 5 on this job's GPUs (0 .. world-1), run by
+    rank 0 after every other rank has left: the N-body 3-stage
+    device→device pipeline (stage transitions over xGMI) and the 256-task
+    pool over a device pool.  Both are single-process multi-GPU programs (the
+    reference's model), so each runs as a child process with its own time
+    limit; a failure is reported in its field and cannot stop the headline."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    out = {}
+    for name, script, args in (("nbody_pipeline", "nbody_pipeline.py", ["--pushes", "8"]),
+                               ("task_pool", "task_pool.py", [])):
+        try:
+            r = subprocess.run([sys.executable, script, "--gpus", str(world), *args], cwd=os.path.join(ROOT, "bench"),
+                               env=env, capture_output=True, text=True, timeout=180)
+            lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            out[name] = json.loads(lines[-1]) if (r.returncode == 0 and lines) else {
+                "error": f"exit {r.returncode}: {(r.stderr or r.stdout)[-300:]}"}
+        except Exception as e:  # timeout or parse failure
+            out[name] = {"error": repr(e)[:300]}
+    return out
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -201,6 +229,8 @@ def main(argv=None) -> int:
     ap.add_argument("--size", type=int, default=8192)
     ap.add_argument("--tile", default=None)
     ap.add_argument("--skip-mandelbrot", action="store_true")
+    ap.add_argument("--skip-node-configs", action="store_true",
+                    help="skip the N-body pipeline and task-pool configs (rank 0, after the headline)")
     args = ap.parse_args(argv)
 
     from cekirdekler_amd.parallel.distributed import init_distributed
@@ -209,6 +239,12 @@ def main(argv=None) -> int:
     sg = bench_sgemm(ctx, args.steps, args.warmup, args.size, args.tile)
     mb = {} if args.skip_mandelbrot else bench_mandelbrot(ctx, args.steps, args.warmup)
     lb = bench_lb_iters() if ctx.rank == 0 else {}
+    if ctx.is_distributed:
+        import torch.distributed as dist
+
+        dist.barrier()
+        dist.destroy_process_group()  # the other ranks exit here; rank 0 goes on alone
+    node = {} if (ctx.rank != 0 or args.skip_node_configs) else bench_node_configs(ctx.world)
     if ctx.rank == 0:
         out = {
             "metric": METRIC,
@@ -235,14 +271,11 @@ def main(argv=None) -> int:
                 "sgemm_ranges": sg["ranges"],
                 "mandelbrot_4k": mb,
                 "load_balance_iters": lb,
+                "nbody_pipeline": node.get("nbody_pipeline"),
+                "task_pool": node.get("task_pool"),
             },
         }
         print(json.dumps(out), flush=True)
-    if ctx.is_distributed:
-        import torch.distributed as dist
-
-        dist.barrier()
-        dist.destroy_process_group()
     return 0
 
 

@@ -173,6 +173,12 @@ class ClPipelineStage:
             # materialise every replica with the host contents once
             for a in self.inputs + self._in_dup + self.outputs + self._out_dup + self.hiddens:
                 self.cruncher.upload(a, 0)
+        else:
+            # hidden buffers never move per push; every device's replica starts
+            # from the host contents (constants, initial state), as above
+            for a in self.hiddens:
+                for d in range(self.cruncher.cores.num_devices):
+                    self.cruncher.upload(a, d)
 
     def _group(self, dup: bool) -> ClParameterGroup:
         ins = self._in_dup if dup else self.inputs

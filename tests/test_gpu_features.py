@@ -329,3 +329,33 @@ def test_devices_ranked_by_nbody_time_gpu_first(gpu):
     plats = ck.ClPlatforms.all()
     ranked = (plats.cpus(True) + gpu[0]).devices_with_highest_direct_nbody_performance(n=4096)
     assert ranked.device(0).is_gpu and ranked.device(1).is_cpu
+
+
+def test_cl_pipeline_multi_gpu_stage_hidden_constants(gpu):
+    """A stage on two (logical) GPUs is range-split and host-staged; its
+    hidden buffers' host contents reach every device's replica."""
+    from cekirdekler_amd.parallel.pipeline import ClPipelineStage
+
+    n = 4096
+    ks = "__global__ void scale(const float* x, const float* c, float* y) { long long i = get_global_id(0); y[i] = x[i] * c[0]; }"
+    k2 = "__global__ void sub3(const float* z, float* w) { long long i = get_global_id(0); w[i] = z[i] - 3.0f; }"
+    s1, s2 = ClPipelineStage(), ClPipelineStage()
+    s1.add_devices(gpu[0] + gpu[0])
+    s1.add_kernels(ks, "scale", [n], [64])
+    s1.add_input_buffers(np.zeros(n, np.float32))
+    s1.add_hidden_buffers(np.array([3.0], np.float32))
+    s1.add_output_buffers(np.zeros(n, np.float32))
+    s2.add_devices(gpu[0])
+    s2.add_kernels(k2, "sub3", [n], [64])
+    s2.add_input_buffers(np.zeros(n, np.float32))
+    s2.add_output_buffers(np.zeros(n, np.float32))
+    s1.prepend_to_stage(s2)
+    pipe = s1.make_pipeline()
+    res = np.zeros(n, np.float32)
+    seen = []
+    for p in range(8):
+        if pipe.push_data([np.full(n, float(p), np.float32)], [res]):
+            assert np.all(res == res[0])
+            seen.append(float(res[0]))
+    pipe.dispose()
+    assert seen == [3.0 * p - 3.0 for p in range(len(seen))] and len(seen) == 4

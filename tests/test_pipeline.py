@@ -70,3 +70,24 @@ def test_device_pipeline_transition_double_buffer():
     # value p enters at feed p+1, passes stage a at p+1, stage b at p+2
     assert got[3:] == [(p + 1) - 3 for p in range(1, 4)]
     dp.dispose()
+
+
+def test_multi_device_stage_sees_hidden_constants():
+    """A stage on several devices (range-split, host-staged) reads its hidden
+    buffers' initial host contents on every device."""
+    cpu = ck.ClPlatforms.all().cpus(True)
+    ks = "__global__ void scale(const float* x, const float* c, float* y) { long long i = get_global_id(0); y[i] = x[i] * c[0]; }"
+    x, y = np.zeros(N, np.float32), np.zeros(N, np.float32)
+    c = np.array([3.0], np.float32)
+    s1 = _stage(cpu + cpu, ks, "scale", [x], [c], [y])
+    s2 = _stage(cpu, K3, "sub3", [np.zeros(N, np.float32)], None, [np.zeros(N, np.float32)])
+    s1.prepend_to_stage(s2)
+    pipe = s1.make_pipeline()
+    res = np.zeros(N, np.float32)
+    seen = []
+    for p in range(8):
+        if pipe.push_data([np.full(N, float(p), np.float32)], [res]):
+            assert np.all(res == res[0])
+            seen.append(float(res[0]))
+    assert seen == [3.0 * p - 3.0 for p in range(len(seen))] and len(seen) == 8 - 4
+    pipe.dispose()
