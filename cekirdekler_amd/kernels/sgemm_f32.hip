@@ -1,0 +1,299 @@
+// fp32 GEMM on CDNA4 matrix cores (v_mfma_f32_16x16x4_f32), fp32 in / out:
+// the single-precision member of the range-partitioned GEMM family.
+//
+//   C = A · Bᵀ      A: [M][K] f32 row-major, Bt: [N][K] f32 row-major
+//   C is written TILE-MAJOR in the grouped tile order of kernels/sgemm_bf16.hip,
+//   so a device's contiguous range of tiles is one contiguous slice of C.
+//
+// Structure: BK = 32 floats = 128 B per row, the same byte geometry as the
+// bf16 kernels (BK = 64 bf16).  Both operands go global→LDS with
+// global_load_lds_dwordx4 (16 B per lane, 8 rows × 128 B per wave
+// instruction) into two LDS stages, XOR-swizzling the 16-B chunk index with
+// (row & 7) on the global source and on the ds_read_b128 address
+// (conflict-free fragment reads).
+//
+// Fragments: v_mfma_f32_16x16x4_f32 takes one float of A per lane
+// (A[row = l%16][k = l/16]) and one of B.  A lane instead reads 16 B —
+// A[row][4·(l/16) .. 4·(l/16)+3] of a 16-deep k block — and feeds element t
+// to the t-th of four MFMAs: MFMA t then sums over k ∈ {t, 4+t, 8+t, 12+t}
+// for A and B alike, and the four together cover the k block exactly.
+// One ds_read_b128 per operand fragment per 16 k, four MFMAs per read.
+#include "cek_kernel.h"
+
+namespace {
+
+template <int WM, int WN, int FM, int FN, bool PIPE>
+__device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, const float* __restrict__ A,
+                                              const float* __restrict__ Bt, float* __restrict__ C, char* smem,
+                                              long long off) {
+  constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN, BK = 32;
+  constexpr int NWAVES = WM * WN, NT = 64 * NWAVES;
+  constexpr int A_BYTES = BM * BK * 4, B_BYTES = BN * BK * 4, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_INSTR = A_BYTES / 1024 / NWAVES, B_INSTR = B_BYTES / 1024 / NWAVES;
+  static_assert(A_INSTR * NWAVES * 1024 == A_BYTES && B_INSTR * NWAVES * 1024 == B_BYTES, "staging split");
+
+  const int M = dims[0], N = dims[1], K = dims[2], GM = dims[3] > 0 ? dims[3] : 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WN, wc = wave % WN;
+  const long long t = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
+  const int ntn = N / BN, ntm = M / BM;
+  const int per_group = GM * ntn, grp = (int)(t / per_group), first = grp * GM;
+  const int gsz = min(ntm - first, GM), in_g = (int)(t % per_group);
+  const int tm = first + in_g % gsz, tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // staging: lane l of a wave instruction lands at row ins·8 + l/8, physical
+  // 16-B chunk l%8, which holds logical chunk (l%8) ^ (row & 7)
+  const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
+  const unsigned lane_off = (unsigned)(lrow * K + lchunk * 4) * 4u;
+  const char* a_wave = (const char*)(A + (size_t)(m0 + wave * A_INSTR * 8) * K);
+  const char* b_wave = (const char*)(Bt + (size_t)(n0 + wave * B_INSTR * 8) * K);
+  auto stage = [&](int buf, int kt) {
+    char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < A_INSTR; ++j) {
+      const char* src = a_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 4;
+      __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
+                                       (lds_void*)(base + (wave * A_INSTR + j) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < B_INSTR; ++j) {
+      const char* src = b_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 4;
+      __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
+                                       (lds_void*)(base + A_BYTES + (wave * B_INSTR + j) * 1024), 16, 0, 0);
+    }
+  };
+
+  // fragment offsets: row (wr·16FM + i·16 + l%16), logical chunk s·4 + l/16
+  const int fr = lane & 15, fq = lane >> 4;
+  int a_off[2], b_off[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int pc = (s * 4 + fq) ^ (lane & 7);
+    a_off[s] = (wr * 16 * FM + fr) * 128 + pc * 16;
+    b_off[s] = A_BYTES + (wc * 16 * FN + fr) * 128 + pc * 16;
+  }
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  auto ld = [&](f32x4(&a)[FM], f32x4(&b)[FN], const char* base, int s) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) b[j] = *(const f32x4*)(base + b_off[s] + j * 2048);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) a[i] = *(const f32x4*)(base + a_off[s] + i * 2048);
+  };
+  auto mma = [&](const f32x4(&a)[FM], const f32x4(&b)[FN]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr (!PIPE) {
+    // one barrier per K-tile; the next K-tile's DMA flies under the MFMAs
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+      const char* base = smem + cur * STAGE;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        f32x4 a[FM], b[FN];
+        ld(a, b, base, s);
+        mma(a, b);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    // register double-buffered fragments: the second 16-deep k block is read
+    // while the first one's MFMAs run, and the next K-tile's first block
+    // right after the barrier that publishes it, under the second's MFMAs
+    f32x4 xa[FM], xb[FN], ya[FM], yb[FN];
+    ld(xa, xb, smem, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      const char* base = smem + cur * STAGE;
+      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+      ld(ya, yb, base, 1);
+      mma(xa, xb);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kt + 1 < nk) ld(xa, xb, smem + (cur ^ 1) * STAGE, 0);
+      mma(ya, yb);
+    }
+  }
+
+  // acc[i][j][r] is C(row = wr·16FM + i·16 + fq·4 + r, col = wc·16FN + j·16 + fr)
+  float* ct = C + (size_t)t * BM * BN;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr] = acc[i][j][r];
+}
+
+
+// The same tile with v_mfma_f32_32x32x2_f32 (64 cycles, 32×32 outputs):
+// lane l reads A[row = l%32][8·kb + 4·(l/32) .. +3] and feeds element t to
+// the t-th of four MFMAs, which then sum over k ∈ {t, 4+t} of the 8-deep
+// block kb.  Fragments per 8-deep block are half those of a 16-deep block of
+// the 16×16×4 form, so two register sets (double-buffered across the four
+// blocks of a K-tile) fit beside the 128 accumulator registers of a 128×64
+// wave tile; the 16×16×4 form spills there.
+// Output layout: acc[i][j][r] is C(row = 32i + 8·(r/4) + 4·(l/32) + r%4, col = 32j + l%32).
+template <int WM, int WN, int FM, int FN>
+__device__ __forceinline__ void gemm_f32w_tile(const int* __restrict__ dims, const float* __restrict__ A,
+                                               const float* __restrict__ Bt, float* __restrict__ C, char* smem,
+                                               long long off) {
+  constexpr int BM = WM * 32 * FM, BN = WN * 32 * FN, BK = 32;
+  constexpr int NWAVES = WM * WN, NT = 64 * NWAVES;
+  constexpr int A_BYTES = BM * BK * 4, B_BYTES = BN * BK * 4, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_INSTR = A_BYTES / 1024 / NWAVES, B_INSTR = B_BYTES / 1024 / NWAVES;
+  static_assert(A_INSTR * NWAVES * 1024 == A_BYTES && B_INSTR * NWAVES * 1024 == B_BYTES, "staging split");
+
+  const int M = dims[0], N = dims[1], K = dims[2], GM = dims[3] > 0 ? dims[3] : 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WN, wc = wave % WN;
+  const long long t = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
+  const int ntn = N / BN, ntm = M / BM;
+  const int per_group = GM * ntn, grp = (int)(t / per_group), first = grp * GM;
+  const int gsz = min(ntm - first, GM), in_g = (int)(t % per_group);
+  const int tm = first + in_g % gsz, tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
+  const unsigned lane_off = (unsigned)(lrow * K + lchunk * 4) * 4u;
+  const char* a_wave = (const char*)(A + (size_t)(m0 + wave * A_INSTR * 8) * K);
+  const char* b_wave = (const char*)(Bt + (size_t)(n0 + wave * B_INSTR * 8) * K);
+  auto stage = [&](int buf, int kt) {
+    char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < A_INSTR; ++j) {
+      const char* src = a_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 4;
+      __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
+                                       (lds_void*)(base + (wave * A_INSTR + j) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < B_INSTR; ++j) {
+      const char* src = b_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 4;
+      __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
+                                       (lds_void*)(base + A_BYTES + (wave * B_INSTR + j) * 1024), 16, 0, 0);
+    }
+  };
+
+  // fragment offsets for 8-deep block kb: row (wr·32FM + i·32 + l%32),
+  // logical 16-B chunk 2·kb + l/32, physical = logical ^ (row & 7)
+  const int fr = lane & 31, fq = lane >> 5;
+  int a_off[4], b_off[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    const int pc = (kb * 2 + fq) ^ (lane & 7);
+    a_off[kb] = (wr * 32 * FM + fr) * 128 + pc * 16;
+    b_off[kb] = A_BYTES + (wc * 32 * FN + fr) * 128 + pc * 16;
+  }
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto ld = [&](f32x4(&a)[FM], f32x4(&b)[FN], const char* base, int kb) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) b[j] = *(const f32x4*)(base + b_off[kb] + j * 4096);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) a[i] = *(const f32x4*)(base + a_off[kb] + i * 4096);
+  };
+  auto mma = [&](const f32x4(&a)[FM], const f32x4(&b)[FN]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = K / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  f32x4 xa[FM], xb[FN], ya[FM], yb[FN];
+  ld(xa, xb, smem, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const char* base = smem + cur * STAGE;
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    ld(ya, yb, base, 1);
+    mma(xa, xb);
+    ld(xa, xb, base, 2);
+    mma(ya, yb);
+    ld(ya, yb, base, 3);
+    mma(xa, xb);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) ld(xa, xb, smem + (cur ^ 1) * STAGE, 0);
+    mma(ya, yb);
+  }
+
+  float* ct = C + (size_t)t * BM * BN;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        ct[(size_t)(wr * 32 * FM + i * 32 + (r / 4) * 8 + fq * 4 + (r % 4)) * BN + wc * 32 * FN + j * 32 + fr] =
+            acc[i][j][r];
+}
+
+}  // namespace
+
+#define CEK_GEMM_F32_KERNEL(NAME, WM, WN, FM, FN, PIPE)                                           \
+  extern "C" __global__ __launch_bounds__(64 * WM * WN) void NAME(                                 \
+      const int* dims, const float* A, const float* Bt, float* C, CEK_HIDDEN) {                     \
+    __shared__ __attribute__((aligned(16))) char smem[2 * (WM * 16 * FM + WN * 16 * FN) * 32 * 4]; \
+    gemm_f32_tile<WM, WN, FM, FN, PIPE>(dims, A, Bt, C, smem, __cek_off);                           \
+  }
+
+// 128×128 tiles, 4 waves (2×2, 64×64 each), 64 KiB LDS: two work-groups per CU.
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_128x128, 2, 2, 4, 4, false)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_128x128p, 2, 2, 4, 4, true)
+// 256×128 tiles, 8 waves (4×2, 64×64 each), 96 KiB LDS.
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128, 4, 2, 4, 4, false)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128p, 4, 2, 4, 4, true)
+// 256×256 tiles, 8 waves (2×4, 128×64 each), 128 KiB LDS.
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256, 2, 4, 8, 4, false)
+// (a register double-buffered 256×256 variant needs 256 + 57 spilled VGPRs)
+
+// 32×32×2 form with register double-buffered fragments (gemm_f32w_tile).
+#define CEK_GEMM_F32W_KERNEL(NAME, WM, WN, FM, FN)                                                 \
+  extern "C" __global__ __launch_bounds__(64 * WM * WN) void NAME(                                  \
+      const int* dims, const float* A, const float* Bt, float* C, CEK_HIDDEN) {                      \
+    __shared__ __attribute__((aligned(16))) char smem[2 * (WM * 32 * FM + WN * 32 * FN) * 32 * 4];  \
+    gemm_f32w_tile<WM, WN, FM, FN>(dims, A, Bt, C, smem, __cek_off);                                 \
+  }
+
+CEK_GEMM_F32W_KERNEL(cek_sgemm_f32_256x256w, 2, 4, 4, 2)  // 8 waves, 128×64 each, 128 KiB LDS
+CEK_GEMM_F32W_KERNEL(cek_sgemm_f32_256x128w, 4, 2, 2, 2)  // 8 waves, 64×64 each, 96 KiB LDS
+CEK_GEMM_F32W_KERNEL(cek_sgemm_f32_128x128w, 2, 2, 2, 2)  // 4 waves, 64×64 each, 64 KiB LDS

@@ -1,4 +1,5 @@
-"""Range-partitioned bf16 GEMM (the "SGEMM 8192² bf16" config of BASELINE.json).
+"""Range-partitioned GEMMs: bf16 (the "SGEMM 8192² bf16" config of
+BASELINE.json) and fp32 on the fp32 matrix cores.
 
 ``C = A · Bᵀ`` with A ``[M][K]`` and Bt ``[N][K]`` bf16 row-major, C fp32 in
 tile-major layout (see ``kernels/sgemm_bf16.hip``).  The global range is one
@@ -50,6 +51,20 @@ TILES = {
 
 
 GEMM_LIBS = ("sgemm_bf16", "sgemm8p_bf16", "sgemm_pp32_bf16")
+
+# fp32 tiles (kernels/sgemm_f32.hip): v_mfma_f32_16x16x4_f32, BK = 32
+F32_TILES = {
+    "128x128": (128, 128, 256, "cek_sgemm_f32_128x128"),
+    "256x128": (256, 128, 512, "cek_sgemm_f32_256x128"),
+    "256x256": (256, 256, 512, "cek_sgemm_f32_256x256"),
+    # "p": register double-buffered fragments (next k block read under the MFMAs)
+    "128x128p": (128, 128, 256, "cek_sgemm_f32_128x128p"),
+    "256x128p": (256, 128, 512, "cek_sgemm_f32_256x128p"),
+    # "w": v_mfma_f32_32x32x2_f32 with register double-buffered fragments
+    "256x256w": (256, 256, 512, "cek_sgemm_f32_256x256w"),
+    "256x128w": (256, 128, 512, "cek_sgemm_f32_256x128w"),
+    "128x128w": (128, 128, 256, "cek_sgemm_f32_128x128w"),
+}
 
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
 SPLIT_K_TILES = {"256x256pp", "256x128pp", "256x256pb"}
@@ -197,4 +212,46 @@ class GemmBf16:
     def reference(self, rows: slice = slice(None)) -> np.ndarray:
         a = from_bf16_bits(self.A.array).reshape(self.M, self.K)[rows].astype(np.float64)
         b = from_bf16_bits(self.B.array).reshape(self.N, self.K).astype(np.float64)
+        return a @ b.T
+
+
+class GemmF32(GemmBf16):
+    """``C = A · Bᵀ`` in fp32 on the fp32 matrix cores (``v_mfma_f32_16x16x4_f32``):
+    A ``[M][K]``, Bt ``[N][K]`` and C fp32, C tile-major like :class:`GemmBf16`
+    (same grouped tile order, so the same range partitioning and
+    wave-quantized balancing apply)."""
+
+    def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256",
+                 cruncher: ClNumberCruncher | None = None, fill: str = "random", seed: int = 0,
+                 group_m: int = 4, wave_granularity: bool | None = None):
+        # 256x256: 140 TF/s at 8192³, 91 % of hipBLASLt fp32 (profiles/gemm_f32_findings.md)
+        BM, BN, L, kname = F32_TILES[tile]
+        if M % BM or N % BN or K % 32:
+            raise ValueError(f"M%{BM}, N%{BN} and K%32 must be 0 (got {M},{N},{K})")
+        self.M, self.N, self.K, self.BM, self.BN, self.L, self.kernel = M, N, K, BM, BN, L, kname
+        self.split_k = 1
+        self.tiles = (M // BM) * (N // BN)
+        self.global_range = self.tiles * L
+        self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library("sgemm_f32"))
+        self.group_m = group_m
+        self.dims = ClArray(np.array([M, N, K, group_m, 1, 0, 0, 0], np.int32))
+        self.dims.write = False
+        self.A = ClArray(M * K, np.float32)
+        self.B = ClArray(N * K, np.float32)
+        self.C = ClArray(M * N, np.float32)
+        for a in (self.A, self.B):
+            a.write = False
+        self.C.read = False
+        self.C.elements_per_work_item = BM * BN // L
+        self.extra = []
+        if fill == "random":
+            rng = np.random.default_rng(seed)
+            self.A.array[:] = rng.uniform(-1, 1, M * K).astype(np.float32)
+            self.B.array[:] = rng.uniform(-1, 1, N * K).astype(np.float32)
+        self._uploaded = False
+        self.wave_granularity = wave_granularity
+
+    def reference(self, rows: slice = slice(None)) -> np.ndarray:
+        a = self.A.array.reshape(self.M, self.K)[rows].astype(np.float64)
+        b = self.B.array.reshape(self.N, self.K).astype(np.float64)
         return a @ b.T

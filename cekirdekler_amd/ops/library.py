@@ -23,6 +23,9 @@ LIBRARY = {
                    "cek_sgemm_bf16_256x128pe"],
     "sgemm8p_bf16": ["cek_sgemm8p_bf16_r8", "cek_sgemm8p_bf16_r10"],
     "sgemm_pp32_bf16": ["cek_sgemm_bf16_256x256q", "cek_sgemm_bf16_256x128q"],
+    "sgemm_f32": ["cek_sgemm_f32_128x128", "cek_sgemm_f32_256x128", "cek_sgemm_f32_256x256",
+                  "cek_sgemm_f32_128x128p", "cek_sgemm_f32_256x128p",
+                  "cek_sgemm_f32_256x256w", "cek_sgemm_f32_256x128w", "cek_sgemm_f32_128x128w"],
     "mandelbrot": ["cek_mandelbrot_f32", "cek_mandelbrot_pool16_f32", "cek_mandelbrot_pool8_f32",
                    "cek_mandelbrot_pk16_f32", "cek_mandelbrot_pk32_f32", "cek_mandelbrot_blk16_f32",
                    "cek_mandelbrot_blk64_f32", "cek_mandelbrot_blk8_f32"],
@@ -37,6 +40,7 @@ LIBRARY = {
 # signature is rejected on the host instead of faulting on the device.
 ARITY = {
     **{k: (6 if k.endswith("_sk") else 4) for k in LIBRARY["sgemm_bf16"] + LIBRARY["sgemm8p_bf16"] + LIBRARY["sgemm_pp32_bf16"]},
+    **{k: 4 for k in LIBRARY["sgemm_f32"]},
     **{k: 3 for k in LIBRARY["mandelbrot"]},
     **{k: 4 for k in LIBRARY["nbody"] if "energy" not in k},
     **{k: 3 for k in LIBRARY["nbody"] if "energy" in k},

@@ -143,7 +143,7 @@ def test_gemm_wave_granularity_two_logical_devices():
     assert GemmBf16(256, 256, 64, devices=g0, tile="256x256pb").granularity() == 512  # < 1 wave: per tile
 
 
-@pytest.mark.parametrize("kernel", ["quad","pool8", "pool16", "pk16", "pk32", "blk16", "blk64", "blk8"])
+@pytest.mark.parametrize("kernel", ["quad", "pool8", "pool16", "pk16", "pk32", "blk16", "blk64", "blk8"])
 def test_mandelbrot_event_pipeline_matches_numpy(kernel):
     from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
 
@@ -197,3 +197,21 @@ def test_nbody_steps_two_logical_devices(resident):
     one.download()
     two.download()
     np.testing.assert_allclose(two.pos.array, one.pos.array, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("tile", ["128x128", "256x128", "256x256", "128x128p", "256x128p", "256x256w", "256x128w", "128x128w"])
+@pytest.mark.parametrize("shape", [(512, 512, 256), (768, 512, 96), (512, 256, 32)])
+def test_gemm_f32_matches_fp64(tile, shape):
+    """fp32 matrix-core GEMM (v_mfma_f32_16x16x4_f32) against a float64 host
+    product; K = 96 leaves an odd number of 32-deep K-tiles."""
+    from cekirdekler_amd.ops.gemm import F32_TILES, GemmF32
+
+    M, N, K = shape
+    BM, BN = F32_TILES[tile][:2]
+    if M % BM or N % BN:
+        pytest.skip("shape not a multiple of the tile")
+    g = GemmF32(M, N, K, devices=_gpu()[0], tile=tile, group_m=2)
+    g.run(resident=False)
+    c = g.result(download=False)
+    ref = g.reference()
+    assert np.abs(c - ref).max() < 1e-4 * np.sqrt(K) * max(1.0, np.abs(ref).max())
