@@ -31,7 +31,7 @@ LIBRARY = {
                    "cek_mandelbrot_blk64_f32", "cek_mandelbrot_blk8_f32"],
     "nbody": ["cek_nbody_f32_b2", "cek_nbody_integrate_f32_b2", "cek_nbody_energy_f32_b2",
               "cek_nbody_f32_b4", "cek_nbody_integrate_f32_b4", "cek_nbody_energy_f32_b4"],
-    "reduce": ["cek_reduce_sum_f32", "cek_reduce_sum_f32_final"],
+    "reduce": ["cek_reduce_sum_f32", "cek_reduce_sum_f32_x32", "cek_reduce_sum_f32_final"],
     "stream": ["cek_saxpy_f32", "cek_copy_u8", "cek_vec_add_f32"],
 }
 
@@ -44,7 +44,7 @@ ARITY = {
     **{k: 3 for k in LIBRARY["mandelbrot"]},
     **{k: 4 for k in LIBRARY["nbody"] if "energy" not in k},
     **{k: 3 for k in LIBRARY["nbody"] if "energy" in k},
-    "cek_reduce_sum_f32": 2, "cek_reduce_sum_f32_final": 3,
+    "cek_reduce_sum_f32": 2, "cek_reduce_sum_f32_x32": 2, "cek_reduce_sum_f32_final": 3,
     "cek_saxpy_f32": 3, "cek_copy_u8": 2, "cek_vec_add_f32": 3,
 }
 

@@ -154,20 +154,22 @@ def test_mandelbrot_event_pipeline_matches_numpy(kernel):
     assert mism < 0.01, mism
 
 
-def test_reduce_sum():
+@pytest.mark.parametrize("kernel,per_item", [("cek_reduce_sum_f32", 8), ("cek_reduce_sum_f32_x32", 32)])
+def test_reduce_sum(kernel, per_item):
     from cekirdekler_amd.ops.library import library
 
-    cr = ck.ClNumberCruncher(_gpu()[0], "", prebuilt=library("reduce"))
-    n = 1 << 20
+    g = _gpu()[0]
+    cr = ck.ClNumberCruncher(g + g, "", prebuilt=library("reduce"))  # two slices, disjoint partials
+    n = 1 << 22
     x = ck.ClArray(np.random.rand(n).astype(np.float32))
-    x.elements_per_work_item = 8
+    x.elements_per_work_item = per_item
     x.write = False
-    groups = n // (256 * 8)
+    groups = n // (256 * per_item)
     part = ck.ClArray(groups, np.float32)
     part.read = False
     part.elements_per_group = 1
-    G = n // 8
-    x.next_param(part).compute(cr, 1, "cek_reduce_sum_f32", G, 256)
+    G = n // per_item
+    x.next_param(part).compute(cr, 1, kernel, G, 256)
     np.testing.assert_allclose(part.array.sum(), x.array.astype(np.float64).sum(), rtol=1e-5)
 
 
