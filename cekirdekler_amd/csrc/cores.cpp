@@ -69,7 +69,17 @@ void Cores::set_time_scale(int device, double scale) {
 void Cores::set_device_enabled(int device, bool on) {
   if (device < 0 || device >= static_cast<int>(enabled_.size())) throw Error("bad device index");
   if (!on && ex_) throw Error("devices cannot be disabled in a distributed job");
+  const bool rejoin = on && !enabled_[device];
   enabled_[device] = on;
+  // A re-enabled device has no range and no timing: restart every compute id
+  // from the equal split so that it rejoins with a real share instead of
+  // whatever a stale bench value would give it.
+  if (rejoin)
+    for (auto& kv : state_) {
+      std::fill(kv.second.ranges.begin(), kv.second.ranges.end(), 0LL);
+      std::fill(kv.second.bench.begin(), kv.second.bench.end(), 0.0);
+      for (auto& h : kv.second.history) std::fill(h.begin(), h.end(), 0.0);
+    }
 }
 
 void Cores::inject_failure(int device, int count) {
