@@ -114,10 +114,13 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
 
     if tile is None:
         # 256² tiles while every CU still gets one (balanced-DMA ping-pong,
-        # 1.35 PF at 8192³); 256×128 once a GPU's slice has fewer 256² tiles
-        # than CUs (8 GPUs × 1024 rows: 128 tiles) — even chunk-split DMA
-        # ping-pong with three stages, 0.95 PF at 1024×8192×8192
-        tile = "256x256pb" if (size // 256) ** 2 // ctx.world >= 256 else "256x128pe"
+        # ~1.45 PF at 8192³).  Once a GPU's slice has fewer 256² tiles than
+        # CUs (8 GPUs × 1024 rows: 128 tiles), the split-K = 2 kernel whose
+        # two K-splits exchange row halves through their XCD's L2 keeps every
+        # CU busy: 1.22 PF at 1024 rows vs 1.08 for the 256×128 tile on the
+        # same box (profiles/gemm_scaling_slices.md)
+        tile = "256x256pb" if (size // 256) ** 2 // ctx.world >= 256 else (
+            "256x256pby" if (size // 64) % 2 == 0 else "256x128pe")
     from cekirdekler_amd.ops.gemm import GEMM_LIBS
 
     cr = DistributedCruncher("", ctx=ctx, prebuilt=library(*GEMM_LIBS))
@@ -137,6 +140,9 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     host_steps = max(2, min(steps, 5))
     ms_host = timed(ctx, lambda: g.run(compute_id=2, resident=False), host_steps, 1)
     ranges = cr.ranges(1)
+    timeouts = g.spin_timeouts()
+    if timeouts:
+        raise RuntimeError(f"GEMM {tile}: {timeouts} work-groups timed out waiting for their K-split partner")
     cr.dispose()
     for a in (g.A, g.B, g.C, g.dims):
         a.dispose()  # release 0.5 GB of pinned host memory before the next config

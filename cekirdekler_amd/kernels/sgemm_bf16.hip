@@ -25,7 +25,7 @@
 
 namespace {
 
-template <int WM, int WN, int FM, int FN, int MODE, bool SK = false, bool NOSTORE = false>
+template <int WM, int WN, int FM, int FN, int MODE, bool SK = false, bool NOSTORE = false, int XCH = 0>
 __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
                                           const uint16_t* __restrict__ A,
                                           const uint16_t* __restrict__ Bt, float* __restrict__ C,
@@ -123,6 +123,14 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / BK / S;
+  unsigned my_xcc = 0;
+  if constexpr (XCH == 2) {
+    // publish this work-group's XCD for the partner split (flags[4t + 2 + s])
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(my_xcc));
+    my_xcc &= 15u;
+    if (tid == 0)
+      __hip_atomic_store(&tile_cnt[4 * t + 2 + (u & 1)], (int)my_xcc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if constexpr (MODE == 0) {
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -472,7 +480,82 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   }
 
   // Epilogue: acc[i][j][r] is C(row = wr·16FM + i·16 + fq·4 + r, col = wc·16FN + j·16 + fr)
-  if constexpr (SK) {
+  if constexpr (XCH > 0) {
+    // Split-K = 2 with exchanged halves (WM = 2): split s finishes row half
+    // s of the tile (waves wr == s) and hands its partial of the other half
+    // to the partner split.  Both work-groups of a tile end at about the
+    // same time, so the reduction tail is exposed; exchanging halves moves
+    // 128 KiB out + 128 KiB in + 128 KiB of C per CU instead of the 256 KiB
+    // ×3 of a last-arriver reduction.  Partials use a fragment-native layout
+    // (16 B per lane, 1 KiB per wave instruction).
+    static_assert(WM == 2, "exchanged halves need two wave rows");
+    const int s = (int)(u & 1);
+    constexpr int HALF = BM / 2 * BN;
+    f32x4* wh = reinterpret_cast<f32x4*>(W + (size_t)t * BM * BN + (size_t)wr * HALF);
+    if (wr != s) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) wh[((wc * FM + i) * FN + j) * 64 + lane] = acc[i][j];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* ok = reinterpret_cast<int*>(smem);
+    // XCH 1: flags[2t + h] = 1 once half h of tile t is in W (agent-scope
+    // release/acquire: an L2 write-back and invalidate per hand-over).
+    // XCH 2: flags[4t + h] plus each split's XCD in flags[4t + 2 + s]; two
+    // work-groups on one XCD share its L2, so the hand-over needs no L2
+    // write-back (the partial is in L2 once the stores are acknowledged, and
+    // no L1 holds those lines); across XCDs it falls back to XCH 1's fences.
+    // The partner has always stored (and published its XCD) before it waits,
+    // so neither side can wait on the other's wait; it is at most 8 dispatch
+    // slots away (XCD remap).  Every spin is bounded: a timeout counts in the
+    // last flag word (checked by the host) instead of hanging the GPU.
+    constexpr int FPT = XCH == 2 ? 4 : 2;  // flag words per tile
+    int* err = &tile_cnt[(size_t)FPT * ntm * ntn];
+    auto spin = [&](int* w) -> int {
+      int v, spins = 0;
+      while ((v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1 << 21)) {
+          __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return 0;
+        }
+      }
+      return v;
+    };
+    if (tid == 0) {
+      bool same = false;
+      int good = 1;
+      if constexpr (XCH == 2) {
+        const int px = spin(&tile_cnt[4 * t + 2 + (1 - s)]);
+        tile_cnt[4 * t + 2 + (1 - s)] = 0;  // re-arm the partner's word
+        same = px == (int)my_xcc + 1;
+        good = px != 0;
+      }
+      if (!same) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(&tile_cnt[FPT * t + (1 - s)], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (good) good = spin(&tile_cnt[FPT * t + s]) != 0;
+      tile_cnt[FPT * t + s] = 0;  // re-arm for the next call
+      ok[0] = good;
+      ok[1] = same;
+    }
+    __syncthreads();
+    if (wr != s) return;
+    if (!ok[1]) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (ok[0]) {
+      const f32x4* rh = reinterpret_cast<const f32x4*>(W + (size_t)t * BM * BN + (size_t)s * HALF);
+      f32x4 part[FM][FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) part[i][j] = rh[((wc * FM + i) * FN + j) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] += part[i][j];
+    }
+  } else if constexpr (SK) {
     if (S > 1) {
       // Every split stores its partial tile; the last of the S to arrive
       // (device-scope counter) adds the others' partials to its own and
@@ -564,6 +647,20 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sk(
     const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
   __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
   gemm_tile<2, 4, 8, 4, 4, true>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
+}
+
+// balanced-DMA split-K = 2 with exchanged row halves (flags: 2 per tile + 1)
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sx(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
+  gemm_tile<2, 4, 8, 4, 4, true, false, 1>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
+}
+// same, with the hand-over through a shared L2 when both splits of a tile run
+// on one XCD (flags: 4 per tile + 1)
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sy(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
+  gemm_tile<2, 4, 8, 4, 4, true, false, 2>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
 }
 
 #define CEK_GEMM_B3_KERNEL(NAME, WM, WN, FM, FN, MODE)                                              \

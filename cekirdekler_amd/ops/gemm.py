@@ -39,6 +39,10 @@ TILES = {
     "256x256pc": (256, 256, 512, "cek_sgemm_bf16_256x256pc"),  # same, LDS reads before the DMA
     "256x128pc": (256, 128, 512, "cek_sgemm_bf16_256x128pc"),
     "256x128pe": (256, 128, 512, "cek_sgemm_bf16_256x128pe"),  # even chunk-split DMA, 3 stages
+    # balanced-DMA, split-K = 2 with exchanged row halves (always two K-splits)
+    "256x256pbx": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sx"),
+    # same, hand-over through the shared L2 when both splits run on one XCD
+    "256x256pby": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sy"),
     # probe only: 256x256pp without the C store (epilogue share)
     "256x256pp_nostore": (256, 256, 512, "cek_sgemm_bf16_256x256pp_nostore"),
     # ping-pong with a 4-deep BK=32 LDS ring (kernels/sgemm_pp32_bf16.hip)
@@ -68,6 +72,8 @@ F32_TILES = {
 
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
 SPLIT_K_TILES = {"256x256pp", "256x128pp", "256x256pb"}
+# tiles whose kernel always runs two K-splits that exchange row halves
+EXCHANGE_TILES = {"256x256pbx": 2, "256x256pby": 4}  # flag words per tile
 
 
 def to_bf16_bits(x: np.ndarray) -> np.ndarray:
@@ -115,6 +121,11 @@ class GemmBf16:
             if (K // 64) % split_k:
                 raise ValueError(f"K/64 ({K // 64}) must be divisible by split_k ({split_k})")
             kname = kname + "_sk"
+        self.exchange = tile in EXCHANGE_TILES
+        if self.exchange:
+            if (K // 64) % 2:
+                raise ValueError(f"K/64 ({K // 64}) must be even for tile {tile}")
+            split_k = 2
         self.M, self.N, self.K, self.BM, self.BN, self.L, self.kernel = M, N, K, BM, BN, L, kname
         self.split_k = max(1, int(split_k))
         self.tiles = (M // BM) * (N // BN)
@@ -134,9 +145,13 @@ class GemmBf16:
         if self.split_k > 1:
             # per-work-group partial tiles (device-only scratch: never transferred;
             # np.empty leaves the host pages untouched) and per-tile arrival counters
-            self.W = ClArray(np.empty(self.tiles * self.split_k * BM * BN, np.float32))
+            # (exchange tiles: one tile of partial halves per tile, two ready
+            # flags per tile and a spin-timeout counter at the end)
+            wtiles = self.tiles if self.exchange else self.tiles * self.split_k
+            self.W = ClArray(np.empty(wtiles * BM * BN, np.float32))
             self.W.read = self.W.write = False
-            self.counters = ClArray(np.zeros(self.tiles, np.int32))
+            nflags = EXCHANGE_TILES[tile] * self.tiles + 1 if self.exchange else self.tiles
+            self.counters = ClArray(np.zeros(nflags, np.int32))
             self.counters.write = False
             self.extra = [self.W, self.counters]
         if fill == "random":
@@ -198,6 +213,17 @@ class GemmBf16:
                 lo, n = refs[g] * e, rng[g] * e
                 self._download_slice(dev, lo, n)
         return untile(self.C.array, self.M, self.N, self.BM, self.BN, self.group_m)
+
+    def spin_timeouts(self) -> int:
+        """Exchange tiles only: how many work-groups gave up waiting for their
+        partner's half (summed over devices; nonzero means a wrong result)."""
+        if not self.exchange:
+            return 0
+        total = 0
+        for dev in range(self.cr._cores.num_devices):
+            self.cr.download(self.counters, dev)
+            total += int(self.counters.array[-1])
+        return total
 
     def _download_slice(self, dev: int, lo: int, n: int) -> None:
         # a sub-view ClArray sharing the same uid would alias buffers; the

@@ -111,6 +111,30 @@ def test_gemm_split_k(tile, split):
     cr.dispose()
 
 
+@pytest.mark.parametrize("tile", ["256x256pbx", "256x256pby"])
+def test_gemm_split_k_exchanged_halves(tile):
+    """Split-K = 2 with exchanged row halves: each split finishes one half
+    of the tile; flags re-armed across calls (4 calls), no spin timeouts, the
+    pair of K-splits kept on one device (two logical devices, one slower)."""
+    from cekirdekler_amd.ops.gemm import GemmBf16
+    from cekirdekler_amd.ops.library import library
+
+    g0 = _gpu()[0]
+    cr = ck.ClNumberCruncher(g0 + g0, "", prebuilt=library("sgemm_bf16"))
+    cr.set_time_scale(1, 2.0)
+    g = GemmBf16(1024, 768, 1024, cruncher=cr, tile=tile, group_m=2)
+    assert g.split_k == 2
+    ref = g.reference()
+    for _ in range(4):
+        g.run(resident=False)
+        c = g.result(download=False)
+        err = np.abs(c - ref).max()
+        assert err < 5e-3 * np.abs(ref).max(), err
+    assert g.spin_timeouts() == 0
+    assert all(r % (2 * g.L) == 0 for r in cr.ranges(1)) and sum(cr.ranges(1)) == g.global_range
+    cr.dispose()
+
+
 def test_gemm_two_logical_devices_balanced():
     from cekirdekler_amd.ops.gemm import GemmBf16
 
