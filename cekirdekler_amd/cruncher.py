@@ -285,6 +285,14 @@ class ClNumberCruncher:
     def benchmarks(self, compute_id: int) -> List[float]:
         return list(self._cores.benchmarks(compute_id))
 
+    def performance_history(self, compute_id: int) -> List[List[float]]:
+        """The balancer's moving-average window for ``compute_id``: 10 rows
+        (oldest first) of normalized per-device throughputs (≙
+        ``Cores.performanceHistory``, reference src/Cores.cs:1075)."""
+        return [list(h) for h in self._cores.history(compute_id)]
+
+    performanceHistory = performance_history
+
     def normalized_compute_powers_of_devices(self, compute_id: Optional[int] = None):
         c = self._cores
         cid = c.last_compute_id if compute_id is None else compute_id
@@ -530,6 +538,11 @@ class Cores:
 
     def benchmarks(self, compute_id: int):
         return self.cruncher.benchmarks(compute_id)
+
+    def performance_history(self, compute_id: int):
+        return self.cruncher.performance_history(compute_id)
+
+    performanceHistory = performance_history
 
     def global_ranges(self, compute_id: int):
         return self.cruncher.ranges(compute_id)

@@ -153,6 +153,9 @@ def test_load_balancer_with_injected_imbalance(cpu):
     r = cr.ranges(9)
     assert r[0] > r[1] * 1.5
     assert cr.normalized_global_ranges_of_devices(9)[0] > 0.55
+    hist = cr.performance_history(9)     # 10-deep window, rows sum to 1 once filled
+    assert len(hist) == 10 and all(len(h) == 2 for h in hist)
+    assert abs(sum(hist[-1]) - 1.0) < 1e-6 and hist[-1][0] > hist[-1][1]
 
 
 def test_kernel_arity_mismatch_is_rejected(cr):
