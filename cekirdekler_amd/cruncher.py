@@ -359,6 +359,24 @@ class ClNumberCruncher:
 
     lastComputePerformanceReport = last_compute_performance_report
 
+    # ------------------------------------------------------------ device timeline
+    @property
+    def record_timeline(self) -> bool:
+        return bool(self._cores.record_timeline) if self._cores else False
+
+    @record_timeline.setter
+    def record_timeline(self, on: bool) -> None:
+        self._cores.record_timeline = bool(on)
+
+    def timeline(self) -> List[dict]:
+        """Kernel spans recorded while ``record_timeline`` was on: one dict per
+        compute per device (``device``, ``compute_id``, ``begin_ms``,
+        ``end_ms``), timed by hipEvents on the stream the kernels ran on and
+        relative to that device's first span.  Waits for the recorded work and
+        clears the list."""
+        return [{"device": d, "compute_id": cid, "begin_ms": b, "end_ms": e}
+                for d, cid, b, e in self._cores.timeline()]
+
     def last_record(self) -> dict:
         """Structured record of the last compute (observability)."""
         r = self._cores.last_record()

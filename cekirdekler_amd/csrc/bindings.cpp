@@ -284,6 +284,18 @@ PYBIND11_MODULE(_cek, m) {
       .def("compute_ids", &Cores::compute_ids)
       .def_property_readonly("last_compute_id", &Cores::last_compute_id)
       .def("last_record", &Cores::last_record)
+      .def_readwrite("record_timeline", &Cores::record_timeline)
+      .def("timeline",
+           [](Cores& c) {
+             std::vector<std::tuple<int, int, double, double>> out;
+             std::vector<Cores::TimelineSpan> spans;
+             {
+               py::gil_scoped_release nogil;
+               spans = c.timeline();
+             }
+             for (auto& s : spans) out.emplace_back(s.device, s.compute_id, s.begin_ms, s.end_ms);
+             return out;
+           })
       .def("markers_reached", &Cores::markers_reached)
       .def("markers_issued", &Cores::markers_issued)
       .def("last_marker", &Cores::last_marker)

@@ -383,6 +383,64 @@ void Cores::gate(UserEvent& ev, int device) {
 
 void Cores::launch_kernels(Worker& wk, hipStream_t s, const ComputeCall& c, long long ref,
                            long long range) {
+  if (!record_timeline || no_compute) {
+    launch_kernels_body(wk, s, c, ref, range);
+    return;
+  }
+  int dev = 0;
+  while (dev < num_devices() && workers_[dev].get() != &wk) ++dev;
+  PendingSpan sp{dev, c.compute_id, nullptr, nullptr, 0, 0};
+  if (wk.gpu()) {
+    CEK_HIP(hipEventCreate(&sp.begin));
+    CEK_HIP(hipEventCreate(&sp.end));
+    CEK_HIP(hipEventRecord(sp.begin, s));
+    launch_kernels_body(wk, s, c, ref, range);
+    CEK_HIP(hipEventRecord(sp.end, s));
+  } else {
+    sp.host_begin = now_ms();
+    launch_kernels_body(wk, s, c, ref, range);
+    sp.host_end = now_ms();
+  }
+  std::lock_guard<std::mutex> g(tl_mu_);
+  pending_spans_.push_back(sp);
+}
+
+std::vector<Cores::TimelineSpan> Cores::timeline() {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
+  std::vector<PendingSpan> spans;
+  {
+    std::lock_guard<std::mutex> g(tl_mu_);
+    spans.swap(pending_spans_);
+  }
+  std::vector<TimelineSpan> out;
+  std::map<int, PendingSpan> epoch;  // first span per device
+  for (auto& sp : spans) epoch.emplace(sp.device, sp);
+  for (auto& sp : spans) {
+    const PendingSpan& e0 = epoch.at(sp.device);
+    TimelineSpan t{sp.device, sp.compute_id, 0, 0};
+    if (sp.begin) {
+      CEK_HIP(hipEventSynchronize(sp.end));
+      float b = 0, e = 0;
+      CEK_HIP(hipEventElapsedTime(&b, e0.begin, sp.begin));
+      CEK_HIP(hipEventElapsedTime(&e, e0.begin, sp.end));
+      t.begin_ms = b;
+      t.end_ms = e;
+    } else {
+      t.begin_ms = sp.host_begin - e0.host_begin;
+      t.end_ms = sp.host_end - e0.host_begin;
+    }
+    out.push_back(t);
+  }
+  for (auto& sp : spans)
+    if (sp.begin) {
+      (void)hipEventDestroy(sp.begin);
+      (void)hipEventDestroy(sp.end);
+    }
+  return out;
+}
+
+void Cores::launch_kernels_body(Worker& wk, hipStream_t s, const ComputeCall& c, long long ref,
+                                long long range) {
   if (no_compute) return;
   const int reps = std::max(1, c.repeats);
   auto body = [&](hipStream_t st) {

@@ -192,6 +192,18 @@ class Cores {
   }
   int failovers() const { return failovers_; }
   void set_dynamic_lds(unsigned bytes);
+  // ---- device timeline ----
+  // With record_timeline on, the kernels of every compute are bracketed by
+  // timing hipEvents on the stream they run on (host clock on the CPU
+  // device).  timeline() waits for the recorded work and returns
+  // (device, compute id, begin ms, end ms) per span, relative to the first
+  // span of that device, then clears the list.
+  struct TimelineSpan {
+    int device, compute_id;
+    double begin_ms, end_ms;
+  };
+  bool record_timeline = false;
+  std::vector<TimelineSpan> timeline();
 
   // ---- state ----
   bool has_state(int id) const { return state_.count(id) > 0; }
@@ -244,6 +256,15 @@ class Cores {
                            long long range, uint64_t* h2d, uint64_t* d2h);
   void launch_kernels(Worker& wk, hipStream_t s, const ComputeCall& c, long long ref,
                       long long range);
+  void launch_kernels_body(Worker& wk, hipStream_t s, const ComputeCall& c, long long ref,
+                           long long range);
+  struct PendingSpan {
+    int device, compute_id;
+    hipEvent_t begin, end;      // GPU: timing events (device epoch: first span's begin)
+    double host_begin, host_end;  // CPU device: host clock
+  };
+  std::mutex tl_mu_;
+  std::vector<PendingSpan> pending_spans_;
   void full_reads(Worker& wk, hipStream_t s, const ComputeCall& c, uint64_t* h2d);
 
   std::vector<std::unique_ptr<Worker>> workers_;

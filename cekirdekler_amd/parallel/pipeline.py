@@ -322,6 +322,34 @@ class DevicePipelineStage:
     bindArray = bind_array
 
 
+def _coverage(intervals):
+    """(time covered by ≥1 interval, time covered by ≥2 intervals)."""
+    ev = sorted([(b, 1) for b, _ in intervals] + [(e, -1) for _, e in intervals])
+    busy = multi = 0.0
+    depth, last = 0, None
+    for t, d in ev:
+        if last is not None:
+            if depth >= 1:
+                busy += t - last
+            if depth >= 2:
+                multi += t - last
+        depth += d
+        last = t
+    return busy, multi
+
+
+def _intersection(b, e, intervals) -> float:
+    """Length of [b, e) covered by the union of ``intervals``."""
+    cut = sorted((max(b, x), min(e, y)) for x, y in intervals if min(e, y) > max(b, x))
+    total, end = 0.0, b
+    for x, y in cut:
+        x = max(x, end)
+        if y > x:
+            total += y - x
+            end = y
+    return total
+
+
 class DevicePipeline:
     """N stages on one device, overlapped on separate HIP streams."""
 
@@ -351,9 +379,46 @@ class DevicePipeline:
     enableSerialMode = enable_serial_mode
     enableParallelMode = enable_parallel_mode
 
+    # Timeline queries (declared but not implemented in the reference,
+    # ClPipeline.cs:2391-2399): every feed with ``record_timeline`` on leaves
+    # one hipEvent-timed kernel span per stage (compute id 100 + stage).
     @property
-    def query_timeline_overlap_percentage(self):
-        raise NotImplementedError("not implemented in the reference either (ClPipeline.cs:2391)")
+    def record_timeline(self) -> bool:
+        return self.cruncher.record_timeline
+
+    @record_timeline.setter
+    def record_timeline(self, on: bool) -> None:
+        self.cruncher.record_timeline = on
+        self._spans = []
+
+    def _collect(self) -> List[tuple]:
+        spans = getattr(self, "_spans", [])
+        spans += [(t["compute_id"] - 100, t["begin_ms"], t["end_ms"]) for t in self.cruncher.timeline()]
+        self._spans = spans
+        return spans
+
+    def query_timeline_overlap_percentage(self) -> float:
+        """Share (%) of the recorded busy time during which two or more stages
+        ran at once (0 for a fully serial pipeline)."""
+        spans = self._collect()
+        busy, multi = _coverage([(b, e) for _, b, e in spans])
+        return 100.0 * multi / busy if busy > 0 else 0.0
+
+    def stages_overlapping_percentages(self) -> List[float]:
+        """Per stage: share (%) of its own kernel time that overlapped any
+        other stage's kernels."""
+        spans = self._collect()
+        out = []
+        for i in range(len(self.stages)):
+            mine = [(b, e) for st, b, e in spans if st == i]
+            others = [(b, e) for st, b, e in spans if st != i]
+            own = sum(e - b for b, e in mine)
+            shared = sum(_intersection(b, e, others) for b, e in mine)
+            out.append(100.0 * shared / own if own > 0 else 0.0)
+        return out
+
+    queryTimelineOverlapPercentage = query_timeline_overlap_percentage
+    stagesOverlappingPercentages = stages_overlapping_percentages
 
     def _args(self, st: DevicePipelineStage) -> ClParameterGroup:
         p = self._parity

@@ -179,6 +179,41 @@ def test_device_pipeline_gpu(gpu):
     dp.dispose()
 
 
+def test_device_pipeline_timeline_overlap_gpu(gpu):
+    """Parallel mode puts each stage on its own HIP stream: with two small,
+    long-running kernels the hipEvent timeline shows the stages overlapping;
+    serial mode shows none."""
+    from cekirdekler_amd.parallel.pipeline import (DevicePipeline, DevicePipelineArray,
+                                                   DevicePipelineArrayType, DevicePipelineStage)
+
+    N = 1 << 14  # 64 work-groups per stage: both fit on the GPU at once
+    body = "float v = x[i]; for (int j = 0; j < 200000; ++j) v = v * 0.9999f + 0.5f;"
+    src = ("__global__ void s0(const float* x, float* y) { long long i = get_global_id(0); " + body + " y[i] = v; }\n"
+           "__global__ void s1(const float* x, float* y) { long long i = get_global_id(0); " + body + " y[i] = v; }")
+    dp = DevicePipeline(gpu[0], src)
+    arrs = [DevicePipelineArray(DevicePipelineArrayType.INPUT, np.ones(N, np.float32)) for _ in range(2)]
+    outs = [DevicePipelineArray(DevicePipelineArrayType.OUTPUT, np.zeros(N, np.float32)) for _ in range(2)]
+    for k in range(2):
+        st = DevicePipelineStage(f"s{k}", N, 256)
+        st.bind_array(arrs[k])
+        st.bind_array(outs[k])
+        dp.add_stage(st)
+    dp.feed()  # warm-up (compiles, allocates)
+    dp.record_timeline = True
+    for _ in range(3):
+        dp.feed()
+    par = dp.query_timeline_overlap_percentage()
+    per_stage = dp.stages_overlapping_percentages()
+    dp.enable_serial_mode()
+    dp.record_timeline = True
+    for _ in range(3):
+        dp.feed()
+    ser = dp.query_timeline_overlap_percentage()
+    dp.dispose()
+    assert par > 30.0 and min(per_stage) > 30.0, (par, per_stage)
+    assert ser < 5.0, ser
+
+
 def test_task_pool_gpu(gpu):
     from cekirdekler_amd.parallel.pool import ClDevicePool, ClDevicePoolType, ClTaskPool
 

@@ -91,3 +91,42 @@ def test_multi_device_stage_sees_hidden_constants():
             seen.append(float(res[0]))
     assert seen == [3.0 * p - 3.0 for p in range(len(seen))] and len(seen) == 8 - 4
     pipe.dispose()
+
+
+def test_timeline_coverage_helpers():
+    from cekirdekler_amd.parallel.pipeline import _coverage, _intersection
+
+    busy, multi = _coverage([(0, 4), (2, 6), (10, 11)])
+    assert busy == 7 and multi == 2
+    assert _intersection(0, 10, [(2, 3), (2.5, 5), (8, 20)]) == 5
+
+
+def test_device_pipeline_timeline_on_cpu():
+    """Serial mode runs the stages one after another: spans are recorded per
+    stage and no two stages overlap."""
+    cpu = ck.ClPlatforms.all().cpus(True)
+    N = 1 << 12
+    src = ("__global__ void add1(const float* x, float* y) { long long i = get_global_id(0); y[i] = x[i] + 1.0f; }\n"
+           "__global__ void sub3(const float* z, float* w) { long long i = get_global_id(0); w[i] = z[i] - 3.0f; }")
+    dp = DevicePipeline(cpu, src)
+    inp = DevicePipelineArray(DevicePipelineArrayType.INPUT, np.zeros(N, np.float32))
+    mid = DevicePipelineArray(DevicePipelineArrayType.TRANSITION, np.zeros(N, np.float32))
+    out = DevicePipelineArray(DevicePipelineArrayType.OUTPUT, np.zeros(N, np.float32))
+    a = DevicePipelineStage("add1", N, 256)
+    a.bind_array(inp)
+    a.bind_array(mid)
+    b = DevicePipelineStage("sub3", N, 256)
+    b.bind_array(mid)
+    b.bind_array(out)
+    dp.add_stage(a)
+    dp.add_stage(b)
+    dp.enable_serial_mode()
+    dp.record_timeline = True
+    for _ in range(4):
+        dp.feed()
+    spans = dp._collect()
+    assert sorted({st for st, _, _ in spans}) == [0, 1] and len(spans) == 8
+    assert all(e >= b for _, b, e in spans)
+    assert dp.query_timeline_overlap_percentage() == 0.0
+    assert dp.stages_overlapping_percentages() == [0.0, 0.0]
+    dp.dispose()
