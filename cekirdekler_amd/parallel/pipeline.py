@@ -300,6 +300,11 @@ class DevicePipelineArray:
     def __init__(self, type_: DevicePipelineArrayType, array):
         self.type = DevicePipelineArrayType(type_)
         self.array = as_clarray(array)
+        if self.type != DevicePipelineArrayType.INTERNAL:
+            # Double buffers live in pinned memory: a copy from or to pageable
+            # memory would block the host until the stream drains, and stage
+            # k+1 could not be enqueued while stage k runs.
+            self.array.fast_arr = True
         self.dup = _clone(self.array) if self.type != DevicePipelineArrayType.INTERNAL else None
         self.stages: List["DevicePipelineStage"] = []
 

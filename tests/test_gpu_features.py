@@ -198,7 +198,8 @@ def test_device_pipeline_timeline_overlap_gpu(gpu):
         st.bind_array(arrs[k])
         st.bind_array(outs[k])
         dp.add_stage(st)
-    dp.feed()  # warm-up (compiles, allocates)
+    for _ in range(18):  # warm-up: both buffer parities and the first use of all 16 compute streams
+        dp.feed()
     dp.record_timeline = True
     for _ in range(3):
         dp.feed()
@@ -210,10 +211,9 @@ def test_device_pipeline_timeline_overlap_gpu(gpu):
         dp.feed()
     ser = dp.query_timeline_overlap_percentage()
     dp.dispose()
-    # measured on MI355X: ~15 % of the busy time with both stages running,
-    # 24-29 % of each stage's kernel time (the second stage starts late in
-    # the first one's span); serial mode: none
-    assert par > 5.0 and min(per_stage) > 5.0, (par, per_stage)
+    # steady state on MI355X: the second stage starts ~0.25 ms into the
+    # first one's 0.41 ms span (tools/timeline_probe.py); serial mode: none
+    assert par > 10.0 and min(per_stage) > 10.0, (par, per_stage)
     assert ser < 1.0, ser
 
 
