@@ -1,63 +1,42 @@
-#!/usr/bin/env python3
-"""Per-compute() host overhead on one GPU: a trivial kernel over resident
-arrays (no transfers), timed at three layers — torch launch+sync (floor),
-the native Cores::compute with a prebuilt ComputeCall, and the public
-ClArray.compute() path.  Prints one JSON line per layer."""
+"""GPU probe: host time per compute() for a tiny kernel, by transfer kind
+and mode (enqueue mode = no host sync per call)."""
 import json
+import os
 import sys
 import time
 
-import numpy as np
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
 
-sys.path.insert(0, ".")
 import cekirdekler_amd as ck  # noqa: E402
-from cekirdekler_amd import cek  # noqa: E402
 
-SRC = "__global__ void inc(float* x) { x[get_global_id(0)] += 1.0f; }"
-N = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-ITERS = 2000
-
-
-def bench(fn, iters=ITERS):
-    for _ in range(50):
-        fn()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        fn()
-    torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / iters * 1e6
-
-
-x_t = torch.zeros(N, device="cuda")
-
-
-def torch_step():
-    x_t.add_(1.0)
-    torch.cuda.synchronize()
-
-
-print(json.dumps({"layer": "torch add_+synchronize", "us": round(bench(torch_step), 2)}))
-
-for devs_name in ("gpu0", "gpu0+gpu0"):
-    g = ck.ClPlatforms.all().gpus()
-    devs = g[0] if devs_name == "gpu0" else g[0] + g[0]
-    cr = ck.ClNumberCruncher(devs, SRC)
-    x = ck.ClArray(np.zeros(N, np.float32))
-    x.compute(cr, 1, "inc", N, 256)
-    x.read = False
-    x.write = False
-    call = cek.ComputeCall()
-    call.kernels = ["inc"]
-    call.arrays = [x._spec()]
-    call.global_range = N
-    call.local_range = 256
-    call.compute_id = 1
-    us_native = bench(lambda: cr._cores.compute(call))
-    us_api = bench(lambda: x.compute(cr, 1, "inc", N, 256))
-    rec = cr.last_record()
-    print(json.dumps({"layer": "native Cores.compute", "devices": devs_name, "us": round(us_native, 2)}))
-    print(json.dumps({"layer": "ClArray.compute", "devices": devs_name, "us": round(us_api, 2),
-                      "wall_ms_record": rec["wall_ms"], "device_ms": rec["device_ms"]}))
-    cr.dispose()
+N = 1 << 14
+src = "__global__ void k(const float* x, float* y) { long long i = get_global_id(0); y[i] = x[i] + 1.0f; }"
+gpu = ck.ClPlatforms.all().gpus()
+cr = ck.ClNumberCruncher(gpu[0], src)
+out = {}
+for pinned in (True, False):
+    for kind in ("none", "h2d", "d2h", "both"):
+        for enq in (False, True):
+            x = ck.ClArray(N, np.float32) if pinned else ck.ClArray(np.zeros(N, np.float32))
+            y = ck.ClArray(N, np.float32) if pinned else ck.ClArray(np.zeros(N, np.float32))
+            x.read = kind in ("h2d", "both")
+            x.write = False
+            y.read = False
+            y.write = kind in ("d2h", "both")
+            g = x.next_param(y)
+            for _ in range(20):
+                g.compute(cr, 5, "k", N, 256)
+            cr.enqueue_mode = enq
+            t = time.perf_counter()
+            for _ in range(200):
+                g.compute(cr, 5, "k", N, 256)
+            host = (time.perf_counter() - t) * 1e3 / 200
+            cr.enqueue_mode = False
+            total = (time.perf_counter() - t) * 1e3 / 200
+            out[f"{'pinned' if pinned else 'pageable'}/{kind}/{'enqueue' if enq else 'sync'}"] = {
+                "host_us_per_call": round(1e3 * host, 1), "total_us_per_call": round(1e3 * total, 1)}
+            x.dispose()
+            y.dispose()
+print(json.dumps(out, indent=1))
+cr.dispose()
