@@ -273,6 +273,7 @@ PYBIND11_MODULE(_cek, m) {
       .def("gate", &Cores::gate, py::arg("event"), py::arg("device") = -1)
       .def_readwrite("dist_gather_writes", &Cores::dist_gather_writes)
       .def_readwrite("dist_broadcast_reads", &Cores::dist_broadcast_reads)
+      .def_readwrite("dist_split_reads", &Cores::dist_split_reads)
       .def("set_time_scale", &Cores::set_time_scale)
       .def("set_dynamic_lds", &Cores::set_dynamic_lds)
       .def("has_state", &Cores::has_state)

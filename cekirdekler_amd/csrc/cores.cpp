@@ -472,7 +472,23 @@ void Cores::full_reads(Worker& wk, hipStream_t s, const ComputeCall& c, uint64_t
   const bool dist = comm_ && dist_broadcast_reads;
   for (auto& a : c.arrays) {
     if (a.zc || a.partial || !a.read) continue;
-    if (dist) {
+    if (comm_ && dist_split_reads) {
+      // Split upload + all-gather (every rank's host copy holds the same
+      // data): rank g copies chunk g of the array over its own PCIe link,
+      // then one RCCL ring all-gather over xGMI completes every replica.
+      // Each link carries 1/N of the array instead of all of it.
+      const int W = global_devices_;
+      uint64_t chunk = (a.bytes + W - 1) / W;
+      chunk = (chunk + a.elem_size - 1) / a.elem_size * a.elem_size;
+      std::vector<uint64_t> offs(W), sizes(W);
+      for (int g = 0; g < W; ++g) {
+        offs[g] = std::min<uint64_t>(g * chunk, a.bytes);
+        sizes[g] = std::min<uint64_t>(chunk, a.bytes - offs[g]);
+      }
+      wk.h2d(s, a, offs[global_base_] / a.elem_size, sizes[global_base_] / a.elem_size);
+      *h2d += sizes[global_base_];
+      comm_->allgatherv(wk.buffer(a), offs, sizes, s);
+    } else if (dist) {
       if (global_base_ == 0) {
         wk.h2d(s, a, 0, a.bytes / a.elem_size);
         *h2d += a.bytes;
@@ -743,7 +759,7 @@ void Cores::run_device_body(int w, const ComputeCall& c, long long ref, long lon
       run_event_pipeline(wk, gidx, c, ref, range, h2d, d2h);
     else
       run_driver_pipeline(wk, gidx, c, ref, range, h2d, d2h);
-  } else if (comm_ && (dist_gather_writes || dist_broadcast_reads)) {
+  } else if (comm_ && (dist_gather_writes || dist_broadcast_reads || dist_split_reads)) {
     // still take part in the collectives
     run_3phase(wk, gidx, c, ref, 0, h2d, d2h);
   }
@@ -860,14 +876,15 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
   bool pipelined = pipe_req && c.repeats <= 1 && !enqueue_mode_ && !hazard;
   for (int i = 0; i < D && pipelined; ++i)
     if (st.ranges[i] != 0 && (st.ranges[i] % (B * U) != 0 || st.ranges[i] < B * U)) pipelined = false;
-  if (comm_ && (dist_gather_writes || dist_broadcast_reads)) pipelined = false;
+  if (comm_ && (dist_gather_writes || dist_broadcast_reads || dist_split_reads)) pipelined = false;
 
   std::vector<double> ms(nloc, 0.0);
   std::vector<uint64_t> h2d(nloc, 0), d2h(nloc, 0);
   DeviceFailure failure;
   int participants = 0;
   for (int w = 0; w < nloc; ++w)
-    if (st.ranges[global_base_ + w] > 0 || (comm_ && (dist_gather_writes || dist_broadcast_reads))) ++participants;
+    if (st.ranges[global_base_ + w] > 0 || (comm_ && (dist_gather_writes || dist_broadcast_reads || dist_split_reads)))
+      ++participants;
   PhaseBarrier phase(participants);
   if (hazard && !enqueue_mode_ && participants > 1) phase_ = &phase;
   struct ResetPhase {

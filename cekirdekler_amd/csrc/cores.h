@@ -240,6 +240,8 @@ class Cores {
                        int global_devices, int global_base);
   bool dist_gather_writes = false;
   bool dist_broadcast_reads = false;
+  // identical host copies on every rank: each uploads 1/N, RCCL all-gathers
+  bool dist_split_reads = false;
   int global_base() const { return global_base_; }
 
  private:

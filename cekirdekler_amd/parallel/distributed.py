@@ -12,8 +12,8 @@ MI355X node the idiomatic layout is one process per GPU (torchrun /
   ``torch.distributed`` for multi-node jobs — every rank then computes the
   identical next split, so no split is ever communicated;
 * an optional native RCCL communicator (xGMI) for the data plane:
-  ``broadcast_reads`` (rank 0 uploads ``read`` arrays, RCCL broadcasts them)
-  and ``gather_writes`` (written slices all-gathered into every rank's device
+  ``broadcast_reads`` (rank 0 uploads ``read`` arrays, RCCL broadcasts them),
+  ``split_reads`` (each rank uploads 1/N, RCCL all-gathers) and ``gather_writes`` (written slices all-gathered into every rank's device
   replica — the "keep resident" iterative mode of SURVEY §5.8 item 5).
 """
 from __future__ import annotations
@@ -179,6 +179,21 @@ class DistributedCruncher(ClNumberCruncher):
         if v and self._comm is None and self.ctx.is_distributed:
             raise RuntimeError("broadcast_reads needs DistributedCruncher(comm=True)")
         self._cores.dist_broadcast_reads = bool(v)
+
+    @property
+    def split_reads(self) -> bool:
+        """Full ``read`` arrays are uploaded 1/N per rank (each over its own
+        PCIe link) and completed by one RCCL all-gather over xGMI.  Requires
+        identical host copies on every rank (e.g. inputs generated from the
+        same seed); ``broadcast_reads`` is the variant where only rank 0's
+        host copy counts."""
+        return self._cores.dist_split_reads
+
+    @split_reads.setter
+    def split_reads(self, v: bool) -> None:
+        if v and self._comm is None and self.ctx.is_distributed:
+            raise RuntimeError("split_reads needs DistributedCruncher(comm=True)")
+        self._cores.dist_split_reads = bool(v)
 
     def _build_call(self, *args, **kwargs):
         call = super()._build_call(*args, **kwargs)

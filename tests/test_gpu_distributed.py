@@ -113,6 +113,20 @@ def test_rccl_data_plane_one_rank():
     np.testing.assert_allclose(y.array, np.arange(n, dtype=np.float32) * 3 + 1)
     cr.dispose()
 
+    # split upload + all-gather of full reads (one rank: the whole array is
+    # its chunk; the all-gather is the identity)
+    cr = DistributedCruncher(src, ctx=DistContext(), devices=gpu, comm=True)
+    cr.split_reads = True
+    a = ck.ClArray(np.arange(n + 3 * 64, dtype=np.float32))  # odd size: uneven chunks at N ranks
+    a.write = False
+    y = ck.ClArray(np.zeros(n, np.float32))
+    y.read = False
+    for _ in range(2):
+        a.next_param(y).compute(cr, 2, "k", n, 256)
+    np.testing.assert_allclose(y.array, np.arange(n, dtype=np.float32) * 3 + 1)
+    assert cr.last_record()["h2d_bytes"] == a.array.nbytes
+    cr.dispose()
+
     comm = cek.Comm(cek.Comm.unique_id(), 0, 1, gpu.device(0).info.ordinal)
     t = torch.arange(1024, dtype=torch.float32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
