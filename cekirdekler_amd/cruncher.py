@@ -133,8 +133,9 @@ class ClNumberCruncher:
         self.kernel_source = kernel_source or ""
         if "enqueue_kernel" in self.kernel_source:
             raise NotImplementedError(
-                "device-side enqueue (OpenCL 2.0 enqueue_kernel) has no HIP equivalent; "
-                "launch follow-up kernels from the host (compute() with several kernel names)")
+                "OpenCL 2.0 enqueue_kernel (blocks) has no HIP equivalent; use cek_enqueue(child, n, param) "
+                "with `__cek_child__ void child(long long id, long long param, <parent's params>)` "
+                "(GPU-resident child levels, see ClNumberCruncher.device_enqueue_errors)")
         cfg = cek.CoresConfig()
         cfg.queue_concurrency = int(queue_concurrency)
         cfg.no_pipelining = bool(no_pipelining)
@@ -358,6 +359,22 @@ class ClNumberCruncher:
         return self.performance_report(self._cores.last_compute_id)
 
     lastComputePerformanceReport = last_compute_performance_report
+
+    # ------------------------------------------------------------ device-side enqueue
+    def device_enqueue_errors(self) -> int:
+        """Child launches dropped so far by ``cek_enqueue`` (a queue level
+        full, or an enqueue deeper than the supported levels), summed over
+        devices.  Waits for the devices.  Device-side enqueue replaces the
+        reference's OpenCL 2.0 default-queue ``enqueue_kernel``
+        (ClNumberCruncher.cs:203-205, Worker.cs:224-227): a kernel appends
+        ``{child, n, param}`` records to its device's queue, and generated
+        dispatcher launches run each child level right after the parent on
+        the same stream, with no host round trip."""
+        return int(self._cores.device_enqueue_errors()) if self._cores else 0
+
+    def set_device_enqueue_levels(self, levels: int) -> None:
+        """Child levels run after each parent launch (0..3, default 3)."""
+        self._cores.set_device_enqueue_levels(int(levels))
 
     # ------------------------------------------------------------ device timeline
     @property

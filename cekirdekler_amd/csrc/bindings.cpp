@@ -286,6 +286,8 @@ PYBIND11_MODULE(_cek, m) {
       .def_property_readonly("last_compute_id", &Cores::last_compute_id)
       .def("last_record", &Cores::last_record)
       .def_readwrite("record_timeline", &Cores::record_timeline)
+      .def("set_device_enqueue_levels", &Cores::set_device_enqueue_levels)
+      .def("device_enqueue_errors", &Cores::device_enqueue_errors, py::call_guard<py::gil_scoped_release>())
       .def("timeline",
            [](Cores& c) {
              std::vector<std::tuple<int, int, double, double>> out;

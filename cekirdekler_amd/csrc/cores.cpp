@@ -123,6 +123,19 @@ void Cores::balance(BalancerState& st, bool first, long long G, long long step) 
   }
 }
 
+void Cores::set_device_enqueue_levels(int levels) {
+  if (levels < 0 || levels > kDynLevels - 1)
+    throw Error("device enqueue levels must be in [0, " + std::to_string(kDynLevels - 1) + "]");
+  for (auto& w : workers_) w->device_enqueue_levels = levels;
+}
+
+int Cores::device_enqueue_errors() {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
+  int e = 0;
+  for (auto& w : workers_) e += w->device_enqueue_errors();
+  return e;
+}
+
 void Cores::set_dynamic_lds(unsigned bytes) {
   for (auto& w : workers_) w->set_dynamic_lds(bytes);
 }

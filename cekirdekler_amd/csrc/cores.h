@@ -192,6 +192,10 @@ class Cores {
   }
   int failovers() const { return failovers_; }
   void set_dynamic_lds(unsigned bytes);
+  // device-side enqueue (cek_enqueue): child levels per parent launch, and
+  // the errors counted on the devices so far (syncs)
+  void set_device_enqueue_levels(int levels);
+  int device_enqueue_errors();
   // ---- device timeline ----
   // With record_timeline on, the kernels of every compute are bracketed by
   // timing hipEvents on the stream they run on (host clock on the CPU

@@ -298,15 +298,133 @@ static inline int atomic_inc(int* p) { return atomicAdd(p, 1); }
 // ---- end prelude ----
 )CEK";
 
+// ------------------------------------------------- device-side enqueue --
+// OpenCL 2.0 enqueue_kernel has no HIP equivalent.  The
+// MI355X-native replacement is GPU-resident: a kernel calls
+//   cek_enqueue(child, n, param)
+// to append a launch record {child, n, param} to its device's queue, one
+// queue level deeper than itself.  Children are written as
+//   __cek_child__ void child(long long id, long long param, <parent's params>)
+// After the parent, the runtime issues one generated dispatcher launch per
+// child level on the same stream (stream order makes each level's records
+// visible to the next): the dispatcher's waves grid-stride over every record
+// of its level and call the child for each id.  No host round trip, no spin
+// waits; the depth is bounded (kDynLevels) and a full level or a too-deep
+// enqueue counts an error the host can read.
+
+bool uses_device_enqueue(const std::string& src) {
+  static const std::regex re(R"((^|[^\w])cek_enqueue\s*\()");
+  return std::regex_search(src, re);
+}
+
+static std::string param_name(const std::string& p) {
+  static const std::regex re(R"(([A-Za-z_]\w*)\s*(\[[^\]]*\])?\s*$)");
+  std::smatch m;
+  return std::regex_search(p, m, re) ? m[1].str() : std::string();
+}
+
+static std::vector<std::string> split_params(const std::string& inside) {
+  std::vector<std::string> out;
+  std::string cur;
+  int depth = 0;
+  for (char c : inside) {
+    if (c == '(' || c == '<' || c == '[') ++depth;
+    if (c == ')' || c == '>' || c == ']') --depth;
+    if (c == ',' && depth == 0) {
+      out.push_back(cur);
+      cur.clear();
+    } else {
+      cur += c;
+    }
+  }
+  std::string t;
+  for (char c : cur)
+    if (!isspace(static_cast<unsigned char>(c))) t += c;
+  if (!t.empty() && t != "void") out.push_back(cur);
+  return out;
+}
+
+static size_t match_brace(const std::string& s, size_t open) {
+  int depth = 0;
+  for (size_t i = open; i < s.size(); ++i) {
+    if (s[i] == '{') ++depth;
+    else if (s[i] == '}') {
+      if (--depth == 0) return i;
+    }
+  }
+  return std::string::npos;
+}
+
+static std::string dyn_prelude(const std::vector<std::string>& children) {
+  std::ostringstream os;
+  os << "// ---- device-side enqueue ----\n"
+     << "#define CEK_DYN_LEVELS " << kDynLevels << "\n#define CEK_DYN_CAP " << kDynCap << "\n"
+     << "struct __CekRec { int child; int pad; long long n; long long param; };\n"
+     << "struct __CekQueue { int count[8]; int errors; int pad[7]; __CekRec recs[CEK_DYN_LEVELS][CEK_DYN_CAP]; };\n"
+     << "__device__ inline void __cek_enqueue(void* qv, int level, int child, long long n, long long param) {\n"
+     << "  __CekQueue* q = (__CekQueue*)qv;\n"
+     << "  if (n <= 0) return;\n"
+     << "  if (level + 1 >= CEK_DYN_LEVELS) { atomicAdd(&q->errors, 1); return; }\n"
+     << "  int slot = atomicAdd(&q->count[level + 1], 1);\n"
+     << "  if (slot >= CEK_DYN_CAP) { atomicAdd(&q->errors, 1); return; }\n"
+     << "  __CekRec r; r.child = child; r.pad = 0; r.n = n; r.param = param;\n"
+     << "  q->recs[level + 1][slot] = r;\n"
+     << "}\n"
+     << "#define cek_enqueue(child, n, param) __cek_enqueue(__cek_q, __cek_level, __cek_child_##child, (long long)(n), (long long)(param))\n"
+     << "#define __cek_child__ __device__\n";
+  if (!children.empty()) {
+    os << "enum {";
+    for (size_t i = 0; i < children.size(); ++i) os << (i ? ", " : " ") << "__cek_child_" << children[i] << " = " << i;
+    os << " };\n";
+  }
+  return os.str();
+}
+
 std::string gpu_rewrite(const std::string& src) {
   std::string s = is_opencl_dialect(src) ? translate_opencl(src) : strip_comments(src);
   // hiprtc supplies the HIP runtime itself.
   s = regex_replace_all(s, R"(#\s*include\s*[<"]hip/hip_runtime\.h[>"])", "");
+  const bool dyn = uses_device_enqueue(s);
   auto sites = find_sites(s);
+  // dispatchers (generated from the unmodified parameter lists)
+  std::vector<std::string> children;
+  std::string dispatchers;
+  if (dyn) {
+    static const std::regex child_re(R"(__cek_child__\s+void\s+([A-Za-z_]\w*)\s*\()");
+    for (auto it = std::sregex_iterator(s.begin(), s.end(), child_re); it != std::sregex_iterator(); ++it)
+      children.push_back((*it)[1].str());
+    std::set<std::string> done;
+    for (auto& k : sites) {
+      if (!done.insert(k.sig.name).second) continue;
+      size_t ob = s.find('{', k.close), cb = ob == std::string::npos ? ob : match_brace(s, ob);
+      if (cb == std::string::npos || !uses_device_enqueue(s.substr(ob, cb - ob))) continue;
+      const std::string inside = s.substr(k.open + 1, k.close - k.open - 1);
+      const auto params = split_params(inside);
+      std::string names;
+      for (auto& p : params) names += ", " + param_name(p);
+      std::ostringstream os;
+      os << "extern \"C\" __global__ void __cek_dispatch_" << k.sig.name << "(" << inside
+         << (params.empty() ? "" : ", ")
+         << "long long __cek_off, long long __cek_gsize, void* __cek_q, int __cek_level) {\n"
+         << "  __CekQueue* q = (__CekQueue*)__cek_q;\n"
+         << "  const int cnt = min(q->count[__cek_level], CEK_DYN_CAP);\n"
+         << "  const long long stride = (long long)gridDim.x * blockDim.x;\n"
+         << "  for (int r = 0; r < cnt; ++r) {\n"
+         << "    const __CekRec rec = q->recs[__cek_level][r];\n"
+         << "    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < rec.n; i += stride) {\n"
+         << "      switch (rec.child) {\n";
+      for (size_t c = 0; c < children.size(); ++c)
+        os << "        case " << c << ": " << children[c] << "(i, rec.param" << names
+           << ", __cek_q, __cek_level); break;\n";
+      os << "        default: break;\n      }\n    }\n  }\n}\n";
+      dispatchers += os.str();
+    }
+  }
+  const std::string hidden =
+      dyn ? "long long __cek_off, long long __cek_gsize, void* __cek_q, int __cek_level"
+          : "long long __cek_off, long long __cek_gsize";
   for (auto it = sites.rbegin(); it != sites.rend(); ++it) {
     const auto& k = *it;
-    std::string inside = s.substr(k.open + 1, k.close - k.open - 1);
-    std::string hidden = "long long __cek_off, long long __cek_gsize";
     if (k.sig.arity == 0) {
       s.replace(k.open + 1, k.close - k.open - 1, hidden);
     } else {
@@ -314,7 +432,19 @@ std::string gpu_rewrite(const std::string& src) {
     }
     if (!k.has_extern_c) s.insert(k.global_pos, "extern \"C\" ");
   }
-  return std::string(kGpuPrelude) + "#line 1\n" + s;
+  if (!dyn) return std::string(kGpuPrelude) + "#line 1\n" + s;
+  // children get the queue and their own level (enqueues go one deeper)
+  static const std::regex child_re(R"(__cek_child__\s+void\s+([A-Za-z_]\w*)\s*\()");
+  std::vector<std::pair<size_t, size_t>> parens;
+  for (auto it = std::sregex_iterator(s.begin(), s.end(), child_re); it != std::sregex_iterator(); ++it) {
+    size_t open = static_cast<size_t>(it->position(0) + it->length(0) - 1);
+    size_t close = match_paren(s, open);
+    if (close != std::string::npos) parens.emplace_back(open, close);
+  }
+  for (auto it = parens.rbegin(); it != parens.rend(); ++it)
+    s.insert(it->second, ", void* __cek_q, int __cek_level");
+  return std::string(kGpuPrelude) + dyn_prelude(children) + "#line 1\n" + s + "\n// ---- dispatchers ----\n" +
+         dispatchers;
 }
 
 std::string cpu_rewrite(const std::string& src) {
@@ -503,6 +633,18 @@ std::shared_ptr<Program> Program::build(const DeviceInfo& dev, const std::string
         CEK_HIP(hipModuleGetFunction(&f, m, k.name.c_str()));
         p->gpu_fns_[k.name] = f;
       }
+      p->dynamic_ = uses_device_enqueue(src);
+      if (p->dynamic_)
+        for (auto& k : p->kernels_) {
+          hipFunction_t f;
+          const std::string dn = "__cek_dispatch_" + k.name;
+          if (hipModuleGetFunction(&f, m, dn.c_str()) == hipSuccess) {
+            p->gpu_fns_[dn] = f;
+            p->dispatchers_.insert(k.name);
+          } else {
+            (void)hipGetLastError();
+          }
+        }
     }
     // prebuilt entries: "path|name1,name2"
     for (auto& pb : prebuilt) {
@@ -529,6 +671,10 @@ std::shared_ptr<Program> Program::build(const DeviceInfo& dev, const std::string
       }
     }
   } else {
+    if (uses_device_enqueue(src)) {
+      p->log_ = "cek_enqueue (device-side enqueue) runs on GPU devices only";
+      return p;
+    }
     if (!src.empty()) {
       std::string so, log;
       if (!compile_cpu(cpu_rewrite(src), options, so, log)) {

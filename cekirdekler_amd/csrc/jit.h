@@ -19,6 +19,7 @@
 #include "device.h"
 
 #include <map>
+#include <set>
 
 namespace cek {
 
@@ -59,8 +60,15 @@ class Program {
   CpuRunner cpu_fn(const std::string& name) const;
   int device_type() const { return type_; }
   double build_ms() const { return build_ms_; }
+  // Device-side enqueue (cek_enqueue in the source): kernels take the queue
+  // and level as extra hidden arguments, and a kernel that enqueues has a
+  // generated "__cek_dispatch_<name>" that runs one level of child launches.
+  bool dynamic() const { return dynamic_; }
+  bool has_dispatcher(const std::string& kernel) const { return dispatchers_.count(kernel) > 0; }
 
  private:
+  bool dynamic_ = false;
+  std::set<std::string> dispatchers_;
   int type_ = kGPU;
   bool ok_ = false;
   std::string log_;
@@ -71,6 +79,14 @@ class Program {
   void* dl_ = nullptr;
   std::map<std::string, CpuRunner> cpu_fns_;
 };
+
+// Device-side enqueue: levels (parent = level 0) and records per level of
+// the per-device queue; layout shared with the generated prelude.
+constexpr int kDynLevels = 4;
+constexpr int kDynCap = 16384;
+constexpr size_t kDynHeaderBytes = 64;  // int count[8]; int errors; pad
+constexpr size_t kDynQueueBytes = kDynHeaderBytes + size_t(kDynLevels) * kDynCap * 24;
+bool uses_device_enqueue(const std::string& src);
 
 // Compile to a gfx950 code object (cached in memory and on disk).  Returns
 // false and fills log on error.

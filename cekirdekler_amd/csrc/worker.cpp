@@ -96,6 +96,7 @@ Worker::~Worker() {
     } catch (...) {
     }
     release_all();
+    for (auto& dq : dyn_queues_) (void)hipFree(dq.second);
     for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
     for (auto e : events_) (void)hipEventDestroy(e);
     if (main_) (void)hipStreamDestroy(main_);
@@ -299,13 +300,32 @@ void Worker::launch(hipStream_t s, const std::string& kernel, const std::vector<
     std::vector<void*> ptrs(arrs.size());
     for (size_t i = 0; i < arrs.size(); ++i) ptrs[i] = buffer(arrs[i]);
     long long off = offset, gs = gsize;
-    std::vector<void*> params(arrs.size() + 2);
+    const bool dyn = prog_->dynamic();
+    void* q = dyn ? dyn_queue(s) : nullptr;
+    int level = 0;
+    std::vector<void*> params(arrs.size() + (dyn ? 4 : 2));
     for (size_t i = 0; i < arrs.size(); ++i) params[i] = &ptrs[i];
     params[arrs.size()] = &off;
     params[arrs.size() + 1] = &gs;
+    if (dyn) {
+      params[arrs.size() + 2] = &q;
+      params[arrs.size() + 3] = &level;
+      // fresh level counts for this parent (errors accumulate)
+      CEK_HIP(hipMemsetAsync(q, 0, 8 * sizeof(int), s));
+    }
     unsigned grid = static_cast<unsigned>(count / local);
     CEK_HIP(hipModuleLaunchKernel(f, grid, 1, 1, static_cast<unsigned>(local), 1, 1, dyn_lds_, s,
                                   params.data(), nullptr));
+    if (dyn && prog_->has_dispatcher(kernel)) {
+      // one launch per child level, same stream: level L's records were
+      // written by level L-1's kernel, which the stream has completed
+      hipFunction_t d = prog_->gpu_fn("__cek_dispatch_" + kernel);
+      const unsigned dgrid = static_cast<unsigned>(std::max(1, dev_.compute_units) * 4);
+      for (int L = 1; L <= std::min(device_enqueue_levels, kDynLevels - 1); ++L) {
+        level = L;
+        CEK_HIP(hipModuleLaunchKernel(d, dgrid, 1, 1, 256, 1, 1, 0, s, params.data(), nullptr));
+      }
+    }
   } else {
     CpuRunner fn = prog_->cpu_fn(kernel);
     std::vector<void*> ptrs(arrs.size());
@@ -321,6 +341,29 @@ void Worker::launch(hipStream_t s, const std::string& kernel, const std::vector<
       fn(argv, offset, gsize, offset + g0 * local, (g1 - g0) * local, local);
     });
   }
+}
+
+void* Worker::dyn_queue(hipStream_t s) {
+  void*& q = dyn_queues_[s];
+  if (!q) {
+    set_device();
+    CEK_HIP(hipMalloc(&q, kDynQueueBytes));
+    CEK_HIP(hipMemset(q, 0, kDynHeaderBytes));
+  }
+  return q;
+}
+
+int Worker::device_enqueue_errors() {
+  if (!gpu() || dyn_queues_.empty()) return 0;
+  set_device();
+  sync_all();
+  int total = 0;
+  for (auto& dq : dyn_queues_) {
+    int e = 0;
+    CEK_HIP(hipMemcpy(&e, static_cast<char*>(dq.second) + 8 * sizeof(int), sizeof(int), hipMemcpyDeviceToHost));
+    total += e;
+  }
+  return total;
 }
 
 void Worker::add_marker(hipStream_t s) {

@@ -103,6 +103,10 @@ class Worker {
   void launch(hipStream_t s, const std::string& kernel, const std::vector<ArraySpec>& arrs,
               long long offset, long long count, int local, long long gsize);
   void set_dynamic_lds(unsigned bytes) { dyn_lds_ = bytes; }
+  // Device-side enqueue: child levels run after each parent launch (1..3)
+  // and errors counted on the device (queue level full / too deep).
+  int device_enqueue_levels = kDynLevels - 1;
+  int device_enqueue_errors();
 
   // --- markers (fine-grained queue control, ClCommandQueue.cs:103-112) ---
   void add_marker(hipStream_t s);
@@ -139,6 +143,10 @@ class Worker {
   int qconc_;
   bool no_pipelining_;
   unsigned dyn_lds_ = 0;
+  // device-side enqueue queues (kDynQueueBytes each), one per stream so
+  // blobs in flight on concurrent streams never share level counts
+  std::unordered_map<hipStream_t, void*> dyn_queues_;
+  void* dyn_queue(hipStream_t s);
   std::unordered_map<uint64_t, std::pair<void*, uint64_t>> bufs_;
   std::unordered_map<uint64_t, bool> zc_;
   uint64_t bytes_allocated_ = 0;

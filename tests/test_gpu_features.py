@@ -397,3 +397,36 @@ def test_cl_pipeline_multi_gpu_stage_hidden_constants(gpu):
             seen.append(float(res[0]))
     pipe.dispose()
     assert seen == [3.0 * p - 3.0 for p in range(len(seen))] and len(seen) == 4
+
+
+def test_device_side_enqueue_levels(gpu):
+    """cek_enqueue: a parent enqueues a child, the child enqueues a grandchild;
+    both levels run on the GPU right after the parent, no host round trip
+    (replaces enqueue_kernel, ClNumberCruncher.cs:203-205)."""
+    src = r"""
+__cek_child__ void fill(long long id, long long param, float* x) {
+  x[param + id] += 1.0f;
+  if (id == 0 && param == 0) cek_enqueue(fill2, 64, 128);
+}
+__cek_child__ void fill2(long long id, long long param, float* x) { x[param + id] += 10.0f; }
+__global__ void parent(float* x) {
+  long long i = get_global_id(0);
+  if (i == 0) cek_enqueue(fill, 128, 0);
+  x[i] += 100.0f;
+}
+"""
+    c = ck.ClNumberCruncher(gpu[0], src)
+    assert c.error_code() == 0, c.error_message()
+    x = ck.ClArray(np.zeros(1024, np.float32))
+    x.compute(c, 1, "parent", 1024, 256)
+    exp = np.full(1024, 100.0, np.float32)
+    exp[:128] += 1.0
+    exp[128:192] += 10.0
+    np.testing.assert_array_equal(x.array, exp)
+    assert c.device_enqueue_errors() == 0
+    c.set_device_enqueue_levels(1)  # grandchildren not dispatched
+    x.compute(c, 2, "parent", 1024, 256)
+    exp2 = exp + 100.0
+    exp2[:128] += 1.0
+    np.testing.assert_array_equal(x.array, exp2)
+    c.dispose()

@@ -55,3 +55,31 @@ def test_hiprtc_reports_errors():
     ok, code, log = cek.compile_gpu("__global__ void k(float* x) { x[0] = undefined_symbol; }", [], "gfx950")
     assert not ok
     assert "undefined_symbol" in log
+
+
+DYN_SRC = r"""
+__cek_child__ void fill(long long id, long long param, float* x) {
+  x[param + id] += 1.0f;
+  if (id == 0 && param == 0) cek_enqueue(fill2, 64, 128);
+}
+__cek_child__ void fill2(long long id, long long param, float* x) { x[param + id] += 10.0f; }
+__global__ void parent(float* x) {
+  long long i = get_global_id(0);
+  if (i == 0) cek_enqueue(fill, 128, 0);
+  x[i] += 100.0f;
+}
+"""
+
+
+def test_device_enqueue_rewrite_and_compile():
+    """cek_enqueue (the OpenCL 2.0 enqueue_kernel replacement): children get
+    the queue + level, the parent gets a generated dispatcher, and the whole
+    program cross-compiles for gfx950."""
+    out = cek.gpu_rewrite(DYN_SRC)
+    assert "__cek_dispatch_parent(float* x, long long __cek_off, long long __cek_gsize, void* __cek_q, int __cek_level)" in out
+    assert "void fill(long long id, long long param, float* x, void* __cek_q, int __cek_level)" in out
+    assert "case 1: fill2(i, rec.param, x, __cek_q, __cek_level)" in out
+    ok, code, log = cek.compile_gpu(DYN_SRC, [], "gfx950")
+    assert ok, log
+    # plain sources are untouched by the dynamic path
+    assert "__cek_dispatch" not in cek.gpu_rewrite("__global__ void k(float* x) { x[0] = 1; }")
