@@ -1,10 +1,12 @@
-"""Summarise rocprofv3 CSV output (kernel trace + counters) into markdown.
+"""Summarise rocprofv3 output (CSV, or the rocpd SQLite ``*_results.db``;
+kernel trace + counters) into markdown.
 
 usage: python tools/summarize_prof.py <rocprof dir> [title] > profiles/<name>.md
 """
 import csv
 import glob
 import os
+import sqlite3
 import sys
 from collections import defaultdict
 
@@ -14,10 +16,16 @@ def main():
     title = sys.argv[2] if len(sys.argv) > 2 else os.path.basename(d.rstrip("/"))
     print(f"# {title}\n")
     kt = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    db = glob.glob(os.path.join(d, "**", "*results.db"), recursive=True)
+    per = defaultdict(list)
     if kt:
-        per = defaultdict(list)
         for r in csv.DictReader(open(kt[0])):
             per[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    elif db:
+        con = sqlite3.connect(db[0])
+        for name, dur in con.execute("select name, duration from kernels"):
+            per[name].append(dur / 1e3)
+    if per:
         print("## Kernel trace (µs per dispatch)\n")
         print("| kernel | calls | mean µs | min µs | max µs | total µs |")
         print("|---|---|---|---|---|---|")
