@@ -155,6 +155,8 @@ class ClNumberCruncher:
         self._error_message = self._cores.error_message
         if self._error_code:
             self.number_of_errors_happened += 1
+        elif os.environ.get("CEK_DEBUG", "") not in ("", "0"):
+            self.debug_checks = True
         _register_cores(self)
 
     # ------------------------------------------------------------ status
@@ -375,6 +377,24 @@ class ClNumberCruncher:
     def set_device_enqueue_levels(self, levels: int) -> None:
         """Child levels run after each parent launch (0..3, default 3)."""
         self._cores.set_device_enqueue_levels(int(levels))
+
+    # ------------------------------------------------------------ debug checks
+    @property
+    def debug_checks(self) -> bool:
+        """Debug mode (the reference has none and lists
+        out-of-bounds native access as a known issue, README.md:40-45).
+        While on, GPU buffers allocated from then on get a 4 KiB guard tail,
+        every kernel launch is synchronised so a fault names its kernel, and
+        a kernel that wrote past the end of one of its arrays fails the
+        compute with the array index and the first corrupted byte.  Costs a
+        sync and a 4 KiB read-back per array per launch.  ``CEK_DEBUG=1``
+        turns it on for every cruncher.  Graph-replayed repeat loops are not
+        checked."""
+        return bool(self._cores.debug_checks) if self._cores else False
+
+    @debug_checks.setter
+    def debug_checks(self, on: bool) -> None:
+        self._cores.debug_checks = bool(on)
 
     # ------------------------------------------------------------ device timeline
     @property

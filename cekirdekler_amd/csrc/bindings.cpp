@@ -287,6 +287,7 @@ PYBIND11_MODULE(_cek, m) {
       .def("last_record", &Cores::last_record)
       .def_readwrite("record_timeline", &Cores::record_timeline)
       .def("set_device_enqueue_levels", &Cores::set_device_enqueue_levels)
+      .def_property("debug_checks", &Cores::debug_checks, &Cores::set_debug_checks)
       .def("device_enqueue_errors", &Cores::device_enqueue_errors, py::call_guard<py::gil_scoped_release>())
       .def("timeline",
            [](Cores& c) {

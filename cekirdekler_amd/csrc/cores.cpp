@@ -129,6 +129,11 @@ void Cores::set_device_enqueue_levels(int levels) {
   for (auto& w : workers_) w->device_enqueue_levels = levels;
 }
 
+void Cores::set_debug_checks(bool on) {
+  debug_checks_ = on;
+  for (auto& w : workers_) w->debug_checks = on;
+}
+
 int Cores::device_enqueue_errors() {
   std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   int e = 0;

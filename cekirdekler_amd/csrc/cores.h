@@ -195,6 +195,9 @@ class Cores {
   // device-side enqueue (cek_enqueue): child levels per parent launch, and
   // the errors counted on the devices so far (syncs)
   void set_device_enqueue_levels(int levels);
+  // debug checks: guard tails on new buffers, synchronous checked launches
+  void set_debug_checks(bool on);
+  bool debug_checks() const { return debug_checks_; }
   int device_enqueue_errors();
   // ---- device timeline ----
   // With record_timeline on, the kernels of every compute are bracketed by
@@ -289,6 +292,7 @@ class Cores {
   }
   std::vector<int> inject_;
   int failovers_ = 0;
+  bool debug_checks_ = false;
   void compute_once(const ComputeCall& call, struct DeviceFailure* failed);
   void balance(struct BalancerState& st, bool first, long long G, long long step);
   std::string error_;

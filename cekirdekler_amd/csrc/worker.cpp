@@ -135,10 +135,17 @@ void* Worker::buffer(const ArraySpec& a) {
   }
   void* d = nullptr;
   set_device();
-  hipError_t e = hipMalloc(&d, a.bytes ? a.bytes : 1);
+  const size_t guard = debug_checks ? kGuardBytes : 0;
+  hipError_t e = hipMalloc(&d, (a.bytes ? a.bytes : 1) + guard);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     throw Error("hipMalloc of " + std::to_string(a.bytes) + " bytes failed on " + dev_.name);
+  }
+  if (guard) {
+    CEK_HIP(hipMemset(static_cast<char*>(d) + a.bytes, kGuardByte, guard));
+    guarded_[a.uid] = a.bytes;
+  } else {
+    guarded_.erase(a.uid);
   }
   bufs_[a.uid] = {d, a.bytes};
   bytes_allocated_ += a.bytes;
@@ -154,6 +161,7 @@ void Worker::release(uint64_t uid) {
     bytes_allocated_ -= it->second.second;
     bufs_.erase(it);
   }
+  guarded_.erase(uid);
   zc_.erase(uid);
 }
 
@@ -164,6 +172,7 @@ void Worker::release_all() {
     for (auto& kv : bufs_) (void)hipFree(kv.second.first);
   }
   bufs_.clear();
+  guarded_.clear();
   zc_.clear();
   bytes_allocated_ = 0;
 }
@@ -326,6 +335,7 @@ void Worker::launch(hipStream_t s, const std::string& kernel, const std::vector<
         CEK_HIP(hipModuleLaunchKernel(d, dgrid, 1, 1, 256, 1, 1, 0, s, params.data(), nullptr));
       }
     }
+    if (debug_checks) check_guards(s, kernel, arrs);
   } else {
     CpuRunner fn = prog_->cpu_fn(kernel);
     std::vector<void*> ptrs(arrs.size());
@@ -340,6 +350,42 @@ void Worker::launch(hipStream_t s, const std::string& kernel, const std::vector<
       long long g0 = t * per, g1 = std::min(groups, g0 + per);
       fn(argv, offset, gsize, offset + g0 * local, (g1 - g0) * local, local);
     });
+  }
+}
+
+void Worker::check_guards(hipStream_t s, const std::string& kernel, const std::vector<ArraySpec>& arrs) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return;  // graph replay
+  hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    throw Error("kernel '" + kernel + "' failed on " + dev_.name + ": " + hipGetErrorString(e));
+  }
+  std::vector<unsigned char> tail(kGuardBytes);
+  for (size_t i = 0; i < arrs.size(); ++i) {
+    void* d = nullptr;
+    uint64_t at = 0;
+    {
+      std::lock_guard<std::mutex> g(buf_mu_);
+      auto gi = guarded_.find(arrs[i].uid);
+      auto bi = bufs_.find(arrs[i].uid);
+      if (gi == guarded_.end() || bi == bufs_.end()) continue;
+      d = bi->second.first;
+      at = gi->second;
+    }
+    CEK_HIP(hipMemcpy(tail.data(), static_cast<char*>(d) + at, kGuardBytes, hipMemcpyDeviceToHost));
+    size_t bad = 0, first = kGuardBytes;
+    for (size_t b = 0; b < kGuardBytes; ++b)
+      if (tail[b] != kGuardByte) {
+        ++bad;
+        if (first == kGuardBytes) first = b;
+      }
+    if (bad) {
+      CEK_HIP(hipMemset(static_cast<char*>(d) + at, kGuardByte, kGuardBytes));
+      throw Error("kernel '" + kernel + "' wrote past the end of array #" + std::to_string(i) + " (" +
+                  std::to_string(at) + " bytes) on " + dev_.name + ": " + std::to_string(bad) +
+                  " guard bytes changed, first at +" + std::to_string(first));
+    }
   }
 }
 

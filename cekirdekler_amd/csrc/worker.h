@@ -106,6 +106,13 @@ class Worker {
   // Device-side enqueue: child levels run after each parent launch (1..3)
   // and errors counted on the device (queue level full / too deep).
   int device_enqueue_levels = kDynLevels - 1;
+  // Debug checks: buffers allocated while on get a guard tail
+  // of kGuardBytes filled with kGuardByte; every launch is then synchronised
+  // (a fault names its kernel) and the guards of its arrays are verified, so
+  // a kernel writing past the end of an array is reported by name.
+  static constexpr size_t kGuardBytes = 4096;
+  static constexpr unsigned char kGuardByte = 0xCE;
+  bool debug_checks = false;
   int device_enqueue_errors();
 
   // --- markers (fine-grained queue control, ClCommandQueue.cs:103-112) ---
@@ -149,6 +156,8 @@ class Worker {
   void* dyn_queue(hipStream_t s);
   std::unordered_map<uint64_t, std::pair<void*, uint64_t>> bufs_;
   std::unordered_map<uint64_t, bool> zc_;
+  std::unordered_map<uint64_t, uint64_t> guarded_;  // uid -> guard offset (bytes)
+  void check_guards(hipStream_t s, const std::string& kernel, const std::vector<ArraySpec>& arrs);
   uint64_t bytes_allocated_ = 0;
   std::mutex buf_mu_;
 

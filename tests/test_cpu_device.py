@@ -251,3 +251,20 @@ def test_devices_ranked_by_nbody_time(cpu):
     plats = ck.ClPlatforms.all()
     ranked = (plats.cpus(True) + plats.cpus(True)).devices_with_highest_direct_nbody_performance(n=1024)
     assert len(ranked) == 2 and all(d.is_cpu for d in ranked)
+
+
+def test_debug_checks_flag_and_env(cpu, monkeypatch):
+    """debug_checks round-trips (host buffers on the CPU device are the
+    user's arrays, so only GPU buffers get guard tails) and CEK_DEBUG=1
+    turns it on at construction."""
+    c = ck.ClNumberCruncher(cpu, SRC)
+    assert not c.debug_checks
+    c.debug_checks = True
+    x = ck.ClArray(np.zeros(256, np.float32))
+    x.compute(c, 1, "inc", 256, 64)
+    np.testing.assert_array_equal(x.array, np.ones(256, np.float32))
+    c.dispose()
+    monkeypatch.setenv("CEK_DEBUG", "1")
+    c2 = ck.ClNumberCruncher(cpu, SRC)
+    assert c2.debug_checks
+    c2.dispose()

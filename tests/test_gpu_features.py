@@ -430,3 +430,23 @@ __global__ void parent(float* x) {
     exp2[:128] += 1.0
     np.testing.assert_array_equal(x.array, exp2)
     c.dispose()
+
+
+def test_debug_checks_catch_out_of_bounds_write(gpu):
+    """Debug mode: guard tails on device buffers name the kernel and the
+    array a past-the-end write corrupted (reference README.md:40-45 lists
+    unchecked out-of-bounds access as a known issue)."""
+    src = """
+__global__ void ok(float* x) { x[get_global_id(0)] += 1.0f; }
+__global__ void oob(float* x) { x[get_global_id(0) + 1] = 7.0f; }
+"""
+    c = ck.ClNumberCruncher(gpu[0], src)
+    assert c.error_code() == 0, c.error_message()
+    c.debug_checks = True
+    assert c.debug_checks
+    x = ck.ClArray(np.zeros(1024, np.float32))
+    x.compute(c, 1, "ok", 1024, 256)
+    np.testing.assert_array_equal(x.array, np.ones(1024, np.float32))
+    with pytest.raises(Exception, match=r"oob.*wrote past the end of array #0 \(4096 bytes\).*first at \+0"):
+        x.compute(c, 2, "oob", 1024, 256)
+    c.dispose()
