@@ -22,7 +22,7 @@
 
 namespace {
 
-template <int WM, int WN, int FM, int FN, bool PIPE>
+template <int WM, int WN, int FM, int FN, int PIPE>
 __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, const float* __restrict__ A,
                                               const float* __restrict__ Bt, float* __restrict__ C, char* smem,
                                               long long off) {
@@ -102,7 +102,23 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (!PIPE) {
+  if constexpr (PIPE == 2) {
+    // both 16-deep k blocks' fragments are read up front: the second block's
+    // ds_reads fly under the first block's MFMAs (2 fragment sets live, no
+    // carry across the barrier, unlike PIPE == 1)
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+      const char* base = smem + cur * STAGE;
+      f32x4 xa[FM], xb[FN], ya[FM], yb[FN];
+      ld(xa, xb, base, 0);
+      ld(ya, yb, base, 1);
+      mma(xa, xb);
+      mma(ya, yb);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else if constexpr (PIPE == 0) {
     // one barrier per K-tile; the next K-tile's DMA flies under the MFMAs
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
@@ -277,13 +293,16 @@ __device__ __forceinline__ void gemm_f32w_tile(const int* __restrict__ dims, con
   }
 
 // 128×128 tiles, 4 waves (2×2, 64×64 each), 64 KiB LDS: two work-groups per CU.
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_128x128, 2, 2, 4, 4, false)
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_128x128p, 2, 2, 4, 4, true)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_128x128, 2, 2, 4, 4, 0)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_128x128p, 2, 2, 4, 4, 1)
 // 256×128 tiles, 8 waves (4×2, 64×64 each), 96 KiB LDS.
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128, 4, 2, 4, 4, false)
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128p, 4, 2, 4, 4, true)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128, 4, 2, 4, 4, 0)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128p, 4, 2, 4, 4, 1)
 // 256×256 tiles, 8 waves (2×4, 128×64 each), 128 KiB LDS.
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256, 2, 4, 8, 4, false)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256, 2, 4, 8, 4, 0)
+// the same with both k blocks' fragments read before the MFMAs
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256h, 2, 4, 8, 4, 2)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128h, 4, 2, 4, 4, 2)
 // (a register double-buffered 256×256 variant needs 256 + 57 spilled VGPRs)
 
 // 32×32×2 form with register double-buffered fragments (gemm_f32w_tile).

@@ -61,6 +61,8 @@ F32_TILES = {
     "128x128": (128, 128, 256, "cek_sgemm_f32_128x128"),
     "256x128": (256, 128, 512, "cek_sgemm_f32_256x128"),
     "256x256": (256, 256, 512, "cek_sgemm_f32_256x256"),
+    "256x256h": (256, 256, 512, "cek_sgemm_f32_256x256h"),
+    "256x128h": (256, 128, 512, "cek_sgemm_f32_256x128h"),
     # "p": register double-buffered fragments (next k block read under the MFMAs)
     "128x128p": (128, 128, 256, "cek_sgemm_f32_128x128p"),
     "256x128p": (256, 128, 512, "cek_sgemm_f32_256x128p"),
