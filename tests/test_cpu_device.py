@@ -268,3 +268,11 @@ def test_debug_checks_flag_and_env(cpu, monkeypatch):
     c2 = ck.ClNumberCruncher(cpu, SRC)
     assert c2.debug_checks
     c2.dispose()
+
+
+def test_license_text_names_gpl():
+    """Reference ``License.cs:58``: the library exposes its license notice."""
+    import cekirdekler_amd
+    text = cekirdekler_amd.license_text()
+    assert "GNU General Public License" in text
+    assert "Cekirdekler" in text
