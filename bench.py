@@ -7,6 +7,11 @@ count ("load-balance iters") as extra fields.
     python bench.py --gpus N --steps K --warmup W
     torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
 
+Without a torchrun environment, ``--gpus N > 1`` starts the N rank processes
+itself: ``torch.distributed.run`` runs as a child process of this one, which
+never imports the runtime or touches a GPU, and this process exits with the
+launcher's code (no exec).
+
 A step is one ``compute()`` of the whole 8192×8192×8192 GEMM through the
 framework: the balancer splits the 1024 (or 2048) output tiles across the
 ranks, every rank runs the hand-written CDNA4 MFMA kernel on its slice, the
@@ -14,7 +19,14 @@ per-device times are exchanged and the next split is computed.  Inputs are
 device-resident after the first call and C stays in device memory
 (BASELINE.md "device-resident"); the host-resident variant (A/B uploaded and
 C slices downloaded each call) is reported separately.  Data: synthetic
-uniform [-1, 1) bf16.  Rank 0 prints one JSON line.
+uniform [-1, 1) bf16.  After the timed loops every rank downloads its device
+replica of C and compares sampled tiles of its own range with a float64 host
+product; the bench exits non-zero when the relative error exceeds 5e-3 or a
+K-split partner wait timed out.  Rank 0 prints one JSON line.
+
+In a container without a GPU the headline runs a plain kernel-string GEMM on
+each rank's CPU device instead (``"device": "cpu"`` in the config): that is
+the launcher / control-plane rehearsal the CPU tests use, not a number.
 """
 from __future__ import annotations
 
@@ -139,19 +151,84 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     ms = timed(ctx, step, steps, 1,
                enter=lambda: setattr(cr, "enqueue_mode", True),
                leave=lambda: setattr(cr, "enqueue_mode", False))
+    ranges = cr.ranges(1)
+    # the benchmarked output itself: sampled tiles of this rank's C replica
+    # against a float64 host product (before the host-resident run below
+    # re-splits compute id 2 and overwrites the host copy)
+    err = _max_over_ranks(ctx, g.verify(compute_id=1))
+    timeouts = int(_sum_over_ranks(ctx, g.spin_timeouts()))
     host_steps = max(2, min(steps, 5))
     ms_host = timed(ctx, lambda: g.run(compute_id=2, resident=False), host_steps, 1)
-    ranges = cr.ranges(1)
-    timeouts = g.spin_timeouts()
-    if timeouts:
-        raise RuntimeError(f"GEMM {tile}: {timeouts} work-groups timed out waiting for their K-split partner")
     cr.dispose()
     for a in (g.A, g.B, g.C, g.dims):
         a.dispose()  # release 0.5 GB of pinned host memory before the next config
     return {"ms": ms, "gflops": g.flops / (ms * 1e-3) / 1e9, "tile": tile, "balancer_setup_calls": converge,
             "sync_per_step_ms": ms_sync, "sync_per_step_gflops": g.flops / (ms_sync * 1e-3) / 1e9,
             "host_resident_ms": ms_host, "host_resident_gflops": g.flops / (ms_host * 1e-3) / 1e9,
-            "ranges": ranges}
+            "ranges": ranges, "max_rel_err": err, "spin_timeouts": timeouts, "device": "gpu"}
+
+
+CPU_GEMM_SRC = """
+__global__ void gemm_nt(const int* d, const float* a, const float* b, float* c) {
+  long long i = get_global_id(0);
+  int n = d[1], k = d[2];
+  long long r = i / n, col = i % n;
+  float s = 0.0f;
+  for (int j = 0; j < k; ++j) s += a[r * k + j] * b[col * k + j];
+  c[i] = s;
+}
+"""
+
+
+def bench_sgemm_cpu(ctx, steps, warmup, size=256):
+    """GPU-less rehearsal of the headline: the same range-partitioned,
+    balanced compute() over one CPU device per rank (plain fp32 kernel
+    string, one work item per output element, C device-resident after the
+    first call).  Exercises the rank launcher, the shared-memory control
+    plane and the identical-split property, not the MI355X kernel."""
+    import cekirdekler_amd as ck
+    from cekirdekler_amd.parallel.distributed import DistributedCruncher
+
+    cr = DistributedCruncher(CPU_GEMM_SRC, ctx=ctx, devices=ck.ClPlatforms.all().cpus(True))
+    rng = np.random.default_rng(0)
+    dims = ck.ClArray(np.array([size, size, size, 0], np.int32))
+    a = ck.ClArray(rng.uniform(-1, 1, size * size).astype(np.float32))
+    b = ck.ClArray(rng.uniform(-1, 1, size * size).astype(np.float32))
+    c = ck.ClArray(np.zeros(size * size, np.float32))
+    for x in (dims, a, b):
+        x.write = False
+    c.read = False
+    n, local = size * size, 64
+
+    def step():
+        dims.next_param(a, b, c).compute(cr, 1, "gemm_nt", n, local)
+
+    converge = _converge(ctx, cr, step, compute_id=1)
+    ms = timed(ctx, step, steps, warmup)
+    ranges = cr.ranges(1)
+    lo = cr.references(1)[ctx.rank]
+    hi = lo + ranges[ctx.rank]
+    ref = (a.array.reshape(size, size).astype(np.float64) @ b.array.reshape(size, size).astype(np.float64).T).ravel()
+    err = float(np.max(np.abs(c.array[lo:hi] - ref[lo:hi])) / max(np.max(np.abs(ref)), 1e-30)) if hi > lo else 0.0
+    err = _max_over_ranks(ctx, err)
+    cr.dispose()
+    flops = 2.0 * size ** 3
+    return {"ms": ms, "gflops": flops / (ms * 1e-3) / 1e9, "tile": "cpu-naive", "balancer_setup_calls": converge,
+            "sync_per_step_ms": ms, "sync_per_step_gflops": flops / (ms * 1e-3) / 1e9,
+            "host_resident_ms": ms, "host_resident_gflops": flops / (ms * 1e-3) / 1e9,
+            "ranges": ranges, "max_rel_err": err, "spin_timeouts": 0, "device": "cpu"}
+
+
+def _all_ranges(ctx, ranges):
+    """Every rank's view of the split (they must be identical: each rank
+    derives it from the same exchanged timings)."""
+    if not ctx.is_distributed:
+        return [list(ranges)]
+    import torch.distributed as dist
+
+    out = [None] * ctx.world
+    dist.all_gather_object(out, list(ranges))
+    return out
 
 
 def bench_mandelbrot(ctx, steps, warmup):
@@ -229,31 +306,71 @@ def bench_node_configs(world: int) -> dict:
     return out
 
 
-def main(argv=None) -> int:
+MAX_REL_ERR = 5e-3
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Start ``n`` rank processes of this script through
+    ``torch.distributed.run`` (a child process, rendezvous on 127.0.0.1) and
+    return its exit code.  Called before anything imports the runtime, so
+    this process never initialises a GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd)
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size", type=int, default=8192)
     ap.add_argument("--tile", default=None)
+    ap.add_argument("--device", choices=("auto", "gpu", "cpu"), default="auto",
+                    help="cpu: kernel-string GEMM on each rank's CPU device (launcher rehearsal)")
     ap.add_argument("--skip-mandelbrot", action="store_true")
     ap.add_argument("--skip-node-configs", action="store_true",
                     help="skip the N-body pipeline and task-pool configs (rank 0, after the headline)")
-    args = ap.parse_args(argv)
+    return ap.parse_args(argv)
 
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, argv)
+
+    from cekirdekler_amd._native import gpu_available
     from cekirdekler_amd.parallel.distributed import init_distributed
 
     ctx = init_distributed()
-    sg = bench_sgemm(ctx, args.steps, args.warmup, args.size, args.tile)
-    mb = {} if args.skip_mandelbrot else bench_mandelbrot(ctx, args.steps, args.warmup)
-    lb = bench_lb_iters() if ctx.rank == 0 else {}
+    if ctx.world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the job has {ctx.world} ranks")
+    use_gpu = args.device == "gpu" or (args.device == "auto" and gpu_available())
+    if use_gpu:
+        sg = bench_sgemm(ctx, args.steps, args.warmup, args.size, args.tile)
+    else:
+        sg = bench_sgemm_cpu(ctx, args.steps, args.warmup, min(args.size, 512))
+    all_ranges = _all_ranges(ctx, sg["ranges"])
+    mb = {} if (args.skip_mandelbrot or not use_gpu) else bench_mandelbrot(ctx, args.steps, args.warmup)
+    lb = bench_lb_iters() if (ctx.rank == 0 and use_gpu) else {}
     if ctx.is_distributed:
         import torch.distributed as dist
 
         dist.barrier()
         dist.destroy_process_group()  # the other ranks exit here; rank 0 goes on alone
-    node = {} if (ctx.rank != 0 or args.skip_node_configs) else bench_node_configs(ctx.world)
+    node = {} if (ctx.rank != 0 or args.skip_node_configs or not use_gpu) else bench_node_configs(ctx.world)
+    ok = sg["max_rel_err"] <= MAX_REL_ERR and sg["spin_timeouts"] == 0
     if ctx.rank == 0:
+        size = args.size if use_gpu else min(args.size, 512)
         out = {
             "metric": METRIC,
             "value": round(sg["gflops"], 1),
@@ -265,18 +382,23 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if use_gpu else "fp32",
             "data": "synthetic",
-            "config": {"model": f"SGEMM {args.size}x{args.size}x{args.size} bf16 (fp32 acc/out), "
+            "config": {"model": f"SGEMM {size}x{size}x{size} {'bf16' if use_gpu else 'fp32'} (fp32 acc/out), "
                                 f"range-partitioned + load-balanced, tile {sg['tile']}",
-                       "global_batch": 1, "seq_len": args.size,
-                       "parallelism": f"range-partition dp{ctx.world}"},
+                       "global_batch": 1, "seq_len": size,
+                       "parallelism": f"range-partition dp{ctx.world}",
+                       "device": sg["device"]},
             "extra": {
                 "sgemm_device_resident_gflops": round(sg["gflops"], 1),
                 "sgemm_sync_per_step_gflops": round(sg["sync_per_step_gflops"], 1),
                 "sgemm_host_resident_gflops": round(sg["host_resident_gflops"], 1),
                 "sgemm_host_resident_ms": round(sg["host_resident_ms"], 3),
+                "sgemm_max_rel_err": sg["max_rel_err"],
+                "sgemm_spin_timeouts": sg["spin_timeouts"],
+                "sgemm_balancer_setup_calls": sg["balancer_setup_calls"],
                 "sgemm_ranges": sg["ranges"],
+                "sgemm_ranges_identical_on_all_ranks": all(r == all_ranges[0] for r in all_ranges),
                 "mandelbrot_4k": mb,
                 "load_balance_iters": lb,
                 "nbody_pipeline": node.get("nbody_pipeline"),
@@ -284,7 +406,10 @@ def main(argv=None) -> int:
             },
         }
         print(json.dumps(out), flush=True)
-    return 0
+        if not ok:
+            print(f"bench.py: SGEMM output check failed: max rel err {sg['max_rel_err']:.3e} "
+                  f"(limit {MAX_REL_ERR}), {sg['spin_timeouts']} spin timeouts", file=sys.stderr, flush=True)
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":

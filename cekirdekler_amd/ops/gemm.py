@@ -227,6 +227,41 @@ class GemmBf16:
             total += int(self.counters.array[-1])
         return total
 
+    def verify(self, compute_id: int = 1, tiles_per_device: int = 8, seed: int = 1) -> float:
+        """Max relative error of the device-resident C of ``compute_id``
+        against a float64 host product, over sampled output tiles of this
+        process's devices' ranges: the first and last tile of each range plus
+        random ones.  Relative to ``max |ref|`` of each tile.  Downloads each
+        local device's C replica (device memory is not changed)."""
+        ranges = self.cr.ranges(compute_id)
+        refs = self.cr.references(compute_id)
+        unit = self.L * self.split_k
+        a = from_bf16_bits(self.A.array).reshape(self.M, self.K) if self.A.array.dtype == np.uint16 else (
+            self.A.array.reshape(self.M, self.K))
+        b = from_bf16_bits(self.B.array).reshape(self.N, self.K) if self.B.array.dtype == np.uint16 else (
+            self.B.array.reshape(self.N, self.K))
+        rng = np.random.default_rng(seed)
+        saved = self.C.array.copy()
+        worst = 0.0
+        tile = self.BM * self.BN
+        for dev in range(self.cr._cores.num_devices):
+            g = self.cr._cores.global_base + dev
+            t0, nt = refs[g] // unit, ranges[g] // unit
+            if nt == 0:
+                continue
+            self.cr.download(self.C, dev)
+            picks = {t0, t0 + nt - 1}
+            picks.update((t0 + rng.choice(nt, size=min(nt, tiles_per_device), replace=False)).tolist())
+            picks = np.array(sorted(picks))
+            tm, tn = tile_coords(picks, self.M, self.N, self.BM, self.BN, self.group_m)
+            for t, r, c in zip(picks, tm, tn):
+                got = self.C.array[t * tile:(t + 1) * tile].reshape(self.BM, self.BN).astype(np.float64)
+                ref = (a[r * self.BM:(r + 1) * self.BM].astype(np.float64)
+                       @ b[c * self.BN:(c + 1) * self.BN].astype(np.float64).T)
+                worst = max(worst, float(np.max(np.abs(got - ref)) / max(float(np.max(np.abs(ref))), 1e-30)))
+        self.C.array[:] = saved
+        return worst
+
     def _download_slice(self, dev: int, lo: int, n: int) -> None:
         # a sub-view ClArray sharing the same uid would alias buffers; the
         # native download copies the whole replica, slice afterwards

@@ -242,3 +242,27 @@ def test_gemm_f32_matches_fp64(tile, shape):
     c = g.result(download=False)
     ref = g.reference()
     assert np.abs(c - ref).max() < 1e-4 * np.sqrt(K) * max(1.0, np.abs(ref).max())
+
+
+@pytest.mark.parametrize("tile,rows", [("256x256pb", 8192), ("256x256pby", 1024)])
+def test_gemm_benchmarked_size_verify(tile, rows):
+    """The headline kernels at the benchmarked size: the full 8192³ problem
+    (N = 1) and the 1024-row slice one GPU of eight computes, device-resident
+    through compute() in enqueue mode as bench.py times it, checked by
+    GemmBf16.verify (sampled tiles vs a float64 host product)."""
+    from cekirdekler_amd.ops.gemm import GEMM_LIBS, GemmBf16
+    from cekirdekler_amd.ops.library import library
+
+    cr = ck.ClNumberCruncher(_gpu()[0], "", prebuilt=library(*GEMM_LIBS))
+    g = GemmBf16(rows, 8192, 8192, cruncher=cr, tile=tile)
+    g.run(compute_id=1, resident=True)
+    cr.enqueue_mode = True
+    for _ in range(5):
+        g.run(compute_id=1, resident=True)
+    cr.enqueue_mode = False
+    err = g.verify(compute_id=1, tiles_per_device=6)
+    assert err < 5e-3, err
+    assert g.spin_timeouts() == 0
+    cr.dispose()
+    for a in (g.A, g.B, g.C, g.dims):
+        a.dispose()
