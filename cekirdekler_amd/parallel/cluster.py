@@ -154,12 +154,8 @@ class ClCruncherServerThread(threading.Thread):
             if a is None or len(a) != r.length or a.dtype != r.data.dtype.newbyteorder("="):
                 a = np.zeros(r.length, r.data.dtype.newbyteorder("="))
                 self.arrays[r.hash] = a
-            if r.partial:
-                a[r.ref * e:(r.ref + r.range) * e] = r.data
-            elif r.range != 0 and len(r.data) == r.length:
-                a[:] = r.data
+            r.scatter_into(a)
             arrays.append(a)
-        ans = NetworkBuffer(nbm.ANSWER_COMPUTE_COMPLETE)
         try:
             # ranges are absolute: the node computes [off, off+G) of the global range
             self.cores.compute(names, steps, step_fn, arrays, rws, epw, G, cid, off, pipe, blobs, ptype)
@@ -167,15 +163,24 @@ class ClCruncherServerThread(threading.Thread):
             err = NetworkBuffer(nbm.ANSWER_ERROR)
             err.add_string(str(e))
             return err
-        for a, r, e, rw in zip(arrays, arr_recs, epw, rws):
-            if a.dtype == np.float32:
-                if "write" in rw.split():
-                    ans.add_array(a, r.hash, off, G, e)
-                else:
-                    ans.add_array(a[:0], r.hash, 0, 0, e)
+        return answer_message(arrays, [r.hash for r in arr_recs], rws, epw, G, off)
+
+
+def answer_message(arrays, hashes, read_writes, epw, global_range: int, global_offset: int) -> NetworkBuffer:
+    """ANSWER_COMPUTE_COMPLETE (reference ClCruncherServerThread.cs:192-210):
+    float arrays return the node's slice ``[off·e, (off+G)·e)`` as a partial
+    record; other types return whole.  Float arrays the kernel does not
+    write come back as header-only partial records (range 0)."""
+    ans = NetworkBuffer(nbm.ANSWER_COMPUTE_COMPLETE)
+    for a, h, rw, e in zip(arrays, hashes, read_writes, epw):
+        if a.dtype == np.float32:
+            if "write" in rw.split():
+                ans.add_array(a, h, global_offset, global_range, e)
             else:
-                ans.add_array(a, r.hash)
-        return ans
+                ans.add_array(a, h, 0, 0, e)
+        else:
+            ans.add_array(a, h)
+    return ans
 
 
 class ClCruncherServer:
@@ -242,6 +247,63 @@ class ClCruncherServer:
 # --------------------------------------------------------------------------- client
 
 
+def setup_message(device_types: str, kernels: str, kernel_names, local_range: int = 256, num_gpus: int = -1,
+                  stream: bool = True, max_cpu: int = -1) -> NetworkBuffer:
+    """SETUP: device types, kernel source and names (UTF-16 char records),
+    local range and GPU count (int), stream (bool), max CPU (int) — the
+    record order of ClCruncherClient.cs:121-153."""
+    nb = NetworkBuffer(nbm.SETUP)
+    nb.add_string(device_types)
+    nb.add_string(kernels)
+    nb.add_string(" ".join(kernel_names) if not isinstance(kernel_names, str) else kernel_names)
+    nb.add_ints([local_range])
+    nb.add_ints([num_gpus])
+    nb.add_array(np.array([stream], np.bool_), 0)
+    nb.add_ints([max_cpu])
+    return nb
+
+
+def compute_message(kernel_names: str, steps: int, step_fn: str, arrays, hashes, read_writes, epw,
+                    global_range: int, compute_id: int, global_offset: int = 0, pipeline: bool = False,
+                    blobs: int = 4, pipeline_type: bool = True) -> NetworkBuffer:
+    """COMPUTE (ClCruncherClient.cs:155-256): names, steps, step function,
+    array count, the array records, one read/write string per array, then
+    elements-per-work-item, global range, compute id, offset, pipeline flag,
+    blob count and pipeline type.
+
+    Array records: ``partial`` float arrays carry the node's slice and
+    ``read`` arrays carry the whole array, as the reference sends them.  The
+    reference client omits every other array, which its own server cannot
+    parse (it indexes the records by position, ClCruncherServerThread.cs:
+    147-175, so the read/write strings shift).  Here such a float array is a
+    header-only partial record (range 0: hash and length, no payload), which
+    the reference parser reads as an empty copy; a non-float one, which has
+    no range field in the layout, is sent whole."""
+    nb = NetworkBuffer(nbm.COMPUTE)
+    nb.add_string(kernel_names)
+    nb.add_ints([steps])
+    nb.add_string(step_fn or "")
+    nb.add_ints([len(arrays)])
+    for a, h, rw, e in zip(arrays, hashes, read_writes, epw):
+        toks = rw.split()
+        if a.dtype == np.float32 and "partial" in toks:
+            nb.add_array(a, h, global_offset, global_range, e)
+        elif "read" in toks or a.dtype != np.float32:
+            nb.add_array(a, h)
+        else:
+            nb.add_array(a, h, 0, 0, e)
+    for rw in read_writes:
+        nb.add_string(rw)
+    nb.add_ints(list(epw))
+    nb.add_ints([global_range])
+    nb.add_ints([compute_id])
+    nb.add_ints([global_offset])
+    nb.add_array(np.array([pipeline], np.bool_), 0)
+    nb.add_ints([blobs])
+    nb.add_array(np.array([pipeline_type], np.bool_), 0)
+    return nb
+
+
 class ClCruncherClient:
     """Client of one compute server (reference ClCruncherClient.cs:29-325)."""
 
@@ -258,15 +320,8 @@ class ClCruncherClient:
 
     def net_setup(self, device_types: str, kernels: str, kernel_names, local_range: int = 256,
                   num_gpus: int = -1, stream: bool = True, max_cpu: int = -1) -> bool:
-        nb = NetworkBuffer(nbm.SETUP)
-        nb.add_string(device_types)
-        nb.add_string(kernels)
-        nb.add_string(" ".join(kernel_names) if not isinstance(kernel_names, str) else kernel_names)
-        nb.add_ints([local_range])
-        nb.add_ints([num_gpus])
-        nb.add_array(np.array([stream], np.bool_), 0)
-        nb.add_ints([max_cpu])
-        cmd, recs = self._rpc(nb)
+        cmd, recs = self._rpc(setup_message(device_types, kernels, kernel_names, local_range, num_gpus,
+                                            stream, max_cpu))
         if cmd != nbm.ANSWER_SUCCESS:
             raise RuntimeError("server setup failed: " + (NetworkBuffer.record_string(recs[0]) if recs else ""))
         return True
@@ -280,40 +335,15 @@ class ClCruncherClient:
         writes the returned slices into ``arrays``.  Returns wall ms."""
         t0 = time.perf_counter()
         nps = [_as_np(a) for a in arrays]
-        nb = NetworkBuffer(nbm.COMPUTE)
-        nb.add_string(kernel_names)
-        nb.add_ints([steps])
-        nb.add_string(step_fn or "")
-        nb.add_ints([len(nps)])
-        for a, rw, e in zip(nps, read_writes, epw):
-            h = self._hash.setdefault(id(a), len(self._hash) + 1)
-            toks = rw.split()
-            if a.dtype == np.float32:
-                if "partial" in toks:
-                    nb.add_array(a, h, global_offset, global_range, e)
-                elif "read" in toks:
-                    nb.add_array(a, h)
-                else:
-                    nb.add_array(a, h, 0, 0, e)
-            else:
-                nb.add_array(a, h)
-        for rw in read_writes:
-            nb.add_string(rw)
-        nb.add_ints(list(epw))
-        nb.add_ints([global_range])
-        nb.add_ints([compute_id])
-        nb.add_ints([global_offset])
-        nb.add_array(np.array([pipeline], np.bool_), 0)
-        nb.add_ints([blobs])
-        nb.add_array(np.array([pipeline_type], np.bool_), 0)
+        hashes = [self._hash.setdefault(id(a), len(self._hash) + 1) for a in nps]
+        nb = compute_message(kernel_names, steps, step_fn, nps, hashes, read_writes, epw, global_range,
+                             compute_id, global_offset, pipeline, blobs, pipeline_type)
         cmd, recs = self._rpc(nb)
         if cmd == nbm.ANSWER_ERROR:
             raise RuntimeError("server compute failed: " + NetworkBuffer.record_string(recs[0]))
-        for a, r, e, rw in zip(nps, recs, epw, read_writes):
-            if r.partial and r.range > 0:
-                a[r.ref * e:(r.ref + r.range) * e] = r.data
-            elif not r.partial and r.range != 0 and "write" in rw.split() and len(r.data) == len(a):
-                a[:] = r.data
+        for a, r, rw in zip(nps, recs, read_writes):
+            if r.partial or "write" in rw.split():
+                r.scatter_into(a)
         return (time.perf_counter() - t0) * 1e3
 
     def control(self) -> bool:
@@ -351,18 +381,70 @@ class ClCruncherClient:
 
 
 def find_servers(candidates: Sequence[str], ports: Sequence[int], timeout: float = 0.3) -> List[tuple]:
-    """Probe ``host`` × ``port`` candidates with the CONTROL handshake."""
-    found = []
-    for host in candidates:
-        for port in ports:
-            try:
-                c = ClCruncherClient(port, host, timeout=timeout)
-            except OSError:
-                continue
-            if c.control():
-                found.append((host, port))
+    """Probe ``host`` × ``port`` candidates with the CONTROL handshake, in
+    parallel (the reference pings then tests each address from a
+    ``Parallel.For``, ClusterAccelerator.cs:77-154).  Returns the answering
+    ``(host, port)`` pairs in candidate order."""
+    pairs = [(h, p) for p in ports for h in candidates]
+    ok = [False] * len(pairs)
+
+    def probe(i):
+        host, port = pairs[i]
+        try:
+            c = ClCruncherClient(port, host, timeout=timeout)
+        except OSError:
+            return
+        try:
+            ok[i] = c.control()
+        finally:
             c.sock.close()
-    return found
+
+    threads = [threading.Thread(target=probe, args=(i,), daemon=True) for i in range(len(pairs))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    return [pr for pr, good in zip(pairs, ok) if good]
+
+
+def parse_cluster_devices(device_types: str) -> dict:
+    """The reference's cluster device string (ClusterAccelerator.cs:364-443),
+    e.g. ``"gpu cluster:50000,50001 fast-search node0_g"``:
+
+    * ``cluster:P[,P...]`` — server ports to search (required);
+    * ``fast-search`` — probe only the first 9 addresses of the sweep;
+    * ``node0_g`` / ``node0_c`` — the local mainframe node computes on the
+      GPU / the CPU (none otherwise);
+    * ``gpu`` / ``cpu`` / ``acc`` anywhere in the string — the device types
+      every server is set up with (the mainframe tokens count, as in the
+      reference's substring test)."""
+    s = device_types.lower()
+    if "cluster:" not in s:
+        raise ValueError("cluster device string needs 'cluster:PORT[,PORT]'")
+    tail = s.split("cluster:", 1)[1].strip().split("port")[0].strip()
+    ports = [int(p) for p in tail.split()[0].split(",") if p.strip()] if tail else []
+    if not ports:
+        raise ValueError("cluster device string needs at least one port after 'cluster:'")
+    mainframe = "gpu" if "node0_g" in s else ("cpu" if "node0_c" in s else None)
+    server = "".join(t for t in ("gpu", "cpu", "acc") if t in s)
+    return {"ports": ports, "fast_search": "fast-search" in s, "mainframe": mainframe, "server_devices": server}
+
+
+def sweep_candidates(fast: bool) -> List[str]:
+    """Addresses the discovery sweep probes: the loopback, plus
+    ``<prefix>1 .. <prefix>254`` (``fast``: 1..9) when ``CEK_CLUSTER_SUBNET``
+    names a prefix such as ``192.168.1.`` (the reference's fixed LAN,
+    ClusterAccelerator.cs:80-86), plus any hosts in ``CEK_CLUSTER_HOSTS``
+    (comma separated)."""
+    import os
+
+    out = ["127.0.0.1"]
+    prefix = os.environ.get("CEK_CLUSTER_SUBNET", "")
+    if prefix:
+        out += [f"{prefix}{i}" for i in range(1, 10 if fast else 255)]
+    out += [h.strip() for h in os.environ.get("CEK_CLUSTER_HOSTS", "").split(",") if h.strip()]
+    seen = set()
+    return [h for h in out if not (h in seen or seen.add(h))]
 
 
 class ClusterAccelerator(IComputeNode):
@@ -374,8 +456,31 @@ class ClusterAccelerator(IComputeNode):
         self.balancer = ClusterLoadBalancer()
         self._state = {}
         self.last_ms: List[float] = []
+        self.discovered: List[tuple] = []
 
-    def setup_nodes(self, nodes: Sequence[tuple], device_types: str, kernels: str, kernel_names=None,
+    def setup_nodes(self, nodes, *args, **kwargs) -> None:
+        """``nodes`` is an explicit ``[(host, port), ...]`` list (then
+        ``device_types, kernels, kernel_names, local_range, num_gpus, stream,
+        max_cpu, mainframe_types``), or the reference's device string, which
+        goes to :meth:`setup_cluster` with the reference's argument order."""
+        if isinstance(nodes, str):
+            return self.setup_cluster(nodes, *args, **kwargs)
+        return self._setup_list(nodes, *args, **kwargs)
+
+    def setup_cluster(self, device_types: str, kernels: str = "", kernel_names=None, local_range: int = 256,
+                      num_gpus: int = -1, stream: bool = True, max_cpu: int = -1) -> None:
+        """Reference ``setupNodes(deviceTypes, kernelsString, kernelNames, L,
+        nGPU, stream, maxCPU)`` (ClusterAccelerator.cs:364-443): parses
+        ``device_types`` (:func:`parse_cluster_devices`), finds the servers
+        on the given ports with the discovery sweep
+        (:func:`sweep_candidates`), sets every server up with the string's
+        device types and builds the ``node0_g``/``node0_c`` mainframe."""
+        spec = parse_cluster_devices(device_types)
+        self.discovered = find_servers(sweep_candidates(spec["fast_search"]), spec["ports"])
+        self._setup_list(self.discovered, spec["server_devices"] or "gpu", kernels, kernel_names, local_range,
+                         num_gpus, stream, max_cpu, spec["mainframe"])
+
+    def _setup_list(self, nodes: Sequence[tuple], device_types: str, kernels: str, kernel_names=None,
                     local_range: int = 256, num_gpus: int = -1, stream: bool = True, max_cpu: int = -1,
                     mainframe_types: Optional[str] = None) -> None:
         from ..cruncher import Cores
@@ -389,7 +494,7 @@ class ClusterAccelerator(IComputeNode):
             self.mainframe = Cores(mainframe_types, kernels, names, False, local_range, num_gpus, stream, max_cpu)
         self.local_range = local_range
 
-    setupNodes = setup_nodes
+    setupNodes = setup_cluster
 
     def compute(self, kernel_names: str, steps: int, step_fn: str, arrays, read_writes, epw,
                 global_range: int, compute_id: int, global_offset: int = 0, pipeline: bool = False,

@@ -12,7 +12,14 @@ Layout (little-endian)::
 
     record = type u8 | hash i32 | length i32 | [ref i32 | range i32]  (float only)
              | payload (length elements, or `range` elements for a partial
-             float record: elements [ref·e, (ref+range)·e) of the array)
+             float record: elements [ref, ref+range) of the array)
+
+A partial float record carries element units on the wire, as the reference
+writes them (``addArray(float[])`` multiplies the work-item offset and range
+by elements-per-work-item, NetworkBuffer.cs:764-790, and ``oku`` advances
+``menzil·4`` bytes, :182): ``add_array(a, h, ref, range_, epw)`` takes work
+items and writes ``ref·epw`` / ``range_·epw``, and :meth:`NetworkBuffer.parse`
+needs nothing out of band.
 
 Element types: 0=byte 1=char(16-bit) 2=int32 3=float32 4=int64 5=float64
 6=bool.  This layout is used for the cluster wire protocol
@@ -70,10 +77,18 @@ class Record:
     type: int
     hash: int
     length: int          # elements of the whole array
-    ref: int = 0         # partial float records: first work item
-    range: int = -1      # partial float records: work items carried (-1 = all)
-    epw: int = 1         # elements per work item (not on the wire; caller supplies)
+    ref: int = 0         # partial float records: first element
+    range: int = -1      # partial float records: elements carried (-1 = all)
     data: Optional[np.ndarray] = None
+
+    def scatter_into(self, a: np.ndarray) -> None:
+        """Writes the record's payload into ``a`` where the sender took it
+        from (element offset ``ref``; the whole array for a full record)."""
+        if self.partial:
+            if self.range > 0:
+                a[self.ref:self.ref + self.range] = self.data
+        elif len(self.data) == len(a):
+            a[:] = self.data
 
     @property
     def partial(self) -> bool:
@@ -96,8 +111,9 @@ class NetworkBuffer:
             a = a.astype(np.uint8)
         head = struct.pack("<Bii", t, _i32(hash_), len(a))
         if t == TYPE_FLOAT:
-            head += struct.pack("<ii", int(ref), int(range_))
-            payload = a[ref * epw:(ref + range_) * epw] if range_ != -1 else a
+            lo, n = (int(ref) * epw, int(range_) * epw) if range_ != -1 else (0, -1)
+            head += struct.pack("<ii", lo, n)
+            payload = a[lo:lo + n] if n != -1 else a
         else:
             if range_ != -1:
                 raise ValueError("partial records exist only for float arrays (reference layout)")
@@ -132,9 +148,8 @@ class NetworkBuffer:
         return struct.unpack_from("<i" if b[8] == 0 else ">i", b, 9)[0]
 
     @staticmethod
-    def parse(b: bytes, epws: Optional[List[int]] = None):
-        """Returns (command, [Record]).  ``epws`` gives elements-per-work-item
-        of partial float records in order (default 1)."""
+    def parse(b: bytes):
+        """Returns (command, [Record])."""
         if b[:8] != MAGIC:
             raise ValueError("not a Cekirdekler NetworkBuffer")
         e = "<" if b[8] == 0 else ">"
@@ -142,7 +157,6 @@ class NetworkBuffer:
         mv = memoryview(b)
         i = HEADER
         out: List[Record] = []
-        k = 0
         while i < total:
             t = b[i]
             h, n = struct.unpack_from(e + "ii", b, i + 1)
@@ -151,15 +165,13 @@ class NetworkBuffer:
             if t == TYPE_FLOAT:
                 ref, rng = struct.unpack_from(e + "ii", b, i)
                 i += 8
-            epw = epws[k] if (epws and k < len(epws)) else 1
             dt = np.dtype(_TYPE_DTYPE[t] if t != TYPE_BOOL else np.uint8).newbyteorder(e)
-            count = n if rng == -1 else rng * epw
+            count = n if rng == -1 else rng
             data = np.frombuffer(mv[i:i + count * dt.itemsize], dtype=dt)
             if t == TYPE_BOOL:
                 data = data.astype(np.bool_)
-            out.append(Record(t, h, n, ref, rng, epw, data))
+            out.append(Record(t, h, n, ref, rng, data))
             i += count * dt.itemsize
-            k += 1
         return command, out
 
     @staticmethod
