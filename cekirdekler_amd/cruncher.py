@@ -419,7 +419,29 @@ class ClNumberCruncher:
         r = self._cores.last_record()
         return {"compute_id": r.compute_id, "wall_ms": r.wall_ms, "ranges": list(r.ranges),
                 "references": list(r.references), "device_ms": list(r.device_ms),
-                "h2d_bytes": r.h2d_bytes, "d2h_bytes": r.d2h_bytes, "pipelined": r.pipelined}
+                "h2d_bytes": r.h2d_bytes, "d2h_bytes": r.d2h_bytes, "p2p_bytes": r.p2p_bytes,
+                "pipelined": r.pipelined}
+
+    # ------------------------------------------------------------ xGMI read fan-out
+    @property
+    def peer_reads(self) -> bool:
+        """Full ``read`` arrays (≥ ``peer_read_min_bytes``, not written by the
+        kernels) are uploaded 1/D per local GPU and all-gathered GPU↔GPU
+        with peer copies over xGMI instead of D whole PCIe uploads (default
+        on; reference behaviour — one upload per device — when off)."""
+        return bool(self._cores.peer_reads) if self._cores else False
+
+    @peer_reads.setter
+    def peer_reads(self, on: bool) -> None:
+        self._cores.peer_reads = bool(on)
+
+    @property
+    def peer_read_min_bytes(self) -> int:
+        return int(self._cores.peer_read_min_bytes) if self._cores else 0
+
+    @peer_read_min_bytes.setter
+    def peer_read_min_bytes(self, n: int) -> None:
+        self._cores.peer_read_min_bytes = int(n)
 
     # ------------------------------------------------------------ compute
     def _validate(self, group: ClParameterGroup, names, G, L, pipeline, blobs) -> None:

@@ -5,6 +5,7 @@
 #include <pybind11/stl.h>
 
 #include "balancer.h"
+#include "copy_engine.h"
 #include "cores.h"
 #include "device.h"
 #include "dist.h"
@@ -103,6 +104,19 @@ PYBIND11_MODULE(_cek, m) {
     }
     CEK_HIP(hipMemcpy(reinterpret_cast<void*>(d), reinterpret_cast<const void*>(s), n, hipMemcpyDefault));
   });
+  py::class_<CopyEngine>(m, "CopyEngine")
+      .def(py::init<>())
+      .def("copy", [](CopyEngine& e, uint64_t d, int dd, uint64_t s, int sd, uint64_t n) {
+        e.copy(reinterpret_cast<void*>(d), dd, reinterpret_cast<const void*>(s), sd, n);
+      }, py::arg("dst"), py::arg("dst_dev"), py::arg("src"), py::arg("src_dev"), py::arg("bytes"),
+         py::call_guard<py::gil_scoped_release>())
+      .def("sync", &CopyEngine::sync, py::call_guard<py::gil_scoped_release>())
+      .def("reset_counters", &CopyEngine::reset_counters)
+      .def_readonly("p2p_bytes", &CopyEngine::p2p_bytes)
+      .def_readonly("h2d_bytes", &CopyEngine::h2d_bytes)
+      .def_readonly("d2h_bytes", &CopyEngine::d2h_bytes)
+      .def_readonly("host_bytes", &CopyEngine::host_bytes)
+      .def_readonly("copies", &CopyEngine::copies);
   m.def("device_synchronize", [](int ordinal) {
     py::gil_scoped_release r;
     if (gpu_count() == 0) return;
@@ -196,6 +210,7 @@ PYBIND11_MODULE(_cek, m) {
       .def_readonly("device_ms", &ComputeRecord::device_ms)
       .def_readonly("h2d_bytes", &ComputeRecord::h2d_bytes)
       .def_readonly("d2h_bytes", &ComputeRecord::d2h_bytes)
+      .def_readonly("p2p_bytes", &ComputeRecord::p2p_bytes)
       .def_readonly("pipelined", &ComputeRecord::pipelined);
 
   py::class_<Exchanger, PyExchanger, std::shared_ptr<Exchanger>>(m, "Exchanger")
@@ -255,6 +270,8 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("fine_grained", &Cores::fine_grained)
       .def_readwrite("smooth", &Cores::smooth)
       .def_readwrite("serial", &Cores::serial)
+      .def_readwrite("peer_reads", &Cores::peer_reads)
+      .def_readwrite("peer_read_min_bytes", &Cores::peer_read_min_bytes)
       .def_readwrite("graph_min_launches", &Cores::graph_min_launches)
       .def_readwrite("auto_failover", &Cores::auto_failover)
       .def_readwrite("record_schedule", &Cores::record_schedule)

@@ -62,6 +62,7 @@ struct ComputeRecord {  // structured per-call record (observability)
   std::vector<long long> ranges, references;
   std::vector<double> device_ms;
   uint64_t h2d_bytes = 0, d2h_bytes = 0;
+  uint64_t p2p_bytes = 0;  // device→device (xGMI peer) bytes of the read fan-out
   bool pipelined = false;
 };
 
@@ -251,6 +252,18 @@ class Cores {
   bool dist_split_reads = false;
   int global_base() const { return global_base_; }
 
+  // ---- xGMI fan-out of full `read` arrays ----
+  // The reference uploads every `read` array to every device
+  // (Worker.cs:833-860): D PCIe copies contending for the host.  With two or
+  // more local GPUs computing, an array of at least peer_read_min_bytes that
+  // the kernels do not write is instead uploaded 1/D per GPU (each over its
+  // own PCIe link) and every GPU pulls the other D-1 chunks straight from its
+  // peers' replicas with hipMemcpyPeerAsync: an all-gather over the
+  // point-to-point xGMI mesh, one link per peer pair, ordered by events (no
+  // host sync).  PCIe carries the array once instead of D times.
+  bool peer_reads = true;
+  uint64_t peer_read_min_bytes = 1u << 20;
+
  private:
   PhaseBarrier* phase_ = nullptr;  // set while a hazardous compute runs
   void run_device(int w, const ComputeCall& c, long long ref, long long range, bool pipelined,
@@ -275,6 +288,18 @@ class Cores {
   std::mutex tl_mu_;
   std::vector<PendingSpan> pending_spans_;
   void full_reads(Worker& wk, hipStream_t s, const ComputeCall& c, uint64_t* h2d);
+  // per-call peer fan-out: which arrays were staged, and per local worker the
+  // event its streams wait on before using them
+  struct PeerEvents {
+    hipEvent_t up = nullptr;      // this GPU's chunk uploaded
+    hipEvent_t pulled = nullptr;  // every other chunk pulled into this GPU
+  };
+  std::vector<PeerEvents> peer_ev_;
+  std::vector<char> staged_arr_;  // by array index, for the current call
+  std::vector<char> staged_dev_;  // by local worker, for the current call
+  uint64_t stage_peer_reads(const ComputeCall& c, const std::vector<long long>& ranges,
+                            std::vector<uint64_t>& h2d);
+  int worker_index(const Worker& wk) const;
 
   std::vector<std::unique_ptr<Worker>> workers_;
   std::map<int, BalancerState> state_;

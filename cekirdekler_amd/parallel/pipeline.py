@@ -10,10 +10,15 @@ Results appear after ~2·stages pushes (same ready-counter rule as the
 reference, :114-124).
 
 MI355X-native difference: the reference moves every stage transition
-device→host→device (ClPipeline.cs:1422-1574).  Here a single-device stage
-keeps its buffers device-resident and forwards output→next input with a
-unified-address device→device copy (xGMI peer copy between GPUs, no host
-bounce); only multi-device stages fall back to host staging.
+device→host→device (ClPipeline.cs:1422-1574).  Here every stage keeps its
+buffers resident on each of its devices (a CPU device's "replica" is the
+host array itself).  A stage transition is a set of async copies on the
+native :class:`CopyEngine`: each device of the next stage pulls every slice
+of the previous stage's output straight from the device that computed it
+(``hipMemcpyPeerAsync`` over that GPU pair's xGMI link), so a multi-device
+stage never bounces through host memory.  Slice ownership follows the
+balancer split of the stage's last kernel, snapshotted when the push that
+wrote the output ended.  Only pipeline inputs and results cross PCIe.
 
 **Single-device multi-queue pipeline** (reference ``DevicePipeline`` /
 ``DevicePipelineStage`` / ``DevicePipelineArray(Type)``,
@@ -156,29 +161,50 @@ class ClPipelineStage:
         self.cruncher = ClNumberCruncher(self.devices, self.kernel_source, no_pipelining=True)
         if self.cruncher.error_code():
             raise RuntimeError(f"stage {self.stage_id} build failed:\n{self.cruncher.error_message()}")
-        self._resident = len(self.devices) == 1
-        if self._resident and self.devices.device(0).is_gpu:
+        self._resident = True
+        self._ordinals = [d.info.ordinal if d.is_gpu else -1 for d in self.devices]
+        if any(o >= 0 for o in self._ordinals):
             _enable_peers()
         self._in_dup = [_clone(a) for a in self.inputs]
         self._out_dup = [_clone(a) for a in self.outputs]
-        for a in self.inputs + self._in_dup:
-            a.write, a.partial_read = False, False
-            a.read = not self._resident
-        for a in self.outputs + self._out_dup:
-            a.read, a.partial_read = False, False
-            a.write = not self._resident
-        for a in self.hiddens:
+        for a in self.inputs + self._in_dup + self.outputs + self._out_dup + self.hiddens:
             a.read, a.partial_read, a.write = False, False, False
-        if self._resident:
-            # materialise every replica with the host contents once
-            for a in self.inputs + self._in_dup + self.outputs + self._out_dup + self.hiddens:
-                self.cruncher.upload(a, 0)
-        else:
-            # hidden buffers never move per push; every device's replica starts
-            # from the host contents (constants, initial state), as above
-            for a in self.hiddens:
-                for d in range(self.cruncher.cores.num_devices):
-                    self.cruncher.upload(a, d)
+        # materialise every replica with the host contents once (constants,
+        # initial state); from here on nothing moves except by the pipeline
+        for a in self.inputs + self._in_dup + self.outputs + self._out_dup + self.hiddens:
+            for d in range(len(self._ordinals)):
+                self.cruncher.upload(a, d)
+        self._owner = None      # (refs, ranges, local) of the output's writer
+        self._owner_next = None
+
+    def _snapshot_owner(self) -> None:
+        """Record which device computed which slice of this push's outputs
+        (the split of the stage's last kernel, compute id ``len(kernels)``)."""
+        if len(self._ordinals) == 1 or not self.kernel_names:
+            self._owner_next = None
+            return
+        cid = len(self.kernel_names)
+        self._owner_next = (self.cruncher.references(cid), self.cruncher.ranges(cid), self.local_ranges[-1])
+
+    def _slices(self, a: ClArray):
+        """(device, byte offset, bytes) of every device's slice of output
+        ``a`` as last written; one whole-array slice from device 0 for a
+        single-device stage or before the first push."""
+        if self._owner is None:
+            return [(0, 0, a.nbytes)]
+        refs, ranges, local = self._owner
+        item = a.nbytes // max(a.N, 1)
+        out = []
+        for d, (r, n) in enumerate(zip(refs, ranges)):
+            if a.elements_per_group:
+                b, c = (r // local) * a.elements_per_group, (n // local) * a.elements_per_group
+            else:
+                b, c = r * a.elements_per_work_item, n * a.elements_per_work_item
+            b, c = min(b * item, a.nbytes), c * item
+            c = max(0, min(c, a.nbytes - b))
+            if c:
+                out.append((d, b, c))
+        return out
 
     def _group(self, dup: bool) -> ClParameterGroup:
         ins = self._in_dup if dup else self.inputs
@@ -198,8 +224,8 @@ class ClPipelineStage:
             g.compute(self.cruncher, 1 + i, k, G, L)
         self.elapsed_time = (time.perf_counter() - t0) * 1e3
 
-    def _replica_ptr(self, a: ClArray) -> int:
-        return self.cruncher.device_pointer(a, 0)
+    def _replica_ptr(self, a: ClArray, device: int = 0) -> int:
+        return self.cruncher.device_pointer(a, device)
 
     def switch_input_buffers(self) -> None:
         self.inputs, self._in_dup = self._in_dup, self.inputs
@@ -208,21 +234,25 @@ class ClPipelineStage:
         self.outputs, self._out_dup = self._out_dup, self.outputs
 
 
-def _copy_array(dst_stage: Optional[ClPipelineStage], dst: ClArray, src_stage: Optional[ClPipelineStage],
-                src: ClArray) -> None:
-    """Move src's data into dst: device→device when both sides are
-    device-resident, else through host memory."""
+def _transfer(engine, dst_stage: Optional[ClPipelineStage], dst: ClArray, src_stage: Optional[ClPipelineStage],
+              src: ClArray) -> None:
+    """Enqueue the copies that move src's data into dst on ``engine``.
+    Stage sides are device-resident replicas (every device of the
+    destination stage receives every slice, pulled from the source device
+    that owns it); a ``None`` stage is the host array itself."""
     n = min(src.nbytes, dst.nbytes)
-    src_dev = src_stage is not None and src_stage._resident
-    dst_dev = dst_stage is not None and dst_stage._resident
-    if src_dev and dst_dev:
-        cek.memcpy_default(dst_stage._replica_ptr(dst), src_stage._replica_ptr(src), n)
-    elif src_dev:
-        cek.memcpy_default(dst.host_pointer(), src_stage._replica_ptr(src), n)
-    elif dst_dev:
-        cek.memcpy_default(dst_stage._replica_ptr(dst), src.host_pointer(), n)
+    if src_stage is None:
+        srcs = [(-1, src.host_pointer(), 0, n)]
     else:
-        cek.copy_memory(dst.host_pointer(), src.host_pointer(), n)
+        srcs = [(src_stage._ordinals[d], src_stage._replica_ptr(src, d), b, min(c, n - b))
+                for d, b, c in src_stage._slices(src) if b < n]
+    if dst_stage is None:
+        dsts = [(-1, dst.host_pointer())]
+    else:
+        dsts = [(dst_stage._ordinals[d], dst_stage._replica_ptr(dst, d)) for d in range(len(dst_stage._ordinals))]
+    for dd, dp in dsts:
+        for sd, sp, b, c in srcs:
+            engine.copy(dp + b, dd, sp + b, sd, c)
 
 
 class ClPipeline:
@@ -232,39 +262,65 @@ class ClPipeline:
         self.stages = stages
         self.debug = debug
         self.counter = 0
-        self._pool = ThreadPoolExecutor(max_workers=max(2, 2 * len(stages)))
+        self._pool = ThreadPoolExecutor(max_workers=max(1, len(stages)))
+        self.engine = cek.CopyEngine()
 
-    def _forward(self, k: int, data, results) -> None:
-        st = self.stages[k]
+    def _forward(self, data, results) -> None:
+        """Enqueue every transfer of this push (no host sync): host data into
+        stage 0's spare inputs, each stage's previous outputs into the next
+        stage's spare inputs, the last stage's previous outputs to the host."""
+        e = self.engine
         last = len(self.stages) - 1
-        if k == 0 and data is not None:
+        if data is not None:
+            st = self.stages[0]
             for dst, d in zip(st._in_dup, data):
-                src = as_clarray(d)
-                _copy_array(st, dst, None, src)
-        if k < last:
-            nxt = self.stages[k + 1]
+                _transfer(e, st, dst, None, as_clarray(d))
+        for k in range(last):
+            st, nxt = self.stages[k], self.stages[k + 1]
             for dst, src in zip(nxt._in_dup, st._out_dup):
-                _copy_array(nxt, dst, st, src)
-        elif results is not None:
+                _transfer(e, nxt, dst, st, src)
+        self._wrapped = []
+        if results is not None:
+            st = self.stages[last]
             for r, src in zip(results, st._out_dup):
-                dst = as_clarray(r)
-                _copy_array(None, dst, st, src)
+                w = as_clarray(r)
+                _transfer(e, None, w, st, src)
                 if not isinstance(r, ClArray):
-                    np.copyto(np.asarray(r).reshape(-1), dst.array[:np.asarray(r).size].reshape(-1))
+                    self._wrapped.append((r, w))
+
+    def transfer_stats(self) -> dict:
+        """Bytes moved by the stage transitions so far, by path: ``p2p``
+        (GPU↔GPU peer copies), ``h2d``/``d2h`` (PCIe, pipeline inputs and
+        results only) and ``host`` (CPU-device memcpy)."""
+        e = self.engine
+        return {"p2p": e.p2p_bytes, "h2d": e.h2d_bytes, "d2h": e.d2h_bytes, "host": e.host_bytes,
+                "copies": e.copies}
 
     def push_data(self, data: Optional[Sequence] = None, results: Optional[Sequence] = None) -> bool:
         """Advance the pipeline one step; returns True once results are
-        flowing out (reference pushData, ClPipeline.cs:49-125)."""
+        flowing out (reference pushData, ClPipeline.cs:49-125).  Every stage
+        computes on its current buffers (one host thread per stage) while
+        the transfers of the previous step's buffers run on the copy
+        engine's streams; one sync joins them."""
         S = len(self.stages)
         futs = [self._pool.submit(st.run) for st in self.stages]
-        futs += [self._pool.submit(self._forward, k, data, results) for k in range(S)]
-        for f in futs:
-            f.result()
+        try:
+            self._forward(data, results)
+            self.engine.sync()
+        finally:
+            for f in futs:
+                f.result()
+        for r, w in self._wrapped:  # a non-contiguous result was wrapped through a copy
+            view = np.asarray(r)
+            if not np.shares_memory(view, w.array):
+                np.copyto(view.reshape(-1), w.array[:view.size].reshape(-1))
         for i, st in enumerate(self.stages):
+            st._snapshot_owner()
             if data is not None or i != 0:
                 st.switch_input_buffers()
             if results is not None or i != S - 1:
                 st.switch_output_buffers()
+                st._owner = st._owner_next
         self.counter += 1
         if data is None and results is None:
             return self.counter > 2 * S - 2
