@@ -1,15 +1,28 @@
-"""BASELINE config 4: N-body as a 3-stage device-to-device pipeline,
-double-buffered, stage transitions over xGMI (peer copies, no host bounce).
+"""BASELINE config 4: N-body (1M bodies) as a 3-stage device-to-device
+pipeline, double-buffered, stage transitions over xGMI (peer copies on the
+native copy engine, no host bounce).
 
-An ensemble of independent N-body systems flows through
-  stage 1: all-pairs forces (LDS-tiled, rsqrt, packed pairs) — dominant, O(n²)
-  stage 2: leapfrog kick-drift                       — O(n)
-  stage 3: kinetic-energy diagnostic (per-group sums) — O(n)
-Each push advances every stage by one system; after 2·3 pushes results flow
-out.  With 4 or more GPUs the force stage runs on all but two of them
-(range-partitioned, load-balanced) and the other two stages get one GPU
-each; with fewer GPUs stages are assigned round-robin (1 GPU: all three on
-GPU 0).  Kernels are user kernel strings JIT-compiled by hiprtc.
+  stage 1: all-pairs forces (LDS-tiled, rsqrt, packed pairs) — O(n²), the
+           force stage is range-split over its GPUs by the load balancer
+  stage 2: leapfrog kick-drift                                 — O(n)
+  stage 3: kinetic-energy diagnostic (per-group sums) + state pass-through
+
+Time stepping.  Step t+1 of one system needs step t's kick output, so a
+single system cannot keep three stages busy: its next input exists only once
+it has left the pipeline (latency L = 2·stages pushes).  The pipeline
+therefore carries M = L + 1 systems of n bodies in rotation: push k feeds
+system k mod M its current state, the state that leaves the pipeline at
+push k + L is written back, and that system is fed again at push k + M.
+Every system is genuinely time-stepped (state carried from step to step);
+every push advances one system by one step through all three stages.  The
+first stepped system is checked against a float64 host step on sampled
+bodies.
+
+Placement: with 3 or more GPUs the stages run on distinct GPUs (force on
+all but two, kick and energy on one each); with fewer, round-robin.  Stage
+times are device times from hipEvent timelines (``record_timeline``), so
+``overlap`` compares what the stages cost on their devices with the push
+wall time.  Kernels are user kernel strings JIT-compiled by hiprtc.
 """
 import argparse
 import time
@@ -80,10 +93,12 @@ __global__ void kick(const float4* pos, const float4* vel, const float4* acc, co
 }
 """
 ENERGY = r"""
-__global__ __launch_bounds__(256) void energy(const float4* pos, const float4* vel, float* e_o) {
+__global__ __launch_bounds__(256) void energy(const float4* pos, const float4* vel, float4* pos_o, float4* vel_o,
+                                              float* e_o) {
   __shared__ float s[256];
   long long i = get_global_id(0);
   float4 p = pos[i], v = vel[i];
+  pos_o[i] = p; vel_o[i] = v;
   s[threadIdx.x] = 0.5f * p.w * (v.x * v.x + v.y * v.y + v.z * v.z);
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) { if (threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w]; __syncthreads(); }
@@ -91,9 +106,26 @@ __global__ __launch_bounds__(256) void energy(const float4* pos, const float4* v
 }
 """
 
+
+def host_step(pos, vel, prm, idx):
+    """float64 leapfrog kick-drift of bodies ``idx`` (forces from all bodies)."""
+    eps2, dt = float(prm[0]), float(prm[3])
+    p = pos.astype(np.float64)
+    out_p, out_v = [], []
+    for i in idx:
+        d = p[:, :3] - p[i, :3]
+        r2 = (d * d).sum(1) + eps2
+        inv = 1.0 / np.sqrt(r2)
+        acc = (d * (p[:, 3] * inv ** 3)[:, None]).sum(0)
+        v = vel[i, :3].astype(np.float64) + acc * dt
+        out_v.append(v)
+        out_p.append(p[i, :3] + v * dt)
+    return np.array(out_p), np.array(out_v)
+
+
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=1 << 20)
-ap.add_argument("--pushes", type=int, default=10)
+ap.add_argument("--pushes", type=int, default=14)
 ap.add_argument("--gpus", type=int, default=0, help="0 = all visible")
 ap.add_argument("--logical", type=int, default=0, help="rehearsal: act as if GPU 0 were this many GPUs")
 a = ap.parse_args()
@@ -105,9 +137,10 @@ if a.logical > 1:
         g0 = g0 + g[0]
     g = g0
 ng = len(g) if a.gpus <= 0 else min(a.gpus, len(g))
-if ng >= 4:
-    # the O(n²) force stage gets every GPU but the last two (range-split by
-    # the load balancer); kick-drift and the energy diagnostic get one each
+if ng >= 3:
+    # distinct GPUs per stage: the O(n²) force stage gets every GPU but the
+    # last two (range-split by the load balancer); kick-drift and the energy
+    # diagnostic get one each
     devs = [g[0:ng - 2], g[ng - 2], g[ng - 1]]
 else:
     devs = [g[i % ng] for i in range(3)]
@@ -120,32 +153,78 @@ s1.add_input_buffers(f4(), f4()); s1.add_hidden_buffers(prm.copy()); s1.add_outp
 s2.add_devices(devs[1]); s2.add_kernels(KICK, "kick", [n], [256])
 s2.add_input_buffers(f4(), f4(), f4()); s2.add_hidden_buffers(prm.copy()); s2.add_output_buffers(f4(), f4())
 s3.add_devices(devs[2]); s3.add_kernels(ENERGY, "energy", [n], [256])
-s3.add_input_buffers(f4(), f4()); s3.add_output_buffers(np.zeros(n // 256, np.float32))
+s3.add_input_buffers(f4(), f4()); s3.add_output_buffers(f4(), f4(), np.zeros(n // 256, np.float32))
 s1.prepend_to_stage(s2)
 s2.prepend_to_stage(s3)
 pipe = s1.make_pipeline()
+for s in (s1, s2, s3):
+    s.cruncher.record_timeline = True
+S = 3
+L = 2 * S                 # a push's data leaves the pipeline L pushes later
+M = L + 1                 # systems in rotation
 rng = np.random.default_rng(0)
-pos = np.zeros((n, 4), np.float32)
-vel = np.zeros((n, 4), np.float32)
-energy = np.zeros(n // 256, np.float32)
-times, ready_at = [], None
-for k in range(a.pushes):
+states = []
+for _ in range(M):
+    pos = np.zeros((n, 4), np.float32)
+    vel = np.zeros((n, 4), np.float32)
     pos[:, :3] = rng.standard_normal((n, 3))
     pos[:, 3] = 1.0 / n
     vel[:, :3] = 0.01 * rng.standard_normal((n, 3))
+    states.append([pos, vel])
+steps = [0] * M
+first_in = [states[0][0].copy(), states[0][1].copy()]
+res_pos, res_vel = np.zeros((n, 4), np.float32), np.zeros((n, 4), np.float32)
+energy = np.zeros(n // 256, np.float32)
+kinetic = {}
+times, ready_at, check = [], None, None
+for k in range(a.pushes):
+    j = k % M
     sync()
     t = time.perf_counter()
-    ready = pipe.push_data([pos.reshape(-1), vel.reshape(-1)], [energy])
+    ready = pipe.push_data([states[j][0].reshape(-1), states[j][1].reshape(-1)],
+                           [res_pos.reshape(-1), res_vel.reshape(-1), energy])
     sync()
     times.append((time.perf_counter() - t) * 1e3)
-    if ready and ready_at is None:
-        ready_at = k
-steady = times[2:] if len(times) > 3 else times
+    if ready:
+        if ready_at is None:
+            ready_at = k
+        done = (k - L) % M   # the system fed L pushes ago
+        states[done][0][:] = res_pos
+        states[done][1][:] = res_vel
+        steps[done] += 1
+        kinetic.setdefault(done, []).append(float(energy.sum()))
+        if done == 0 and steps[0] == 1:
+            idx = np.random.default_rng(1).choice(n, 8, replace=False)
+            hp, hv = host_step(first_in[0], first_in[1], prm, idx)
+            err_p = np.abs(res_pos[idx, :3] - hp).max() / np.abs(hp).max()
+            err_v = np.abs(res_vel[idx, :3] - hv).max() / np.abs(hv).max()
+            check = float(max(err_p, err_v))
+steady = times[L:] if len(times) > L + 1 else times[2:]
 ms = float(np.median(steady))
-stage_ms = pipe.elapsed_times()
-emit({"config": "nbody_pipeline_3stage", "n": n, "gpus_used": ng, "force_stage_gpus": len(devs[0]), "push_ms_median": ms,
-      "stage_ms_last": stage_ms, "ready_after_pushes": ready_at,
+
+
+def stage_device_ms(stage, pushes):
+    """Median per-push kernel time of a stage: each push is one compute per
+    device; a push costs the stage its slowest device's span."""
+    spans = stage.cruncher.timeline()
+    per_dev = {}
+    for sp in spans:
+        per_dev.setdefault(sp["device"], []).append(sp["end_ms"] - sp["begin_ms"])
+    rows = [max(v[i] for v in per_dev.values() if i < len(v)) for i in range(min(len(v) for v in per_dev.values()))]
+    rows = rows[-len(steady):] if len(rows) > len(steady) else rows
+    return float(np.median(rows))
+
+
+stage_ms = [stage_device_ms(s, a.pushes) for s in (s1, s2, s3)]
+xfer = pipe.transfer_stats()
+emit({"config": "nbody_pipeline_3stage", "n": n, "systems_in_flight": M, "gpus_used": ng,
+      "stage_gpus": [len(d) if hasattr(d, "__len__") else 1 for d in devs], "push_ms_median": ms,
+      "stage_device_ms": stage_ms, "ready_after_pushes": ready_at,
       "interactions_per_s": n * n / (ms * 1e-3), "tflops_20flop": 20 * n * n / (ms * 1e-3) / 1e12,
       "force_stage_pct_fp32_peak": 100 * 20 * n * n / (stage_ms[0] * 1e-3) / 1e12 / FP32_PEAK_TFLOPS / len(devs[0]),
-      "overlap_efficiency": max(stage_ms) / ms, "kinetic_energy_sum": float(energy.sum())})
+      "overlap_efficiency": max(stage_ms) / ms, "serial_over_push": sum(stage_ms) / ms,
+      "steps_per_system": steps, "step_check_max_rel_err": check,
+      "transfer_bytes": xfer, "kinetic_energy_system0": kinetic.get(0, [])})
 pipe.dispose()
+if check is None or not check < 1e-3:
+    raise SystemExit(f"nbody step check failed: {check}")
