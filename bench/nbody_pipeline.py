@@ -154,6 +154,14 @@ s2.add_devices(devs[1]); s2.add_kernels(KICK, "kick", [n], [256])
 s2.add_input_buffers(f4(), f4(), f4()); s2.add_hidden_buffers(prm.copy()); s2.add_output_buffers(f4(), f4())
 s3.add_devices(devs[2]); s3.add_kernels(ENERGY, "energy", [n], [256])
 s3.add_input_buffers(f4(), f4()); s3.add_output_buffers(f4(), f4(), np.zeros(n // 256, np.float32))
+# slice ownership in multi-device stages: a force work item owns 4 bodies
+# (16 floats) of each output, a kick / energy work item one body (4 floats),
+# an energy work-group one partial sum
+for arr in s1.outputs:
+    arr.elements_per_work_item = 16
+for arr in s2.outputs + s3.outputs[:2]:
+    arr.elements_per_work_item = 4
+s3.outputs[2].elements_per_group = 1
 s1.prepend_to_stage(s2)
 s2.prepend_to_stage(s3)
 pipe = s1.make_pipeline()

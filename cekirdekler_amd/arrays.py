@@ -200,11 +200,17 @@ ArrayLike = Union[np.ndarray, FastArr, "ClArray", Sequence]
 class ClArray:
     """A kernel-parameter array with transfer flags (reference ``ClArray<T>``).
 
+    Wrapped host memory of at least ``ClArray.auto_pin_min_bytes`` (64 KiB;
+    0 disables) is registered with HIP (``hipHostRegister``) on its first
+    compute, so its copies are DMA from pinned pages like a FastArr's.
+
     ``ClArray(n, dtype)`` allocates pinned native memory (like
     ``new ClArray<float>(n)``); ``ClArray(ndarray)`` / ``ClArray(tensor)``
     wraps existing host memory without copying (like the implicit
     ``float[] → ClArray<float>`` conversion, ClArray.cs:1014).
     """
+
+    auto_pin_min_bytes = 64 * 1024
 
     def __init__(self, data: Union[int, ArrayLike, None] = None, dtype=None, alignment: int = 4096,
                  fast: Optional[bool] = None):
@@ -486,7 +492,14 @@ class ClArray:
         if cached is not None and cached[0] == key:
             return cached[1]
         arr = self.array
-        if self.zero_copy and self._fast is None and not self._registered:
+        if self._fast is None and not self._registered and (
+                self.zero_copy or (arr.nbytes >= ClArray.auto_pin_min_bytes > 0)):
+            # Page-lock wrapped host memory on first use (the reference pins
+            # every array for each compute, Cores.cs:535-541): a copy from
+            # pageable memory is staged by the runtime and a D2H blocks the
+            # host until the stream drains, which defeats enqueue mode.
+            # Refcounted per pointer in the native layer; released on
+            # dispose / GC.
             self._registered = bool(cek.host_register(arr.ctypes.data, arr.nbytes))
         # zero-copy only when the GPU can map the memory (pinned FastArr or a
         # successful registration); otherwise the array is copied as usual
@@ -532,6 +545,11 @@ class ClArray:
             except Exception:
                 pass
             self._registered = False
+
+    @property
+    def pinned(self) -> bool:
+        """Host storage is page-locked (a FastArr, or registered wrapped memory)."""
+        return (self._fast is not None and self._fast.pinned) or self._registered
 
     @property
     def is_deleted(self) -> bool:

@@ -58,6 +58,7 @@ def _clone(a: ClArray) -> ClArray:
     d = ClArray(a.N, a.dtype if not a.is_bf16 else "bfloat16")
     d.array[:] = a.array
     d.elements_per_work_item = a.elements_per_work_item
+    d.elements_per_group = a.elements_per_group
     return d
 
 
