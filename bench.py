@@ -286,17 +286,18 @@ def bench_node_configs(world: int) -> dict:
     """BASELINE configs 4 and 5 on this job's GPUs (0 .. world-1), run by
     rank 0 after every other rank has left: the N-body 3-stage
     device→device pipeline (stage transitions over xGMI) and the 256-task
-    pool over a device pool.  Both are single-process multi-GPU programs (the
+    pool over a device pool; plus config 1, SAXPY 1M on the CPU device.  Both are single-process multi-GPU programs (the
     reference's model), so each runs as a child process with its own time
     limit; a failure is reported in its field and cannot stop the headline."""
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                         "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
     out = {}
-    for name, script, args in (("nbody_pipeline", "nbody_pipeline.py", ["--pushes", "8"]),
-                               ("task_pool", "task_pool.py", [])):
+    for name, script, args in (("nbody_pipeline", "nbody_pipeline.py", ["--gpus", str(world), "--pushes", "14"]),
+                               ("task_pool", "task_pool.py", ["--gpus", str(world)]),
+                               ("saxpy_1m_cpu", "saxpy_cpu.py", [])):
         try:
-            r = subprocess.run([sys.executable, script, "--gpus", str(world), *args], cwd=os.path.join(ROOT, "bench"),
+            r = subprocess.run([sys.executable, script, *args], cwd=os.path.join(ROOT, "bench"),
                                env=env, capture_output=True, text=True, timeout=180)
             lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
             out[name] = json.loads(lines[-1]) if (r.returncode == 0 and lines) else {
@@ -403,6 +404,7 @@ def main(argv=None) -> int:
                 "load_balance_iters": lb,
                 "nbody_pipeline": node.get("nbody_pipeline"),
                 "task_pool": node.get("task_pool"),
+                "saxpy_1m_cpu": node.get("saxpy_1m_cpu"),
             },
         }
         print(json.dumps(out), flush=True)

@@ -492,14 +492,16 @@ class ClArray:
         if cached is not None and cached[0] == key:
             return cached[1]
         arr = self.array
+        moves = self._read or self._partial or self._write or self._write_all
         if self._fast is None and not self._registered and (
-                self.zero_copy or (arr.nbytes >= ClArray.auto_pin_min_bytes > 0)):
+                self.zero_copy or (moves and arr.nbytes >= ClArray.auto_pin_min_bytes > 0)):
             # Page-lock wrapped host memory on first use (the reference pins
             # every array for each compute, Cores.cs:535-541): a copy from
             # pageable memory is staged by the runtime and a D2H blocks the
             # host until the stream drains, which defeats enqueue mode.
             # Refcounted per pointer in the native layer; released on
-            # dispose / GC.
+            # dispose / GC.  Device-only arrays (no transfer flag) stay as
+            # they are (pinning would commit their untouched pages).
             self._registered = bool(cek.host_register(arr.ctypes.data, arr.nbytes))
         # zero-copy only when the GPU can map the memory (pinned FastArr or a
         # successful registration); otherwise the array is copied as usual

@@ -192,16 +192,47 @@ class GemmBf16:
     def flops(self) -> float:
         return 2.0 * self.M * self.N * self.K
 
-    def run(self, compute_id: int = 1, resident: bool = True) -> None:
+    def _group_work_items(self) -> int:
+        """Work items of one tile group (``group_m`` tile rows × every tile
+        column): the unit whose A rows form one contiguous panel."""
+        return self.group_m * (self.N // self.BN) * self.L * self.split_k
+
+    def can_stream(self) -> bool:
+        """Host-resident streaming needs whole tile groups (A row panels) per
+        blob and an integral A panel per work item."""
+        ntm, ntn = self.M // self.BM, self.N // self.BN
+        per_wi = self.BM * self.K
+        return (self.split_k == 1 and ntm % self.group_m == 0
+                and per_wi % (ntn * self.L) == 0)
+
+    def run(self, compute_id: int = 1, resident: bool = True, stream_blobs: int = 0) -> None:
+        """One GEMM through compute().  ``resident``: A/B stay on the devices
+        after the first call and C stays in device memory.  ``stream_blobs``
+        (host-resident only): run the call through the event-driven
+        read/compute/write pipeline (Cores.cs:1197-1367) in that many blobs
+        per device — B is a full read, A goes up one row panel per blob
+        (``partial``) and every blob's C tiles come down while later blobs'
+        panels upload and compute, on the two half-pipelines' streams."""
         first = not self._uploaded
+        streamed = bool(stream_blobs) and not resident
+        if streamed and not self.can_stream():
+            raise ValueError("stream_blobs needs split_k == 1, whole tile groups and an integral A panel "
+                             "per work item")
         for a in (self.dims, self.A, self.B):
             a.read = first or not resident
+        self.A.partial_read = streamed
+        # an A row panel of one tile group spans group_m·BM rows; per work item
+        self.A.elements_per_work_item = (self.BM * self.K) // ((self.N // self.BN) * self.L) if streamed else 1
         if self.split_k > 1:
             self.counters.read = first  # zeroed once; the kernel re-arms them
         self.C.write = not resident
+        gran = self.granularity()
+        if streamed:
+            gran = self._group_work_items()
         self.dims.next_param(self.A, self.B, self.C, *self.extra).compute(
             self.cr, compute_id, self.kernel, self.global_range, self.L,
-            granularity=self.granularity())
+            pipeline=streamed, pipeline_type=True, pipeline_blobs=max(1, stream_blobs),
+            granularity=gran)
         self._uploaded = True
 
     def result(self, download: bool = True) -> np.ndarray:

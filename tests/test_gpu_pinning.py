@@ -40,7 +40,7 @@ def test_pinned_wrapped_d2h_does_not_block_enqueue_mode():
     from the registered array, compute() returns while the kernel runs."""
     cr = ck.ClNumberCruncher(ck.ClPlatforms.all().gpus()[0], SPIN)
     n = 1 << 18
-    it = ck.ClArray(np.array([200000], np.int32))  # a kernel of tens of ms
+    it = ck.ClArray(np.array([1000000], np.int32))  # a kernel of ~20 ms
     it.write = False
 
     def host_ms(pin_threshold):
