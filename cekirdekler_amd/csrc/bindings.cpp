@@ -352,6 +352,10 @@ PYBIND11_MODULE(_cek, m) {
       .def("outstanding", &DevicePool::outstanding)
       .def("device_task_counts", &DevicePool::device_task_counts)
       .def("device_busy_ms", &DevicePool::device_busy_ms)
+      .def("queue_limit", &DevicePool::queue_limit)
+      .def("queue_limit_history", &DevicePool::queue_limit_history)
+      .def("marker_speeds", &DevicePool::marker_speeds)
+      .def("device_in_flight", &DevicePool::device_in_flight)
       .def_property_readonly("num_devices", &DevicePool::num_devices)
       .def_property_readonly("max_in_flight", &DevicePool::max_in_flight)
       .def("close", &DevicePool::close, py::call_guard<py::gil_scoped_release>());

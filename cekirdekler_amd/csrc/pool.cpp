@@ -15,6 +15,8 @@ DevicePool::DevicePool(std::vector<std::shared_ptr<Cores>> devices, int max_in_f
   }
   counts_.assign(devs_.size(), 0);
   busy_ms_.assign(devs_.size(), 0.0);
+  inflight_.assign(devs_.size(), 0);
+  speed_.assign(devs_.size(), Speed());
   for (int i = 0; i < num_devices(); ++i) threads_.emplace_back([this, i] { consumer(i); });
 }
 
@@ -42,9 +44,12 @@ void DevicePool::enqueue(const std::vector<PoolTask>& tasks) {
     std::lock_guard<std::mutex> g(mu_);
     if (closed_) throw Error("device pool is closed");
     bool sync_next = false;
+    const int pid = static_cast<int>(pools_.size());
+    pools_.push_back(PoolProgress());
     for (const auto& t : tasks) {
       Item it;
       it.task = t;
+      it.pool = pid;
       // GLOBAL_SYNC_LAST of the previous task = a barrier before this one
       if (sync_next) it.task.type |= kTaskSyncFirst;
       sync_next = (t.type & kTaskSyncLast) != 0;
@@ -54,14 +59,46 @@ void DevicePool::enqueue(const std::vector<PoolTask>& tasks) {
           c.target = d;
           queue_.push_back(std::move(c));
           ++outstanding_;
+          ++pools_[pid].total;
         }
       } else {
         queue_.push_back(std::move(it));
         ++outstanding_;
+        ++pools_[pid].total;
       }
     }
   }
   work_cv_.notify_all();
+}
+
+int DevicePool::least_loaded_locked() const {
+  int best = 0;
+  for (int d = 1; d < num_devices(); ++d)
+    if (inflight_[d] < inflight_[best]) best = d;
+  return best;
+}
+
+int DevicePool::limit_locked() {
+  if (queue_.empty()) return max_in_flight_;
+  const PoolProgress& p = pools_[queue_.front().pool];
+  const long long n = p.total, sub = p.taken, rem = n - sub;
+  long long q;
+  if (rem < 3)
+    q = 1;
+  else if (sub < n / 10)
+    q = n / 10;
+  else if (sub < n / 5)
+    q = n / 20;
+  else if (sub < n / 3)
+    q = n / 33;
+  else if (sub < n / 2)
+    q = n / 50;
+  else
+    q = 2;
+  q /= num_devices();
+  const int lim = static_cast<int>(std::max<long long>(1, std::min<long long>(q, max_in_flight_)));
+  if (limit_history_.empty() || limit_history_.back() != lim) limit_history_.push_back(lim);
+  return lim;
 }
 
 bool DevicePool::take_locked(int dev, Item& out) {
@@ -72,6 +109,14 @@ bool DevicePool::take_locked(int dev, Item& out) {
     if (u.task.type & kTaskSyncFirst) {
       // a barrier: every earlier task has retired and nothing precedes it
       if (j != 0 || running_ > 0) return false;
+    }
+    if (u.target < 0 && owner_ < 0 && (u.task.type & (kTaskSelectBegin | kTaskSerialBegin))) {
+      // a new select/serial group: pin it to the least-loaded device
+      owner_ = least_loaded_locked();
+      if (owner_ != dev) {
+        work_cv_.notify_all();
+        return false;
+      }
     }
     out = std::move(u);
     queue_.erase(queue_.begin() + static_cast<long>(j));
@@ -84,6 +129,8 @@ bool DevicePool::take_locked(int dev, Item& out) {
       serial_owner_ = false;
     }
     ++running_;
+    ++inflight_[dev];
+    ++pools_[out.pool].taken;
     return true;
   }
   return false;
@@ -97,6 +144,7 @@ void DevicePool::complete(int dev, long long id, double ms, const std::string& e
     busy_ms_[dev] += ms;
     --outstanding_;
     --running_;
+    --inflight_[dev];
   }
   comp_cv_.notify_all();
   done_cv_.notify_all();
@@ -116,6 +164,13 @@ int DevicePool::retire(int dev, std::vector<Inflight>& inflight) {
       ++i;
     }
   }
+  if (n > 0) {  // marker-reach speed (ClPipeline.cs:4788-4817)
+    std::lock_guard<std::mutex> g(mu_);
+    Speed& sp = speed_[dev];
+    const double t = now_ms();
+    if (sp.last_ms >= 0) sp.hist[sp.n++ % 15] = n / (t - sp.last_ms + 0.001);
+    sp.last_ms = t;
+  }
   return n;
 }
 
@@ -130,7 +185,7 @@ void DevicePool::consumer(int dev) {
     bool got = false, idle = false, stop = false;
     {
       std::unique_lock<std::mutex> lk(mu_);
-      if (static_cast<int>(inflight.size()) < max_in_flight_) got = take_locked(dev, it);
+      if (static_cast<int>(inflight.size()) < limit_locked()) got = take_locked(dev, it);
       if (!got && inflight.empty()) {
         if (closed_ && queue_.empty())
           stop = true;
@@ -211,6 +266,32 @@ std::vector<long long> DevicePool::device_task_counts() {
 std::vector<double> DevicePool::device_busy_ms() {
   std::lock_guard<std::mutex> g(mu_);
   return busy_ms_;
+}
+
+int DevicePool::queue_limit() {
+  std::lock_guard<std::mutex> g(mu_);
+  return limit_locked();
+}
+
+std::vector<int> DevicePool::queue_limit_history() {
+  std::lock_guard<std::mutex> g(mu_);
+  return limit_history_;
+}
+
+std::vector<double> DevicePool::marker_speeds() {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<double> out;
+  for (auto& sp : speed_) {
+    double s = 0;
+    for (double h : sp.hist) s += h;
+    out.push_back(s / 15.0 + 0.001);
+  }
+  return out;
+}
+
+std::vector<int> DevicePool::device_in_flight() {
+  std::lock_guard<std::mutex> g(mu_);
+  return inflight_;
 }
 
 }  // namespace cek

@@ -23,6 +23,19 @@
 //   NO_COMPUTE                          transfers only
 // Completions (task id, device, ms, error) are queued for the caller, which
 // runs user callbacks off the device threads.
+//
+// Scheduling policy (reference producer, ClPipeline.cs:4100-4236, :4788-4817):
+//   * a select/serial group goes to the least-loaded device — fewest tasks
+//     taken and not yet retired (the reference's remaining tasks + markers
+//     remaining), first index on ties;
+//   * per-device queue depth follows the pool's progress: with N tasks in
+//     the pool of which `taken` have been handed out, the limit is N/10
+//     until 10 % are out, N/20 until 20 %, N/33 until 33 %, N/50 until half,
+//     then 2 (1 once fewer than 3 remain), divided by the device count and
+//     clamped to [1, max_in_flight] — deep queues while the pool is full,
+//     shallow ones in the tail so the last tasks spread over every device;
+//   * each device keeps a smoothed marker-reach speed (markers retired per
+//     ms, 15-sample moving average).
 #pragma once
 #include <condition_variable>
 #include <deque>
@@ -75,6 +88,11 @@ class DevicePool {
   long long outstanding();
   std::vector<long long> device_task_counts();
   std::vector<double> device_busy_ms();
+  // current per-device queue-depth limit (policy above) and its history
+  int queue_limit();
+  std::vector<int> queue_limit_history();
+  std::vector<double> marker_speeds();  // smoothed markers per ms, per device
+  std::vector<int> device_in_flight();
   int num_devices() const { return static_cast<int>(devs_.size()); }
   int max_in_flight() const { return max_in_flight_; }
   void close();  // drain, stop and join the consumer threads
@@ -84,7 +102,13 @@ class DevicePool {
     PoolTask task;
     int target = -1;  // broadcast copy: only this device may take it
     bool serial = false;
+    int pool = 0;     // enqueue() call it came from
   };
+  struct PoolProgress {
+    long long total = 0, taken = 0;
+  };
+  int limit_locked();
+  int least_loaded_locked() const;
   struct Inflight {
     long long id;
     int slot;
@@ -109,6 +133,15 @@ class DevicePool {
   bool closed_ = false;
   std::vector<long long> counts_;
   std::vector<double> busy_ms_;
+  std::vector<int> inflight_;              // taken, not retired, per device
+  std::vector<PoolProgress> pools_;
+  std::vector<int> limit_history_;
+  struct Speed {
+    double last_ms = -1;
+    double hist[15] = {0};
+    long long n = 0;
+  };
+  std::vector<Speed> speed_;
   std::vector<std::thread> threads_;
 };
 

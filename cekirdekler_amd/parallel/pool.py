@@ -306,6 +306,29 @@ class ClDevicePool:
     def device_busy_ms(self) -> List[float]:
         return list(self._native.device_busy_ms()) if self._native is not None else []
 
+    # ---- scheduling policy (ClPipeline.cs:4100-4236, :4788-4817) --------------
+    def queue_limit(self) -> int:
+        """Current per-device queue-depth limit: follows the head pool's
+        progress (N/10 → N/20 → N/33 → N/50 → 2 → 1 tasks, over the device
+        count, within ``max_queues_per_device``)."""
+        return int(self._native.queue_limit()) if self._native is not None else 0
+
+    def queue_limit_history(self) -> List[int]:
+        """Every distinct limit the consumers have applied, in order."""
+        return list(self._native.queue_limit_history()) if self._native is not None else []
+
+    def marker_reach_speeds(self) -> List[float]:
+        """Per device: markers retired per ms, 15-sample moving average
+        (reference ``markerReachSpeed``)."""
+        return list(self._native.marker_speeds()) if self._native is not None else []
+
+    markerReachSpeed = marker_reach_speeds
+
+    def device_in_flight(self) -> List[int]:
+        """Per device: tasks taken and not yet retired (the load measure a
+        select/serial group is placed by)."""
+        return list(self._native.device_in_flight()) if self._native is not None else []
+
     def dispose(self) -> None:
         if self._native is not None:
             try:

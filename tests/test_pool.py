@@ -127,3 +127,73 @@ def test_task_error_is_reported_by_finish():
         pool.finish()
     assert sum(pool.device_task_counts()) == 2  # the failing task retired too
     pool.dispose()
+
+
+SPIN = """
+__global__ void spin(float* x, int* it) {
+  long long i = get_global_id(0);
+  float v = x[i];
+  for (int k = 0; k < it[0]; ++k) v = v * 0.999f + 0.5f;
+  x[i] = v;
+}
+__global__ void fill(float* x, int* it) { x[get_global_id(0)] = (float)it[0]; }
+"""
+
+
+def _spin_task(kernel, n, iters):
+    x = ck.ClArray(np.zeros(n, np.float32))
+    it = ck.ClArray(np.array([iters], np.int32))
+    it.write = False
+    return x, x.next_param(it).task(1, kernel, n, 64)
+
+
+def test_select_group_lands_on_least_loaded_device():
+    """A device-select group goes to the device with the fewest tasks in
+    flight (ClPipeline.cs:4100-4127), not to whichever consumer grabs it."""
+    cpu = ck.ClPlatforms.all().cpus(True)
+    pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SPIN, True, 3)
+    pool.add_device(cpu + cpu)
+    busy = ClTaskPool()
+    xb, tb = _spin_task("spin", 64 * 8, 3_000_000)  # one long task keeps its device busy
+    busy.feed(tb)
+    pool.enqueue_task_pool(busy)
+    import time
+    for _ in range(200):  # wait until a consumer has taken it
+        if sum(pool.device_in_flight()) == 1:
+            break
+        time.sleep(0.005)
+    busy_dev = pool.device_in_flight().index(1)
+    grp = ClTaskPool()
+    tasks = []
+    for k in range(4):
+        _, t = _spin_task("fill", 64, k)
+        t.type = (ClTaskType.TASK_MESSAGE_DEVICE_SELECT_BEGIN if k == 0 else
+                  ClTaskType.TASK_MESSAGE_DEVICE_SELECT_END if k == 3 else ClTaskType.TASK_MESSAGE_DEFAULT)
+        grp.feed(t)
+        tasks.append(t)
+    pool.enqueue_task_pool(grp)
+    pool.finish()
+    assert {t.device_index for t in tasks} == {1 - busy_dev}
+    assert tb.device_index == busy_dev
+    pool.dispose()
+
+
+def test_queue_limit_shrinks_as_pool_drains():
+    """Per-device queue depth follows pool progress (ClPipeline.cs:4178-4236):
+    N/10 → N/20 → N/33 → N/50 → 2 → 1 tasks over the device count."""
+    cpu = ck.ClPlatforms.all().cpus(True)
+    pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SPIN, True, 16)
+    pool.add_device(cpu + cpu)
+    tp = ClTaskPool()
+    for _ in range(400):
+        _, t = _spin_task("spin", 64, 2000)
+        tp.feed(t)
+    pool.enqueue_task_pool(tp)
+    pool.finish()
+    h = pool.queue_limit_history()
+    # 400 tasks / 2 devices: 20 → 10 → 6 → 4 → 1 (and 1 at the tail)
+    assert h[0] == 16 and h[-1] == 1, h          # N/10/2 = 20 clamped to 16 queues
+    assert all(a >= b for a, b in zip(h, h[1:])), h
+    assert {10, 6, 4}.issubset(h), h
+    assert len(pool.marker_reach_speeds()) == 2
+    pool.dispose()

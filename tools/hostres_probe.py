@@ -1,0 +1,48 @@
+"""GPU probe: host-resident SGEMM 8192³ (A, B uploaded and C downloaded on
+every call) — serial 3-phase vs the event-driven streamed pipeline with
+several blob counts.  Checks the streamed C against a float64 host product
+on sampled tiles."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+import cekirdekler_amd as ck  # noqa: E402
+from cekirdekler_amd.ops.gemm import GEMM_LIBS, GemmBf16, tile_coords  # noqa: E402
+from cekirdekler_amd.ops.library import library  # noqa: E402
+
+size = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+blob_list = [int(b) for b in (sys.argv[2] if len(sys.argv) > 2 else "0,2,4,8").split(",")]
+reps = 5
+cr = ck.ClNumberCruncher(ck.ClPlatforms.all().gpus()[0], "", prebuilt=library(*GEMM_LIBS))
+g = GemmBf16(size, size, size, cruncher=cr, tile="256x256pb")
+out = {}
+for cid, blobs in enumerate(blob_list, start=10):
+    g.C.array[:] = 0
+    g.run(compute_id=cid, resident=False, stream_blobs=blobs)  # warm
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        g.run(compute_id=cid, resident=False, stream_blobs=blobs)
+        ts.append((time.perf_counter() - t) * 1e3)
+    # sampled check of the host C written by the last call
+    rng = np.random.default_rng(cid)
+    a = (g.A.array.astype(np.uint32) << 16).view(np.float32).reshape(size, size)
+    b = (g.B.array.astype(np.uint32) << 16).view(np.float32).reshape(size, size)
+    picks = rng.choice(g.tiles, 6, replace=False)
+    tm, tn = tile_coords(picks, size, size, g.BM, g.BN, g.group_m)
+    err = 0.0
+    for t, r, c in zip(picks, tm, tn):
+        got = g.C.array[t * g.BM * g.BN:(t + 1) * g.BM * g.BN].reshape(g.BM, g.BN)
+        ref = a[r * g.BM:(r + 1) * g.BM].astype(np.float64) @ b[c * g.BN:(c + 1) * g.BN].astype(np.float64).T
+        err = max(err, float(np.abs(got - ref).max() / np.abs(ref).max()))
+    rec = cr.last_record()
+    out[f"blobs={blobs}"] = {"ms_median": float(np.median(ts)), "ms_min": float(min(ts)),
+                             "tflops": 2 * size ** 3 / (np.median(ts) * 1e-3) / 1e12, "max_rel_err": err,
+                             "pipelined": rec["pipelined"], "h2d_MiB": rec["h2d_bytes"] / 2 ** 20,
+                             "d2h_MiB": rec["d2h_bytes"] / 2 ** 20}
+    print(json.dumps({f"blobs={blobs}": out[f"blobs={blobs}"]}), flush=True)
+cr.dispose()
