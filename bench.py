@@ -162,14 +162,21 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     # panel (tile group) per blob, as many blobs as each rank has groups (≤ 8)
     groups = g.tiles // (g.group_m * (size // g.BN)) // ctx.world
     blobs = next((b for b in (8, 4, 2) if groups % b == 0 and groups >= b), 0) if g.can_stream() else 0
-    ms_host = timed(ctx, lambda: g.run(compute_id=2, resident=False, stream_blobs=blobs), host_steps, 1)
+    host_calls = []
+
+    def host_step():
+        t = time.perf_counter()
+        g.run(compute_id=2, resident=False, stream_blobs=blobs)
+        host_calls.append((time.perf_counter() - t) * 1e3)
+
+    ms_host = timed(ctx, host_step, host_steps, 2)
     cr.dispose()
     for a in (g.A, g.B, g.C, g.dims):
         a.dispose()  # release 0.5 GB of pinned host memory before the next config
     return {"ms": ms, "gflops": g.flops / (ms * 1e-3) / 1e9, "tile": tile, "balancer_setup_calls": converge,
             "sync_per_step_ms": ms_sync, "sync_per_step_gflops": g.flops / (ms_sync * 1e-3) / 1e9,
             "host_resident_ms": ms_host, "host_resident_gflops": g.flops / (ms_host * 1e-3) / 1e9,
-            "host_resident_blobs": blobs,
+            "host_resident_blobs": blobs, "host_resident_calls_ms": [round(x, 3) for x in host_calls],
             "ranges": ranges, "max_rel_err": err, "spin_timeouts": timeouts, "device": "gpu"}
 
 
@@ -401,6 +408,7 @@ def main(argv=None) -> int:
                 "sgemm_host_resident_gflops": round(sg["host_resident_gflops"], 1),
                 "sgemm_host_resident_ms": round(sg["host_resident_ms"], 3),
                 "sgemm_host_resident_stream_blobs": sg.get("host_resident_blobs", 0),
+                "sgemm_host_resident_calls_ms": sg.get("host_resident_calls_ms", []),
                 "sgemm_max_rel_err": sg["max_rel_err"],
                 "sgemm_spin_timeouts": sg["spin_timeouts"],
                 "sgemm_balancer_setup_calls": sg["balancer_setup_calls"],
