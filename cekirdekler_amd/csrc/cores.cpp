@@ -42,6 +42,7 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
     error_ = "no device selected";
   }
   global_devices_ = static_cast<int>(workers_.size());
+  spans_.resize(workers_.size());
   time_scale_.assign(workers_.size(), 1.0);
   enabled_.assign(workers_.size(), true);
   inject_.assign(workers_.size(), 0);
@@ -52,6 +53,15 @@ Cores::~Cores() {
   try {
     finish();
   } catch (...) {
+  }
+  for (size_t w = 0; w < spans_.size() && w < workers_.size(); ++w) {
+    workers_[w]->set_device();
+    for (auto& p : spans_[w].pool) {
+      (void)hipEventDestroy(p.first);
+      (void)hipEventDestroy(p.second);
+    }
+    if (spans_[w].gap_a) (void)hipEventDestroy(spans_[w].gap_a);
+    if (spans_[w].gap_b) (void)hipEventDestroy(spans_[w].gap_b);
   }
   for (size_t w = 0; w < peer_ev_.size() && w < workers_.size(); ++w) {
     if (!peer_ev_[w].up) continue;
@@ -169,7 +179,11 @@ void Cores::set_enqueue_mode(bool on) {
     double el = now_ms() - enqueue_t0_;
     auto it = state_.find(last_id_);
     std::vector<double> ms(num_devices());
-    for (int w = 0; w < num_devices(); ++w) ms[w] = el * time_scale_[w];
+    for (int w = 0; w < num_devices(); ++w) {
+      // GPU: union of this device's timed spans; CPU device: wall clock
+      const double dev = workers_[w]->gpu() ? enqueue_spans_ms(w) : -1.0;
+      ms[w] = (dev > 0 ? dev : el) * time_scale_[w];
+    }
     // every rank leaves enqueue mode together: exchange so all ranks keep the
     // identical benchmark vector (and hence derive the identical next split)
     std::vector<double> all = ex_ ? ex_->allgather(ms) : ms;
@@ -492,6 +506,82 @@ void Cores::launch_kernels_body(Worker& wk, hipStream_t s, const ComputeCall& c,
   wk.launch_graph(s, key, body);
 }
 
+void Cores::span_begin(Worker& wk, hipStream_t s) {
+  if (!wk.gpu()) return;
+  const int w = worker_index(wk);
+  DevSpans& d = spans_[w];
+  // enqueue mode keeps up to kMaxSpans pairs; past that the last pair's end
+  // is re-recorded, so its span stretches over the remaining computes
+  constexpr int kMaxSpans = 1024;
+  if (enqueue_mode_ && d.used >= kMaxSpans) return;
+  const int i = enqueue_mode_ ? d.used++ : 0;
+  while (static_cast<int>(d.pool.size()) <= i) {
+    hipEvent_t a, b;
+    CEK_HIP(hipEventCreate(&a));
+    CEK_HIP(hipEventCreate(&b));
+    d.pool.emplace_back(a, b);
+  }
+  d.gap = false;
+  CEK_HIP(hipEventRecord(d.pool[i].first, s));
+}
+
+void Cores::span_end(Worker& wk, hipStream_t s) {
+  if (!wk.gpu()) return;
+  DevSpans& d = spans_[worker_index(wk)];
+  const int i = enqueue_mode_ ? d.used - 1 : 0;
+  if (i < 0) return;
+  CEK_HIP(hipEventRecord(d.pool[i].second, s));
+}
+
+double Cores::span_ms(int w) {
+  DevSpans& d = spans_[w];
+  if (d.pool.empty()) return -1.0;
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, d.pool[0].first, d.pool[0].second) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1.0;
+  }
+  double out = ms;
+  if (d.gap) {
+    float g = 0.f;
+    if (hipEventElapsedTime(&g, d.gap_a, d.gap_b) == hipSuccess)
+      out -= g;
+    else
+      (void)hipGetLastError();
+  }
+  return out;
+}
+
+double Cores::enqueue_spans_ms(int w) {
+  DevSpans& d = spans_[w];
+  const int n = d.used;
+  d.used = 0;
+  if (n <= 0) return -1.0;
+  workers_[w]->set_device();
+  std::vector<std::pair<double, double>> iv;
+  for (int i = 0; i < n; ++i) {
+    float b = 0.f, e = 0.f;
+    if (hipEventElapsedTime(&b, d.pool[0].first, d.pool[i].first) != hipSuccess ||
+        hipEventElapsedTime(&e, d.pool[0].first, d.pool[i].second) != hipSuccess) {
+      (void)hipGetLastError();
+      return -1.0;
+    }
+    iv.emplace_back(b, e);
+  }
+  std::sort(iv.begin(), iv.end());
+  double total = 0, cb = iv[0].first, ce = iv[0].second;
+  for (size_t i = 1; i < iv.size(); ++i) {
+    if (iv[i].first > ce) {
+      total += ce - cb;
+      cb = iv[i].first;
+      ce = iv[i].second;
+    } else {
+      ce = std::max(ce, iv[i].second);
+    }
+  }
+  return total + (ce - cb);
+}
+
 int Cores::worker_index(const Worker& wk) const {
   for (int i = 0; i < num_devices(); ++i)
     if (workers_[i].get() == &wk) return i;
@@ -624,6 +714,7 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
   hipStream_t s = nullptr;
   if (wk.gpu())
     s = (enqueue_mode_ && async_enqueue) ? wk.compute_stream(wk.next_compute_queue()) : wk.main_stream();
+  span_begin(wk, s);
   const bool gather = comm_ && dist_gather_writes;
   // phase 1: host → device (partial slice wins over full read)
   for (auto& a : c.arrays) {
@@ -658,11 +749,23 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
   // no device may write its slice into host memory another device is still
   // reading (reference: all reads and computes finish before any write).
   if (phase_) {
+    DevSpans* ds = wk.gpu() ? &spans_[worker_index(wk)] : nullptr;
+    if (ds) {
+      if (!ds->gap_a) {
+        CEK_HIP(hipEventCreate(&ds->gap_a));
+        CEK_HIP(hipEventCreate(&ds->gap_b));
+      }
+      CEK_HIP(hipEventRecord(ds->gap_a, s));
+    }
     if (wk.gpu()) CEK_HIP(hipStreamSynchronize(s));
     t_phase_arrived = true;
     const double w0 = now_ms();
     phase_->arrive_and_wait();
     t_phase_wait = now_ms() - w0;  // not this device's work: kept out of its time
+    if (ds) {
+      CEK_HIP(hipEventRecord(ds->gap_b, s));
+      ds->gap = true;
+    }
   }
   // phase 3: device → host
   for (size_t i = 0; i < c.arrays.size(); ++i) {
@@ -683,6 +786,7 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
       *d2h += n * a.elem_size;
     }
   }
+  span_end(wk, s);
   if (fine_grained) wk.add_marker(s);
   if (!enqueue_mode_ && wk.gpu()) CEK_HIP(hipStreamSynchronize(s));
 }
@@ -694,6 +798,7 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
   const int halves = (B % 2 == 0) ? 2 : 1;
   const long long per_half = B / halves;
   hipStream_t m = wk.main_stream();
+  span_begin(wk, m);
   full_reads(wk, m, c, h2d);
   log_op(gidx, "h2d", 0, -1, -1);  // full reads
   int slot = 0;
@@ -775,6 +880,7 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
       }
     }
   }
+  span_end(wk, m);
   if (fine_grained) wk.add_marker(m);
   if (wk.gpu()) CEK_HIP(hipStreamSynchronize(m));
 }
@@ -784,6 +890,7 @@ void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long
   const long long B = std::max(1, c.blobs);
   const long long chunk = range / B;
   hipStream_t m = wk.main_stream();
+  span_begin(wk, m);
   full_reads(wk, m, c, h2d);
   log_op(gidx, "h2d", 0, -1, -1);  // full reads
   int slot = 0;
@@ -842,6 +949,7 @@ void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long
       *d2h += a.bytes;
     }
   }
+  span_end(wk, m);
   if (fine_grained) wk.add_marker(m);
   if (wk.gpu()) CEK_HIP(hipStreamSynchronize(m));
 }
@@ -881,7 +989,12 @@ void Cores::run_device_body(int w, const ComputeCall& c, long long ref, long lon
     // still take part in the collectives
     run_3phase(wk, gidx, c, ref, 0, h2d, d2h);
   }
-  *out_ms = (now_ms() - t0 - t_phase_wait) * time_scale_[w];
+  double el = now_ms() - t0 - t_phase_wait;
+  if (range > 0 && wk.gpu() && !enqueue_mode_) {
+    const double dev = span_ms(w);  // the stream was drained: device time of this compute
+    if (dev > 0) el = dev;
+  }
+  *out_ms = el * time_scale_[w];
 }
 
 void Cores::compute(const ComputeCall& c) {

@@ -326,6 +326,25 @@ class Cores {
   bool enqueue_mode_ = false;
   double enqueue_t0_ = 0;
   int last_id_ = 0;
+  // ---- device-time spans for the balancer ----
+  // Each GPU device's work in a compute is bracketed by a pair of timing
+  // hipEvents on the stream it starts and ends on; the balancer gets the
+  // device time between them (hipEventElapsedTime) instead of host wall
+  // clock.  Sync mode reuses pair 0; enqueue mode takes a fresh pair per
+  // compute and, when the mode is left, credits each device with the union
+  // of its spans (so devices of one process re-balance by their own device
+  // time, not the shared wall clock).
+  struct DevSpans {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
+    int used = 0;
+    hipEvent_t gap_a = nullptr, gap_b = nullptr;  // phase-barrier idle gap
+    bool gap = false;
+  };
+  std::vector<DevSpans> spans_;
+  void span_begin(Worker& wk, hipStream_t s);
+  void span_end(Worker& wk, hipStream_t s);
+  double span_ms(int w);              // sync mode: the last span (stream drained)
+  double enqueue_spans_ms(int w);     // enqueue mode: union of the spans so far
   ComputeRecord last_record_;
   CoresConfig cfg_;
 
