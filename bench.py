@@ -164,10 +164,13 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     blobs = next((b for b in (8, 4, 2) if groups % b == 0 and groups >= b), 0) if g.can_stream() else 0
     host_calls = []
 
+    host_piped = []
+
     def host_step():
         t = time.perf_counter()
         g.run(compute_id=2, resident=False, stream_blobs=blobs)
         host_calls.append((time.perf_counter() - t) * 1e3)
+        host_piped.append(cr.last_record()["pipelined"])
 
     ms_host = timed(ctx, host_step, host_steps, 2)
     cr.dispose()
@@ -177,6 +180,7 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
             "sync_per_step_ms": ms_sync, "sync_per_step_gflops": g.flops / (ms_sync * 1e-3) / 1e9,
             "host_resident_ms": ms_host, "host_resident_gflops": g.flops / (ms_host * 1e-3) / 1e9,
             "host_resident_blobs": blobs, "host_resident_calls_ms": [round(x, 3) for x in host_calls],
+            "host_resident_pipelined": host_piped,
             "ranges": ranges, "max_rel_err": err, "spin_timeouts": timeouts, "device": "gpu"}
 
 
@@ -409,6 +413,7 @@ def main(argv=None) -> int:
                 "sgemm_host_resident_ms": round(sg["host_resident_ms"], 3),
                 "sgemm_host_resident_stream_blobs": sg.get("host_resident_blobs", 0),
                 "sgemm_host_resident_calls_ms": sg.get("host_resident_calls_ms", []),
+                "sgemm_host_resident_pipelined": sg.get("host_resident_pipelined", []),
                 "sgemm_max_rel_err": sg["max_rel_err"],
                 "sgemm_spin_timeouts": sg["spin_timeouts"],
                 "sgemm_balancer_setup_calls": sg["balancer_setup_calls"],

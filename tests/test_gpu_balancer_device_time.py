@@ -34,14 +34,13 @@ def test_uneven_work_rebalances_by_device_time(mode):
     assert cr.ranges(1) == [n // 2, n // 2]
     for _ in range(6):
         if mode == "enqueue":
-            cr.enqueue_mode = True
+            cr.enqueue_mode = True  # the split is frozen while enqueueing
             for _ in range(3):
                 x.next_param(nv).compute(cr, 1, "skew", n, 256)
-            cr.enqueue_mode = False  # timings credited here, per device
+            cr.enqueue_mode = False  # each device credited with its own spans here
             b = cr.benchmarks(1)
-        x.next_param(nv).compute(cr, 1, "skew", n, 256) if mode == "sync" else None
-    b = cr.benchmarks(1)
+            assert b[1] > 2.0 * b[0], b  # not one shared wall-clock time
+        x.next_param(nv).compute(cr, 1, "skew", n, 256)  # re-balances from those timings
     r = cr.ranges(1)
-    assert b[1] > 1.5 * b[0] or r[0] > 1.3 * r[1], (b, r)
-    assert r[0] > r[1], r  # device 0 (cheap half) takes more work items
+    assert r[0] > 1.3 * r[1], r  # device 0 (cheap half) takes more work items
     cr.dispose()

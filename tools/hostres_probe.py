@@ -16,7 +16,11 @@ from cekirdekler_amd.ops.library import library  # noqa: E402
 
 size = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 blob_list = [int(b) for b in (sys.argv[2] if len(sys.argv) > 2 else "0,2,4,8").split(",")]
-resident_first = len(sys.argv) > 3 and sys.argv[3] == "resident-first"
+opts = sys.argv[3].split(",") if len(sys.argv) > 3 else []
+resident_first = "resident-first" in opts
+if "torch-first" in opts:  # initialise torch's HIP state first, as bench.py does
+    import torch
+    torch.cuda.synchronize()
 reps = 5
 cr = ck.ClNumberCruncher(ck.ClPlatforms.all().gpus()[0], "", prebuilt=library(*GEMM_LIBS))
 g = GemmBf16(size, size, size, cruncher=cr, tile="256x256pb")
