@@ -43,6 +43,7 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
   }
   global_devices_ = static_cast<int>(workers_.size());
   spans_.resize(workers_.size());
+  if (const char* e = std::getenv("CEK_DEVICE_SPANS")) device_spans = std::string(e) != "0";
   time_scale_.assign(workers_.size(), 1.0);
   enabled_.assign(workers_.size(), true);
   inject_.assign(workers_.size(), 0);
@@ -507,7 +508,7 @@ void Cores::launch_kernels_body(Worker& wk, hipStream_t s, const ComputeCall& c,
 }
 
 void Cores::span_begin(Worker& wk, hipStream_t s) {
-  if (!wk.gpu()) return;
+  if (!wk.gpu() || !device_spans) return;
   const int w = worker_index(wk);
   DevSpans& d = spans_[w];
   // enqueue mode keeps up to kMaxSpans pairs; past that the last pair's end
@@ -526,7 +527,7 @@ void Cores::span_begin(Worker& wk, hipStream_t s) {
 }
 
 void Cores::span_end(Worker& wk, hipStream_t s) {
-  if (!wk.gpu()) return;
+  if (!wk.gpu() || !device_spans) return;
   DevSpans& d = spans_[worker_index(wk)];
   const int i = enqueue_mode_ ? d.used - 1 : 0;
   if (i < 0) return;
@@ -535,7 +536,7 @@ void Cores::span_end(Worker& wk, hipStream_t s) {
 
 double Cores::span_ms(int w) {
   DevSpans& d = spans_[w];
-  if (d.pool.empty()) return -1.0;
+  if (!device_spans || d.pool.empty()) return -1.0;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, d.pool[0].first, d.pool[0].second) != hipSuccess) {
     (void)hipGetLastError();

@@ -341,6 +341,9 @@ class Cores {
     bool gap = false;
   };
   std::vector<DevSpans> spans_;
+ public:
+  bool device_spans = true;  // CEK_DEVICE_SPANS=0: host wall clock instead
+ private:
   void span_begin(Worker& wk, hipStream_t s);
   void span_end(Worker& wk, hipStream_t s);
   double span_ms(int w);              // sync mode: the last span (stream drained)

@@ -127,19 +127,45 @@ void* Worker::buffer(const ArraySpec& a) {
   }
   std::lock_guard<std::mutex> g(buf_mu_);
   auto it = bufs_.find(a.uid);
+  const bool checks = debug_checks.load(std::memory_order_relaxed);
+  void* keep = nullptr;  // old replica whose contents move into a guarded one
+  uint64_t keep_bytes = 0;
   if (it != bufs_.end()) {
-    if (it->second.second >= a.bytes) return it->second.first;
-    (void)hipFree(it->second.first);
-    bytes_allocated_ -= it->second.second;
+    void* d = it->second.first;
+    const uint64_t cap = it->second.second;  // usable bytes (a guard, if any, lies past them)
+    if (cap >= a.bytes) {
+      if (!checks) return d;
+      auto gi = guarded_.find(a.uid);
+      if (gi != guarded_.end() && gi->second == a.bytes) return d;
+      // Debug checks need the guard right at the current extent: re-stamp it
+      // there when the allocation has room (a guarded buffer reused at a
+      // smaller size has), else move the contents into a guarded allocation.
+      const uint64_t room = gi != guarded_.end() ? gi->second + kGuardBytes : cap;
+      if (room >= a.bytes + kGuardBytes) {
+        set_device();
+        CEK_HIP(hipMemset(static_cast<char*>(d) + a.bytes, kGuardByte, kGuardBytes));
+        guarded_[a.uid] = a.bytes;
+        return d;
+      }
+      keep = d;
+      keep_bytes = std::min<uint64_t>(cap, a.bytes);
+    } else {
+      (void)hipFree(d);
+    }
+    bytes_allocated_ -= cap;
     bufs_.erase(it);
   }
   void* d = nullptr;
   set_device();
-  const size_t guard = debug_checks ? kGuardBytes : 0;
+  const size_t guard = checks ? kGuardBytes : 0;
   hipError_t e = hipMalloc(&d, (a.bytes ? a.bytes : 1) + guard);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     throw Error("hipMalloc of " + std::to_string(a.bytes) + " bytes failed on " + dev_.name);
+  }
+  if (keep) {
+    CEK_HIP(hipMemcpy(d, keep, keep_bytes, hipMemcpyDeviceToDevice));
+    (void)hipFree(keep);
   }
   if (guard) {
     CEK_HIP(hipMemset(static_cast<char*>(d) + a.bytes, kGuardByte, guard));
@@ -335,7 +361,7 @@ void Worker::launch(hipStream_t s, const std::string& kernel, const std::vector<
         CEK_HIP(hipModuleLaunchKernel(d, dgrid, 1, 1, 256, 1, 1, 0, s, params.data(), nullptr));
       }
     }
-    if (debug_checks) check_guards(s, kernel, arrs);
+    if (debug_checks.load(std::memory_order_relaxed)) check_guards(s, kernel, arrs);
   } else {
     CpuRunner fn = prog_->cpu_fn(kernel);
     std::vector<void*> ptrs(arrs.size());

@@ -10,6 +10,7 @@
 // The CPU device executes the same kernel source compiled for the host on a
 // thread pool; it works directly on host memory (no copies).
 #pragma once
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <exception>
@@ -112,7 +113,8 @@ class Worker {
   // a kernel writing past the end of an array is reported by name.
   static constexpr size_t kGuardBytes = 4096;
   static constexpr unsigned char kGuardByte = 0xCE;
-  bool debug_checks = false;
+  // atomic: Cores::set_debug_checks flips it while job threads read it
+  std::atomic<bool> debug_checks{false};
   int device_enqueue_errors();
 
   // --- markers (fine-grained queue control, ClCommandQueue.cs:103-112) ---

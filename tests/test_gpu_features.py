@@ -450,3 +450,23 @@ __global__ void oob(float* x) { x[get_global_id(0) + 1] = 7.0f; }
     with pytest.raises(Exception, match=r"oob.*wrote past the end of array #0 \(4096 bytes\).*first at \+0"):
         x.compute(c, 2, "oob", 1024, 256)
     c.dispose()
+
+
+def test_debug_checks_on_buffer_allocated_before(gpu):
+    """A replica allocated while debug checks were off gets its guard when
+    the checks are turned on: device-resident contents kept, a
+    past-the-end write still named."""
+    src = """
+__global__ void ok(float* x) { x[get_global_id(0)] += 1.0f; }
+__global__ void oob(float* x) { x[get_global_id(0) + 1] = 7.0f; }
+"""
+    c = ck.ClNumberCruncher(gpu[0], src)
+    x = ck.ClArray(np.zeros(1024, np.float32))
+    x.compute(c, 1, "ok", 1024, 256)           # replica without a guard
+    x.read = False                             # from here on device-resident
+    c.debug_checks = True
+    x.compute(c, 1, "ok", 1024, 256)           # moved into a guarded replica, contents kept
+    np.testing.assert_array_equal(x.array, np.full(1024, 2.0, np.float32))
+    with pytest.raises(Exception, match=r"oob.*wrote past the end of array #0"):
+        x.compute(c, 2, "oob", 1024, 256)
+    c.dispose()
