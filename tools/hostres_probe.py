@@ -22,8 +22,13 @@ if "torch-first" in opts:  # initialise torch's HIP state first, as bench.py doe
     import torch
     torch.cuda.synchronize()
 reps = 5
-cr = ck.ClNumberCruncher(ck.ClPlatforms.all().gpus()[0], "", prebuilt=library(*GEMM_LIBS))
+if "dist" in opts:
+    from cekirdekler_amd.parallel.distributed import DistributedCruncher
+    cr = DistributedCruncher("", prebuilt=library(*GEMM_LIBS))
+else:
+    cr = ck.ClNumberCruncher(ck.ClPlatforms.all().gpus()[0], "", prebuilt=library(*GEMM_LIBS))
 g = GemmBf16(size, size, size, cruncher=cr, tile="256x256pb")
+sync_each = "sync-each" in opts
 if resident_first:  # the bench's order: device-resident computes in enqueue mode first
     for _ in range(10):
         g.run(compute_id=1, resident=True)
@@ -31,12 +36,18 @@ if resident_first:  # the bench's order: device-resident computes in enqueue mod
     for _ in range(20):
         g.run(compute_id=1, resident=True)
     cr.enqueue_mode = False
+if "verify-first" in opts:
+    g.run(compute_id=1, resident=True)
+    print("verify", g.verify(compute_id=1), flush=True)
 out = {}
 for cid, blobs in enumerate(blob_list, start=10):
     g.C.array[:] = 0
     g.run(compute_id=cid, resident=False, stream_blobs=blobs)  # warm
     ts = []
     for _ in range(reps):
+        if sync_each:
+            import torch
+            torch.cuda.synchronize()
         t = time.perf_counter()
         g.run(compute_id=cid, resident=False, stream_blobs=blobs)
         ts.append((time.perf_counter() - t) * 1e3)
