@@ -158,10 +158,12 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     err = _max_over_ranks(ctx, g.verify(compute_id=1))
     timeouts = int(_sum_over_ranks(ctx, g.spin_timeouts()))
     host_steps = max(2, min(steps, 5))
-    # host-resident: the event-driven read/compute/write pipeline, one A row
-    # panel (tile group) per blob, as many blobs as each rank has groups (≤ 8)
-    groups = g.tiles // (g.group_m * (size // g.BN)) // ctx.world
-    blobs = next((b for b in (8, 4, 2) if groups % b == 0 and groups >= b), 0) if g.can_stream() else 0
+    # host-resident: serial upload / compute / download.  The streamed event
+    # pipeline (GemmBf16.run(stream_blobs=8)) reaches 7.9-8.2 ms when calls
+    # run back to back, but after a device-wide sync (the bench's bracket)
+    # its copies stall for ~6 ms per call on this image (14 ms,
+    # profiles/hostres_streaming.md), so the bench reports the serial path.
+    blobs = 0
     host_calls = []
 
     host_piped = []

@@ -815,7 +815,10 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
   // Interleave the two half-pipelines' chunks so both read streams start early.
   for (long long k = 0; k < per_half; ++k) {
     for (int h = 0; h < halves; ++h) {
-      hipStream_t rs = wk.pipe_stream(h, 0), ks = wk.pipe_stream(h, 1), ws = wk.pipe_stream(h, 2);
+      hipStream_t rs = wk.pipe_stream(h, 0), ks = wk.pipe_stream(h, 1);
+      // writes_on_compute_stream: a blob's D2H follows its kernel on the same
+      // stream (in-stream order) instead of a write stream gated by an event
+      hipStream_t ws = pipeline_writes_on_compute_stream ? ks : wk.pipe_stream(h, 2);
       long long off = ref + h * (range / halves) + k * chunk;
       const int rsid = 17 + 3 * h, ksid = rsid + 1, wsid = rsid + 2;
       for (auto& a : c.arrays) {
@@ -836,7 +839,7 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
       ++slot;
       launch_kernels(wk, ks, c, off, chunk);
       log_op(gidx, "kernel", ksid, off, chunk);
-      if (wk.gpu()) {
+      if (wk.gpu() && ws != ks) {
         hipEvent_t ek = wk.event(slot);
         CEK_HIP(hipEventRecord(ek, ks));
         CEK_HIP(hipStreamWaitEvent(ws, ek, 0));

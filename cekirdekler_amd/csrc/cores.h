@@ -262,6 +262,8 @@ class Cores {
   // point-to-point xGMI mesh, one link per peer pair, ordered by events (no
   // host sync).  PCIe carries the array once instead of D times.
   bool peer_reads = true;
+  // event pipeline: issue each blob's D2H on its compute stream
+  bool pipeline_writes_on_compute_stream = false;
   uint64_t peer_read_min_bytes = 1u << 20;
 
  private:

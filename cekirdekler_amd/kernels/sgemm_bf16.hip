@@ -25,7 +25,8 @@
 
 namespace {
 
-template <int WM, int WN, int FM, int FN, int MODE, bool SK = false, bool NOSTORE = false, int XCH = 0>
+template <int WM, int WN, int FM, int FN, int MODE, bool SK = false, bool NOSTORE = false, int XCH = 0,
+          bool NTS = false>
 __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
                                           const uint16_t* __restrict__ A,
                                           const uint16_t* __restrict__ Bt, float* __restrict__ C,
@@ -490,6 +491,11 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     // (16 B per lane, 1 KiB per wave instruction).
     static_assert(WM == 2, "exchanged halves need two wave rows");
     const int s = (int)(u & 1);
+    if constexpr (XCH == 4) {
+      // probe build: no hand-over at all (wrong sums), to time the
+      // exchange's share of the epilogue
+      if (wr != s) return;
+    } else {
     constexpr int HALF = BM / 2 * BN;
     f32x4* wh = reinterpret_cast<f32x4*>(W + (size_t)t * BM * BN + (size_t)wr * HALF);
     if (wr != s) {
@@ -555,6 +561,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] += part[i][j];
     }
+    }  // XCH != 4
   } else if constexpr (SK) {
     if (S > 1) {
       // Every split stores its partial tile; the last of the S to arrive
@@ -609,8 +616,13 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) {
+        float* dst = &ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr];
+        if constexpr (NTS)
+          __builtin_nontemporal_store(acc[i][j][r], dst);  // C is never re-read: stream it past L2
+        else
+          *dst = acc[i][j][r];
+      }
 }
 
 }  // namespace
@@ -661,6 +673,29 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sy(
     const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
   __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
   gemm_tile<2, 4, 8, 4, 4, true, false, 2>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
+}
+
+// Probe-only builds of the exchanged-halves kernel: no C store / no
+// hand-over (each times its share of the epilogue), and nontemporal C stores.
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sy_nostore(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
+  gemm_tile<2, 4, 8, 4, 4, true, true, 2>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
+}
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sy_noxch(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
+  gemm_tile<2, 4, 8, 4, 4, true, false, 4>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
+}
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_syn(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
+  gemm_tile<2, 4, 8, 4, 4, true, false, 2, true>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
+}
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pbn(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
+  gemm_tile<2, 4, 8, 4, 4, false, false, 0, true>(dims, A, Bt, C, smem, __cek_off);
 }
 
 #define CEK_GEMM_B3_KERNEL(NAME, WM, WN, FM, FN, MODE)                                              \

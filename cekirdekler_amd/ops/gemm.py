@@ -43,6 +43,12 @@ TILES = {
     "256x256pbx": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sx"),
     # same, hand-over through the shared L2 when both splits run on one XCD
     "256x256pby": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sy"),
+    # same with nontemporal C stores; probe-only: no C store / no hand-over
+    "256x256pbyn": (256, 256, 512, "cek_sgemm_bf16_256x256pb_syn"),
+    "256x256pby_nostore": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sy_nostore"),
+    "256x256pby_noxch": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sy_noxch"),
+    # balanced-DMA ping-pong with nontemporal C stores
+    "256x256pbn": (256, 256, 512, "cek_sgemm_bf16_256x256pbn"),
     # probe only: 256x256pp without the C store (epilogue share)
     "256x256pp_nostore": (256, 256, 512, "cek_sgemm_bf16_256x256pp_nostore"),
     # ping-pong with a 4-deep BK=32 LDS ring (kernels/sgemm_pp32_bf16.hip)
@@ -75,7 +81,8 @@ F32_TILES = {
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
 SPLIT_K_TILES = {"256x256pp", "256x128pp", "256x256pb"}
 # tiles whose kernel always runs two K-splits that exchange row halves
-EXCHANGE_TILES = {"256x256pbx": 2, "256x256pby": 4}  # flag words per tile
+EXCHANGE_TILES = {"256x256pbx": 2, "256x256pby": 4, "256x256pbyn": 4, "256x256pby_nostore": 4,
+                  "256x256pby_noxch": 4}  # flag words per tile
 
 
 def to_bf16_bits(x: np.ndarray) -> np.ndarray:
@@ -205,7 +212,8 @@ class GemmBf16:
         return (self.split_k == 1 and ntm % self.group_m == 0
                 and per_wi % (ntn * self.L) == 0)
 
-    def run(self, compute_id: int = 1, resident: bool = True, stream_blobs: int = 0) -> None:
+    def run(self, compute_id: int = 1, resident: bool = True, stream_blobs: int = 0,
+            stream_event: bool = True) -> None:
         """One GEMM through compute().  ``resident``: A/B stay on the devices
         after the first call and C stays in device memory.  ``stream_blobs``
         (host-resident only): run the call through the event-driven
@@ -231,7 +239,7 @@ class GemmBf16:
             gran = self._group_work_items()
         self.dims.next_param(self.A, self.B, self.C, *self.extra).compute(
             self.cr, compute_id, self.kernel, self.global_range, self.L,
-            pipeline=streamed, pipeline_type=True, pipeline_blobs=max(1, stream_blobs),
+            pipeline=streamed, pipeline_type=stream_event, pipeline_blobs=max(1, stream_blobs),
             granularity=gran)
         self._uploaded = True
 

@@ -29,6 +29,20 @@ else:
     cr = ck.ClNumberCruncher(ck.ClPlatforms.all().gpus()[0], "", prebuilt=library(*GEMM_LIBS))
 g = GemmBf16(size, size, size, cruncher=cr, tile="256x256pb")
 sync_each = "sync-each" in opts
+cr.cores.pipeline_writes_on_compute_stream = "wcs" in opts
+if "npC" in opts:  # C in plain (registered) host memory instead of hipHostMalloc
+    e = g.C.elements_per_work_item
+    g.C = ck.ClArray(np.zeros(size * size, np.float32))
+    g.C.read = False
+    g.C.elements_per_work_item = e
+if "npAB" in opts:
+    for nm in ("A", "B"):
+        old = getattr(g, nm)
+        new = ck.ClArray(old.array.copy())
+        new.write = False
+        setattr(g, nm, new)
+hip_sync_each = "hipsync-each" in opts
+finish_each = "finish-each" in opts
 if resident_first:  # the bench's order: device-resident computes in enqueue mode first
     for _ in range(10):
         g.run(compute_id=1, resident=True)
@@ -42,14 +56,21 @@ if "verify-first" in opts:
 out = {}
 for cid, blobs in enumerate(blob_list, start=10):
     g.C.array[:] = 0
-    g.run(compute_id=cid, resident=False, stream_blobs=blobs)  # warm
+    g.run(compute_id=cid, resident=False, stream_blobs=blobs, stream_event="driver" not in opts)  # warm
     ts = []
     for _ in range(reps):
         if sync_each:
             import torch
             torch.cuda.synchronize()
+        if hip_sync_each:
+            from cekirdekler_amd import cek
+            cek.device_synchronize(0)
+        if finish_each:
+            cr.cores.finish()
         t = time.perf_counter()
-        g.run(compute_id=cid, resident=False, stream_blobs=blobs)
+        g.run(compute_id=cid, resident=False, stream_blobs=blobs, stream_event="driver" not in opts)
+        if "finish-in" in opts:
+            cr.cores.finish()  # inside the timed region: anything still in flight is counted
         ts.append((time.perf_counter() - t) * 1e3)
     # sampled check of the host C written by the last call
     rng = np.random.default_rng(cid)
