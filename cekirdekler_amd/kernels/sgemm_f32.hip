@@ -164,6 +164,157 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
 }
 
 
+// Balanced-DMA ping-pong (the bf16 "pb" schedule, kernels/sgemm_bf16.hip
+// MODE 4, on fp32 operands): the work-group's two wave groups (waves <
+// NWAVES/2 = G0, the rest = G1, one of each per SIMD) alternate between an
+// LDS-read section and an MFMA section one s_barrier apart, so each SIMD's
+// matrix pipe always has one wave issuing.  G0 stages the A tile of K-tile
+// k+1 and G1 the Bt tile of K-tile k+2, each during its own read section.
+// A: 2 LDS buffers, Bt: 3 (160 KiB at 256², BK = 32 floats).
+//   WAR: both targets were last read in the previous read sections.
+//   RAW: G0's vmcnt(0) closes its MFMA section (A k+1 retired before G0
+//        reads it); G1 ends its read section k with only B k+2 in flight.
+template <int WM, int WN, int FM, int FN>
+__device__ __forceinline__ void gemm_f32_pb_tile(const int* __restrict__ dims, const float* __restrict__ A,
+                                                 const float* __restrict__ Bt, float* __restrict__ C, char* smem,
+                                                 long long off) {
+  constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN, BK = 32;
+  constexpr int NWAVES = WM * WN, NT = 64 * NWAVES, HALF = NWAVES / 2;
+  constexpr int A_BYTES = BM * BK * 4, B_BYTES = BN * BK * 4;
+  constexpr int A_INSTR = A_BYTES / 1024 / HALF, B_INSTR = B_BYTES / 1024 / HALF;
+  static_assert(A_INSTR * HALF * 1024 == A_BYTES && B_INSTR * HALF * 1024 == B_BYTES, "staging split");
+
+  const int M = dims[0], N = dims[1], K = dims[2], GM = dims[3] > 0 ? dims[3] : 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WN, wc = wave % WN;
+  const bool g1 = wave >= HALF;
+  const int sw = wave % HALF;  // staging wave index inside its group
+  const long long t = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
+  const int ntn = N / BN, ntm = M / BM;
+  const int per_group = GM * ntn, grp = (int)(t / per_group), first = grp * GM;
+  const int gsz = min(ntm - first, GM), in_g = (int)(t % per_group);
+  const int tm = first + in_g % gsz, tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
+  const unsigned lane_off = (unsigned)(lrow * K + lchunk * 4) * 4u;
+  const char* a_wave = (const char*)(A + (size_t)(m0 + sw * A_INSTR * 8) * K);
+  const char* b_wave = (const char*)(Bt + (size_t)(n0 + sw * B_INSTR * 8) * K);
+  char* const a_base = smem;
+  char* const b_base = smem + 2 * A_BYTES;
+  auto stage_a = [&](int kt) {
+    char* base = a_base + (kt & 1) * A_BYTES;
+#pragma unroll
+    for (int j = 0; j < A_INSTR; ++j) {
+      const char* src = a_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 4;
+      __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off), (lds_void*)(base + (sw * A_INSTR + j) * 1024),
+                                       16, 0, 0);
+    }
+  };
+  auto stage_b = [&](int kt) {
+    char* base = b_base + (kt % 3) * B_BYTES;
+#pragma unroll
+    for (int j = 0; j < B_INSTR; ++j) {
+      const char* src = b_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 4;
+      __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off), (lds_void*)(base + (sw * B_INSTR + j) * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  const int fr = lane & 15, fq = lane >> 4;
+  int a_off[2], b_off[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int pc = (s * 4 + fq) ^ (lane & 7);
+    a_off[s] = (wr * 16 * FM + fr) * 128 + pc * 16;
+    b_off[s] = (wc * 16 * FN + fr) * 128 + pc * 16;
+  }
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  f32x4 fa[2][FM], fb[2][FN];
+  auto ldall = [&](int kt) {
+    const char* ab = a_base + (kt & 1) * A_BYTES;
+    const char* bb = b_base + (kt % 3) * B_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[s][j] = *(const f32x4*)(bb + b_off[s] + j * 2048);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[s][i] = *(const f32x4*)(ab + a_off[s] + i * 2048);
+    }
+  };
+  auto mmaall = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[s][i][q], fb[s][j][q], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  const int nk = K / BK;
+  if (!g1) {
+    stage_a(0);
+  } else {
+    stage_b(0);
+    if (nk > 1) stage_b(1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bar();
+  if (g1) bar();  // G1 runs one section behind
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool b_issued = g1 && kt + 2 < nk;
+    if (!g1) {
+      if (kt + 1 < nk) stage_a(kt + 1);
+    } else if (b_issued) {
+      stage_b(kt + 2);
+    }
+    ldall(kt);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (g1) {
+      if (b_issued) {
+        static_assert(B_INSTR == 8 || B_INSTR == 4, "vmcnt immediates below");
+        if constexpr (B_INSTR == 8)
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    bar();
+    mmaall();
+    if (!g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+  }
+  if (!g1) bar();  // equal barrier counts for both groups
+
+  float* ct = C + (size_t)t * BM * BN;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        __builtin_nontemporal_store(acc[i][j][r],
+                                    &ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr]);
+}
+
 // The same tile with v_mfma_f32_32x32x2_f32 (64 cycles, 32×32 outputs):
 // lane l reads A[row = l%32][8·kb + 4·(l/32) .. +3] and feeds element t to
 // the t-th of four MFMAs, which then sum over k ∈ {t, 4+t} of the 8-deep
@@ -304,6 +455,19 @@ CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256, 2, 4, 8, 4, 0)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256h, 2, 4, 8, 4, 2)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128h, 4, 2, 4, 4, 2)
 // (a register double-buffered 256×256 variant needs 256 + 57 spilled VGPRs)
+
+// Balanced-DMA ping-pong: 256×256 (A 2 × 32 KiB + Bt 3 × 32 KiB = 160 KiB LDS)
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_f32_256x256pb(
+    const int* dims, const float* A, const float* Bt, float* C, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 32 * 4];
+  gemm_f32_pb_tile<2, 4, 8, 4>(dims, A, Bt, C, smem, __cek_off);
+}
+// 256×128 (A 2 × 32 KiB + Bt 3 × 16 KiB = 112 KiB LDS)
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_f32_256x128pb(
+    const int* dims, const float* A, const float* Bt, float* C, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 128) * 32 * 4];
+  gemm_f32_pb_tile<4, 2, 4, 4>(dims, A, Bt, C, smem, __cek_off);
+}
 
 // 32×32×2 form with register double-buffered fragments (gemm_f32w_tile).
 #define CEK_GEMM_F32W_KERNEL(NAME, WM, WN, FM, FN)                                                 \

@@ -76,6 +76,9 @@ F32_TILES = {
     "256x256w": (256, 256, 512, "cek_sgemm_f32_256x256w"),
     "256x128w": (256, 128, 512, "cek_sgemm_f32_256x128w"),
     "128x128w": (128, 128, 256, "cek_sgemm_f32_128x128w"),
+    # "pb": balanced-DMA ping-pong wave groups (the bf16 pb schedule)
+    "256x256pb": (256, 256, 512, "cek_sgemm_f32_256x256pb"),
+    "256x128pb": (256, 128, 512, "cek_sgemm_f32_256x128pb"),
 }
 
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
