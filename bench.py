@@ -311,16 +311,26 @@ def bench_node_configs(world: int) -> dict:
            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                         "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
     out = {}
-    for name, script, args in (("nbody_pipeline", "nbody_pipeline.py", ["--gpus", str(world), "--pushes", "14"]),
-                               ("task_pool", "task_pool.py", ["--gpus", str(world)]),
-                               ("saxpy_1m_cpu", "saxpy_cpu.py", [])):
+    rccl = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "rccl_gemm.py"]
+    for name, cmd in (("nbody_pipeline", [sys.executable, "nbody_pipeline.py", "--gpus", str(world), "--pushes", "14"]),
+                      ("task_pool", [sys.executable, "task_pool.py", "--gpus", str(world)]),
+                      ("saxpy_1m_cpu", [sys.executable, "saxpy_cpu.py"]),
+                      ("sgemm_host_resident_rccl", rccl)):
+        # own session: a timeout kills the whole process group (torchrun's ranks too)
+        p = subprocess.Popen(cmd, cwd=os.path.join(ROOT, "bench"), env=env, stdout=subprocess.PIPE,
+                             stderr=subprocess.PIPE, text=True, start_new_session=True)
         try:
-            r = subprocess.run([sys.executable, script, *args], cwd=os.path.join(ROOT, "bench"),
-                               env=env, capture_output=True, text=True, timeout=180)
-            lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-            out[name] = json.loads(lines[-1]) if (r.returncode == 0 and lines) else {
-                "error": f"exit {r.returncode}: {(r.stderr or r.stdout)[-300:]}"}
+            so, se = p.communicate(timeout=180)
+            lines = [ln for ln in so.splitlines() if ln.startswith("{")]
+            out[name] = json.loads(lines[-1]) if (p.returncode == 0 and lines) else {
+                "error": f"exit {p.returncode}: {(se or so)[-300:]}"}
         except Exception as e:  # timeout or parse failure
+            try:
+                os.killpg(p.pid, 9)
+            except OSError:
+                pass
+            p.communicate()
             out[name] = {"error": repr(e)[:300]}
     return out
 
@@ -426,6 +436,7 @@ def main(argv=None) -> int:
                 "nbody_pipeline": node.get("nbody_pipeline"),
                 "task_pool": node.get("task_pool"),
                 "saxpy_1m_cpu": node.get("saxpy_1m_cpu"),
+                "sgemm_host_resident_rccl": node.get("sgemm_host_resident_rccl"),
             },
         }
         print(json.dumps(out), flush=True)
