@@ -44,7 +44,8 @@ def step():
 
 step()
 step()
-dist.barrier()
+if ctx.is_distributed:
+    dist.barrier()
 sync()
 t0 = time.perf_counter()
 for _ in range(a.steps):
@@ -84,8 +85,10 @@ for r in range(ctx.world):
     if n:
         picks += [lo, lo + n - 1]
 err_gather = max(tile_err(g.C.array, t) for t in picks)
-errs = [None] * ctx.world
-dist.all_gather_object(errs, (err_split, err_gather, ms, rec["h2d_bytes"]))
+errs = [(err_split, err_gather, ms, rec["h2d_bytes"])]
+if ctx.is_distributed:
+    errs = [None] * ctx.world
+    dist.all_gather_object(errs, (err_split, err_gather, ms, rec["h2d_bytes"]))
 if ctx.rank == 0:
     print(json.dumps({"config": "sgemm_host_resident_rccl", "ranks": ctx.world, "size": size,
                       "split_reads_ms": max(e[2] for e in errs),
@@ -94,5 +97,6 @@ if ctx.rank == 0:
                       "max_rel_err_split_reads": max(e[0] for e in errs),
                       "max_rel_err_gathered_replicas": max(e[1] for e in errs)}), flush=True)
 cr.dispose()
-dist.barrier()
-dist.destroy_process_group()
+if ctx.is_distributed:
+    dist.barrier()
+    dist.destroy_process_group()

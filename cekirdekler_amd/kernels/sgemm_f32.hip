@@ -455,6 +455,13 @@ CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256, 2, 4, 8, 4, 0)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256h, 2, 4, 8, 4, 2)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128h, 4, 2, 4, 4, 2)
 // (a register double-buffered 256×256 variant needs 256 + 57 spilled VGPRs)
+// 256×256 tiles with 4 waves of 128×128 (one wave per SIMD, 512 registers
+// per lane: the 256 accumulator registers go to AGPRs): twice the MFMAs per
+// fragment byte of the 8-wave 128×64 layout, as hipBLASLt's MT256x256x32
+// fp32 kernel (1 wave per SIMD, 98 % MFMA-busy: profiles/gemm_f32_pmc.md).
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q, 2, 2, 8, 8, 1)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q0, 2, 2, 8, 8, 0)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q2, 2, 2, 8, 8, 2)
 
 // Balanced-DMA ping-pong: 256×256 (A 2 × 32 KiB + Bt 3 × 32 KiB = 160 KiB LDS)
 extern "C" __global__ __launch_bounds__(512) void cek_sgemm_f32_256x256pb(

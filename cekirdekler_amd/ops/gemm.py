@@ -79,6 +79,10 @@ F32_TILES = {
     # "pb": balanced-DMA ping-pong wave groups (the bf16 pb schedule)
     "256x256pb": (256, 256, 512, "cek_sgemm_f32_256x256pb"),
     "256x128pb": (256, 128, 512, "cek_sgemm_f32_256x128pb"),
+    # "q": 4 waves of 128×128 (one per SIMD), register double-buffered / plain / both blocks up front
+    "256x256q": (256, 256, 256, "cek_sgemm_f32_256x256q"),
+    "256x256q0": (256, 256, 256, "cek_sgemm_f32_256x256q0"),
+    "256x256q2": (256, 256, 256, "cek_sgemm_f32_256x256q2"),
 }
 
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)

@@ -10,9 +10,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import cekirdekler_amd as ck  # noqa: E402
 from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer  # noqa: E402
 
+import numpy as np  # noqa: E402
+
 m = MandelbrotRenderer(4096, 4096, 256, devices=ck.ClPlatforms.all().gpus()[0])
 res = {}
-for wcs in (False, True):
+if "np" in sys.argv[1:]:  # image in registered numpy memory instead of hipHostMalloc
+    e = m.out.elements_per_work_item
+    m.out = ck.ClArray(np.zeros(4096 * 4096, np.int32))
+    m.out.read = False
+    m.out.elements_per_work_item = e
+for wcs in ((False,) if "np" in sys.argv[1:] else (False, True)):
     m.cr.cores.pipeline_writes_on_compute_stream = wcs
     for blobs in (4, 8, 16):
         for fin in (False, True):
