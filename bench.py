@@ -261,7 +261,7 @@ def bench_mandelbrot(ctx, steps, warmup):
     ms = timed(ctx, lambda: m.render(compute_id=3, pipeline=True), max(3, steps // 2), warmup)
     flops = _sum_over_ranks(ctx, m.flops())
     out = {"ms": ms, "gflops": flops / (ms * 1e-3) / 1e9, "flop_per_iter": 8, "kernel": m.kernel,
-           "image_pinned": m.out.fast_arr and m.out._fast.pinned}
+           "image_pinned": m.out.pinned}
     cr.dispose()
     return out
 
