@@ -102,7 +102,53 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (PIPE == 2) {
+  if constexpr (PIPE == 3) {
+    // one wave per SIMD: both k blocks' fragments read up front, then the
+    // next K-tile's LDS-DMA pieces issued one by one between groups of
+    // MFMAs, so their issue cost hides in the MFMA stream instead of
+    // stalling the only wave on the SIMD before it
+    constexpr int NGLDS = A_INSTR + B_INSTR;
+    static_assert(NGLDS % 8 == 0, "pieces spread over the 8 (block, q) MFMA groups");
+    constexpr int PER_GROUP = NGLDS / 8;
+    auto stage_one = [&](int buf, int kt, int g) {
+      char* base = smem + buf * STAGE;
+      if (g < A_INSTR) {
+        const char* src = a_wave + ((size_t)g * 8 * K + (size_t)kt * BK) * 4;
+        __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
+                                         (lds_void*)(base + (wave * A_INSTR + g) * 1024), 16, 0, 0);
+      } else {
+        const int j = g - A_INSTR;
+        const char* src = b_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 4;
+        __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
+                                         (lds_void*)(base + A_BYTES + (wave * B_INSTR + j) * 1024), 16, 0, 0);
+      }
+    };
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      const char* base = smem + cur * STAGE;
+      const bool pre = kt + 1 < nk;
+      f32x4 fa[2][FM], fb[2][FN];
+      ld(fa[0], fb[0], base, 0);
+      ld(fa[1], fb[1], base, 1);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int sq = 0; sq < 8; ++sq) {
+        const int sb = sq / 4, q = sq % 4;
+        if (pre) {
+#pragma unroll
+          for (int p2 = 0; p2 < PER_GROUP; ++p2) stage_one(cur ^ 1, kt + 1, sq * PER_GROUP + p2);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[sb][i][q], fb[sb][j][q], acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else if constexpr (PIPE == 2) {
     // both 16-deep k blocks' fragments are read up front: the second block's
     // ds_reads fly under the first block's MFMAs (2 fragment sets live, no
     // carry across the barrier, unlike PIPE == 1)
@@ -462,6 +508,8 @@ CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128h, 4, 2, 4, 4, 2)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q, 2, 2, 8, 8, 1)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q0, 2, 2, 8, 8, 0)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q2, 2, 2, 8, 8, 2)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q3, 2, 2, 8, 8, 3)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256i, 2, 4, 8, 4, 3)
 
 // Balanced-DMA ping-pong: 256×256 (A 2 × 32 KiB + Bt 3 × 32 KiB = 160 KiB LDS)
 extern "C" __global__ __launch_bounds__(512) void cek_sgemm_f32_256x256pb(

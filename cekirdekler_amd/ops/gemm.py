@@ -83,6 +83,9 @@ F32_TILES = {
     "256x256q": (256, 256, 256, "cek_sgemm_f32_256x256q"),
     "256x256q0": (256, 256, 256, "cek_sgemm_f32_256x256q0"),
     "256x256q2": (256, 256, 256, "cek_sgemm_f32_256x256q2"),
+    # fragments up front, next K-tile's LDS-DMA interleaved through the MFMAs
+    "256x256q3": (256, 256, 256, "cek_sgemm_f32_256x256q3"),
+    "256x256i": (256, 256, 512, "cek_sgemm_f32_256x256i"),
 }
 
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
