@@ -102,14 +102,17 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (PIPE == 3) {
+  if constexpr (PIPE == 3 || PIPE == 4) {
     // one wave per SIMD: both k blocks' fragments read up front, then the
     // next K-tile's LDS-DMA pieces issued one by one between groups of
     // MFMAs, so their issue cost hides in the MFMA stream instead of
     // stalling the only wave on the SIMD before it
+    // PIPE 3: spread over all 8 (block, q) MFMA groups; PIPE 4: all within
+    // block 0's four groups, so the pieces have block 1's MFMAs to land
+    // before the vmcnt(0) that closes the K-tile
     constexpr int NGLDS = A_INSTR + B_INSTR;
-    static_assert(NGLDS % 8 == 0, "pieces spread over the 8 (block, q) MFMA groups");
-    constexpr int PER_GROUP = NGLDS / 8;
+    constexpr int NGROUPS = PIPE == 4 ? 4 : 8;
+    constexpr int PER_GROUP = (NGLDS + NGROUPS - 1) / NGROUPS;
     auto stage_one = [&](int buf, int kt, int g) {
       char* base = smem + buf * STAGE;
       if (g < A_INSTR) {
@@ -134,9 +137,10 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
 #pragma unroll
       for (int sq = 0; sq < 8; ++sq) {
         const int sb = sq / 4, q = sq % 4;
-        if (pre) {
+        if (pre && sq < NGROUPS) {
 #pragma unroll
-          for (int p2 = 0; p2 < PER_GROUP; ++p2) stage_one(cur ^ 1, kt + 1, sq * PER_GROUP + p2);
+          for (int p2 = 0; p2 < PER_GROUP; ++p2)
+            if (sq * PER_GROUP + p2 < NGLDS) stage_one(cur ^ 1, kt + 1, sq * PER_GROUP + p2);
         }
 #pragma unroll
         for (int i = 0; i < FM; ++i)
@@ -510,6 +514,8 @@ CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q0, 2, 2, 8, 8, 0)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q2, 2, 2, 8, 8, 2)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q3, 2, 2, 8, 8, 3)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256i, 2, 4, 8, 4, 3)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ie, 2, 4, 8, 4, 4)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128ie, 4, 2, 4, 4, 4)
 
 // Balanced-DMA ping-pong: 256×256 (A 2 × 32 KiB + Bt 3 × 32 KiB = 160 KiB LDS)
 extern "C" __global__ __launch_bounds__(512) void cek_sgemm_f32_256x256pb(

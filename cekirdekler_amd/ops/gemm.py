@@ -86,6 +86,9 @@ F32_TILES = {
     # fragments up front, next K-tile's LDS-DMA interleaved through the MFMAs
     "256x256q3": (256, 256, 256, "cek_sgemm_f32_256x256q3"),
     "256x256i": (256, 256, 512, "cek_sgemm_f32_256x256i"),
+    # same, every piece issued within the first k block's MFMAs
+    "256x256ie": (256, 256, 512, "cek_sgemm_f32_256x256ie"),
+    "256x128ie": (256, 128, 512, "cek_sgemm_f32_256x128ie"),
 }
 
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
