@@ -102,7 +102,7 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (PIPE == 3 || PIPE == 4) {
+  if constexpr (PIPE == 3 || PIPE == 4 || PIPE == 5) {
     // one wave per SIMD: both k blocks' fragments read up front, then the
     // next K-tile's LDS-DMA pieces issued one by one between groups of
     // MFMAs, so their issue cost hides in the MFMA stream instead of
@@ -111,7 +111,7 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
     // block 0's four groups, so the pieces have block 1's MFMAs to land
     // before the vmcnt(0) that closes the K-tile
     constexpr int NGLDS = A_INSTR + B_INSTR;
-    constexpr int NGROUPS = PIPE == 4 ? 4 : 8;
+    constexpr int NGROUPS = PIPE == 4 ? 4 : 8;  // PIPE 5 spreads like PIPE 3
     constexpr int PER_GROUP = (NGLDS + NGROUPS - 1) / NGROUPS;
     auto stage_one = [&](int buf, int kt, int g) {
       char* base = smem + buf * STAGE;
@@ -132,11 +132,25 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
       const bool pre = kt + 1 < nk;
       f32x4 fa[2][FM], fb[2][FN];
       ld(fa[0], fb[0], base, 0);
-      ld(fa[1], fb[1], base, 1);
+      if constexpr (PIPE != 5) ld(fa[1], fb[1], base, 1);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int sq = 0; sq < 8; ++sq) {
         const int sb = sq / 4, q = sq % 4;
+        if constexpr (PIPE == 5) {
+          // block 1's fragment reads ride between block 0's MFMA groups
+          constexpr int NRD = FM + FN, PER_RD = (NRD + 3) / 4;
+          if (sq < 4) {
+#pragma unroll
+            for (int r = 0; r < PER_RD; ++r) {
+              const int x = sq * PER_RD + r;
+              if (x < FN)
+                fb[1][x] = *(const f32x4*)(base + b_off[1] + x * 2048);
+              else if (x < NRD)
+                fa[1][x - FN] = *(const f32x4*)(base + a_off[1] + (x - FN) * 2048);
+            }
+          }
+        }
         if (pre && sq < NGROUPS) {
 #pragma unroll
           for (int p2 = 0; p2 < PER_GROUP; ++p2)
@@ -515,6 +529,7 @@ CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q2, 2, 2, 8, 8, 2)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q3, 2, 2, 8, 8, 3)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256i, 2, 4, 8, 4, 3)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ie, 2, 4, 8, 4, 4)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ir, 2, 4, 8, 4, 5)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128ie, 4, 2, 4, 4, 4)
 
 // Balanced-DMA ping-pong: 256×256 (A 2 × 32 KiB + Bt 3 × 32 KiB = 160 KiB LDS)

@@ -89,6 +89,8 @@ F32_TILES = {
     # same, every piece issued within the first k block's MFMAs
     "256x256ie": (256, 256, 512, "cek_sgemm_f32_256x256ie"),
     "256x128ie": (256, 128, 512, "cek_sgemm_f32_256x128ie"),
+    # "i" with block 1's fragment reads between block 0's MFMA groups
+    "256x256ir": (256, 256, 512, "cek_sgemm_f32_256x256ir"),
 }
 
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
