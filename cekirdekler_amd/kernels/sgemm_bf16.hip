@@ -44,7 +44,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   // split — G0 stages the A tile during its read section, G1 stages the B
   // tile of the K-tile after next at the start of its MFMA section, so each
   // DMA has ~1.5 sections to land.
-  constexpr int STAGERS = MODE >= 2 ? NWAVES / 2 : NWAVES;
+  constexpr int STAGERS = (MODE >= 2 && MODE != 7) ? NWAVES / 2 : NWAVES;  // MODE 7: every wave stages
   constexpr int A_INSTR = A_BYTES / 1024 / STAGERS;
   constexpr int B_INSTR = B_BYTES / 1024 / STAGERS;
 
@@ -79,7 +79,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
   // per-lane 32-bit byte offset + wave-uniform 64-bit base (saddr form)
   const unsigned lane_off = (unsigned)(lrow * K + lchunk * 8) * 2u;
-  const int sw = MODE >= 2 ? wave % (NWAVES / 2) : wave;  // staging wave index
+  const int sw = (MODE >= 2 && MODE != 7) ? wave % (NWAVES / 2) : wave;  // staging wave index
   const char* a_wave = (const char*)(A + (size_t)(m0 + sw * A_INSTR * 8) * K);
   const char* b_wave = (const char*)(Bt + (size_t)(n0 + sw * B_INSTR * 8) * K);
 
@@ -193,6 +193,57 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       __syncthreads();
       if (kt + 1 < nk) ld(xa, xb, smem + (cur ^ 1) * STAGE, 0);
       mma(ya, yb);
+    }
+  } else if constexpr (MODE == 7) {
+    // Both k-steps' fragments read up front, the next K-tile's LDS-DMA
+    // pieces issued one at a time between the (k-step, row-block) MFMA
+    // groups, spread evenly, so their issue cost lands between MFMAs of
+    // this wave (the other wave on the SIMD keeps the matrix pipe busy)
+    // instead of in front of them; one vmcnt(0) + barrier per K-tile.
+    constexpr int NP = A_INSTR + B_INSTR, NG = 2 * FM;
+    bf16x8 fa[2][FM], fb[2][FN];
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      const char* base = smem + cur * STAGE;
+      const bool pre = kt + 1 < nk;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[s2][j] = *(const bf16x8*)(base + b_off[s2] + j * 2048);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[s2][i] = *(const bf16x8*)(base + a_off[s2] + i * 2048);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        if (pre) {
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+            if ((p * NG) / NP != g) continue;  // piece p goes to group p·NG/NP
+            char* sb = smem + (cur ^ 1) * STAGE;
+            if (p < A_INSTR) {
+              const char* src = a_wave + ((size_t)p * 8 * K + (size_t)(ks + kt + 1) * BK) * 2;
+              __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
+                                               (lds_void*)(sb + (sw * A_INSTR + p) * 1024), 16, 0, 0);
+            } else {
+              const int q = p - A_INSTR;
+              const char* src = b_wave + ((size_t)q * 8 * K + (size_t)(ks + kt + 1) * BK) * 2;
+              __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
+                                               (lds_void*)(sb + A_BYTES + (sw * B_INSTR + q) * 1024), 16, 0, 0);
+            }
+          }
+        }
+        const int s2 = g / FM, i = g % FM;
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s2][i], fb[s2][j], acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
     }
   } else if constexpr (MODE == 2) {
     // Ping-pong.  Interval n (between two block barriers): one group runs its
@@ -721,6 +772,9 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x128pe(
 
 // 256×256 tiles, 8 waves (2×4, 128×64 each), 128 KiB LDS, 1 block/CU.
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256, 2, 4, 8, 4, 0)
+// LDS-DMA pieces interleaved between MFMA groups (MODE 7)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256i, 2, 4, 8, 4, 7)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128i, 4, 2, 4, 4, 7)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256p, 2, 4, 8, 4, 1)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256pp, 2, 4, 8, 4, 2)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256ps, 2, 4, 8, 4, 3)

@@ -47,6 +47,9 @@ TILES = {
     "256x256pbyn": (256, 256, 512, "cek_sgemm_bf16_256x256pb_syn"),
     "256x256pby_nostore": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sy_nostore"),
     "256x256pby_noxch": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sy_noxch"),
+    # LDS-DMA pieces interleaved between MFMA groups, 2 waves per SIMD in step
+    "256x256i": (256, 256, 512, "cek_sgemm_bf16_256x256i"),
+    "256x128i": (256, 128, 512, "cek_sgemm_bf16_256x128i"),
     # balanced-DMA ping-pong with nontemporal C stores
     "256x256pbn": (256, 256, 512, "cek_sgemm_bf16_256x256pbn"),
     # probe only: 256x256pp without the C store (epilogue share)
@@ -338,7 +341,7 @@ class GemmF32(GemmBf16):
     (same grouped tile order, so the same range partitioning and
     wave-quantized balancing apply)."""
 
-    def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256",
+    def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256ir",
                  cruncher: ClNumberCruncher | None = None, fill: str = "random", seed: int = 0,
                  group_m: int = 4, wave_granularity: bool | None = None):
         # 256x256: 140 TF/s at 8192³, 91 % of hipBLASLt fp32 (profiles/gemm_f32_findings.md)

@@ -19,7 +19,7 @@ LIBRARY = {
                    "cek_sgemm_bf16_128x128", "cek_sgemm_bf16_128x128p",
                    "cek_sgemm_bf16_256x256pp_sk", "cek_sgemm_bf16_256x128pp_sk", "cek_sgemm_bf16_256x256pb_sk", "cek_sgemm_bf16_256x256pb_sx", "cek_sgemm_bf16_256x256pb_sy",
                    "cek_sgemm_bf16_256x256pb_sy_nostore", "cek_sgemm_bf16_256x256pb_sy_noxch", "cek_sgemm_bf16_256x256pb_syn",
-                   "cek_sgemm_bf16_256x256pbn",
+                   "cek_sgemm_bf16_256x256pbn", "cek_sgemm_bf16_256x256i", "cek_sgemm_bf16_256x128i",
                    "cek_sgemm_bf16_256x256pp_nostore", "cek_sgemm_bf16_256x256pb", "cek_sgemm_bf16_256x128pb",
                    "cek_sgemm_bf16_256x256pc", "cek_sgemm_bf16_256x128pc",
                    "cek_sgemm_bf16_256x128pe"],

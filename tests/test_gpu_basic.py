@@ -56,7 +56,8 @@ def test_logical_devices_pipelines(pipeline, ptype):
 
 @pytest.mark.parametrize("tile", ["256x256", "256x256p", "256x256pp", "256x256ps", "256x128", "256x128p", "256x128pp", "256x128ps",
                                   "128x128", "128x128p", "256x256e8", "256x256e10", "256x256q", "256x128q",
-                                  "256x256pb", "256x128pb", "256x256pc", "256x128pc", "256x128pe"])
+                                  "256x256pb", "256x128pb", "256x256pc", "256x128pc", "256x128pe",
+                                  "256x256i", "256x128i", "256x256pbn"])
 def test_gemm_bf16_matches_fp64(tile):
     from cekirdekler_amd.ops.gemm import GemmBf16
 
