@@ -136,3 +136,39 @@ def test_cl_pipeline_multi_device_stages_stay_on_device():
     r1 = s1.cruncher.ranges(1)
     assert len(set(r1)) > 1, r1             # the split really was uneven
     pipe.dispose()
+
+
+def test_cl_pipeline_mixed_cpu_gpu_stage():
+    """A stage spanning the CPU device and a GPU: the CPU device's replica
+    is the host array itself, the GPU's is device memory; the copy engine
+    moves each slice from whichever device computed it (host↔GPU copies
+    for the mixed stage, GPU→GPU pulls elsewhere)."""
+    from cekirdekler_amd.parallel.pipeline import ClPipelineStage
+
+    plats = ck.ClPlatforms.all()
+    g0, cpu = plats.gpus()[0], plats.cpus(True)
+    n = 1 << 14
+    k1 = "__global__ void f1(const float* x, float* y) { long long i = get_global_id(0); y[i] = x[i] * 2.0f + (float)i; }"
+    k2 = "__global__ void f2(const float* y, float* z) { long long i = get_global_id(0); z[i] = y[i] + 1.0f; }"
+    s1, s2 = ClPipelineStage(), ClPipelineStage()
+    s1.add_devices(g0 + cpu)
+    s1.add_kernels(k1, "f1", [n], [64])
+    s1.add_input_buffers(np.zeros(n, np.float32))
+    s1.add_output_buffers(np.zeros(n, np.float32))
+    s2.add_devices(g0)
+    s2.add_kernels(k2, "f2", [n], [64])
+    s2.add_input_buffers(np.zeros(n, np.float32))
+    s2.add_output_buffers(np.zeros(n, np.float32))
+    s1.prepend_to_stage(s2)
+    pipe = s1.make_pipeline()
+    i = np.arange(n, dtype=np.float32)
+    res = np.zeros(n, np.float32)
+    seen = 0
+    for p in range(10):
+        if pipe.push_data([np.full(n, float(p), np.float32)], [res]):
+            np.testing.assert_array_equal(res, np.float32(seen) * 2 + i + 1)
+            seen += 1
+    assert seen == 6
+    r = s1.cruncher.ranges(1)
+    assert all(x > 0 for x in r), r  # both devices computed a slice
+    pipe.dispose()
