@@ -32,8 +32,10 @@
 //     the pool of which `taken` have been handed out, the limit is N/10
 //     until 10 % are out, N/20 until 20 %, N/33 until 33 %, N/50 until half,
 //     then 2 (1 once fewer than 3 remain), divided by the device count and
-//     clamped to [1, max_in_flight] — deep queues while the pool is full,
-//     shallow ones in the tail so the last tasks spread over every device;
+//     clamped to [min(2, max_in_flight), max_in_flight] — deep queues while
+//     the pool is full, shallow ones in the tail so the last tasks spread
+//     over every device (the floor of 2 is ours: one task in flight leaves
+//     the device idle for the host turnaround between tasks);
 //   * each device keeps a smoothed marker-reach speed (markers retired per
 //     ms, 15-sample moving average).
 #pragma once

@@ -191,8 +191,8 @@ def test_queue_limit_shrinks_as_pool_drains():
     pool.enqueue_task_pool(tp)
     pool.finish()
     h = pool.queue_limit_history()
-    # 400 tasks / 2 devices: 20 → 10 → 6 → 4 → 1 (and 1 at the tail)
-    assert h[0] == 16 and h[-1] == 1, h          # N/10/2 = 20 clamped to 16 queues
+    # 400 tasks / 2 devices: 20 → 10 → 6 → 4 → 1, floored at 2 in flight
+    assert h[0] == 16 and h[-1] == 2, h          # N/10/2 = 20 clamped to 16 queues
     assert all(a >= b for a, b in zip(h, h[1:])), h
     assert {10, 6, 4}.issubset(h), h
     assert len(pool.marker_reach_speeds()) == 2
