@@ -22,7 +22,7 @@
 
 namespace {
 
-template <int WM, int WN, int FM, int FN, int PIPE>
+template <int WM, int WN, int FM, int FN, int PIPE, bool NTS = false>
 __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, const float* __restrict__ A,
                                               const float* __restrict__ Bt, float* __restrict__ C, char* smem,
                                               long long off) {
@@ -223,8 +223,13 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) {
+        float* dst = &ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr];
+        if constexpr (NTS)
+          __builtin_nontemporal_store(acc[i][j][r], dst);
+        else
+          *dst = acc[i][j][r];
+      }
 }
 
 
@@ -530,6 +535,12 @@ CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q3, 2, 2, 8, 8, 3)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256i, 2, 4, 8, 4, 3)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ie, 2, 4, 8, 4, 4)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ir, 2, 4, 8, 4, 5)
+// same with nontemporal C stores
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_f32_256x256irn(
+    const int* dims, const float* A, const float* Bt, float* C, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * (256 + 256) * 32 * 4];
+  gemm_f32_tile<2, 4, 8, 4, 5, true>(dims, A, Bt, C, smem, __cek_off);
+}
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128ie, 4, 2, 4, 4, 4)
 
 // Balanced-DMA ping-pong: 256×256 (A 2 × 32 KiB + Bt 3 × 32 KiB = 160 KiB LDS)

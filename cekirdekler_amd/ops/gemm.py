@@ -94,6 +94,7 @@ F32_TILES = {
     "256x128ie": (256, 128, 512, "cek_sgemm_f32_256x128ie"),
     # "i" with block 1's fragment reads between block 0's MFMA groups
     "256x256ir": (256, 256, 512, "cek_sgemm_f32_256x256ir"),
+    "256x256irn": (256, 256, 512, "cek_sgemm_f32_256x256irn"),  # + nontemporal C stores
 }
 
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)

@@ -21,7 +21,9 @@ tiles = (sys.argv[2] if len(sys.argv) > 2 else "128x128,256x128,256x256").split(
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 steps = int(sys.argv[4]) if len(sys.argv) > 4 else 5
 dev = ck.ClPlatforms.all().gpus()[0]
-runs = {t: GemmF32(n, n, n, devices=dev, tile=t) for t in tiles}
+# a tile may carry its tile-group height: "256x256ir@8"
+runs = {t: GemmF32(n, n, n, devices=dev, tile=t.split("@")[0], group_m=int(t.split("@")[1]) if "@" in t else 4)
+        for t in tiles}
 for g in runs.values():
     g.run(resident=True)
 torch.backends.cuda.matmul.allow_tf32 = False
