@@ -272,6 +272,21 @@ static inline void __threadfence() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
 struct __CekFibers { ucontext_t sched; ucontext_t* items; int cur; };
 static thread_local __CekFibers* __cek_fib = nullptr;
 static inline void __syncthreads() { if (__cek_fib) swapcontext(&__cek_fib->items[__cek_fib->cur], &__cek_fib->sched); }
+// Typed call of a kernel from the runner's void* argument array: the
+// parameter types come from the kernel's own signature, so the call is a
+// direct call the compiler can inline into the work-item loop (and
+// vectorize), not a call through a function pointer of another type.
+template <unsigned long long... I> struct __CekSeq {};
+template <unsigned long long N, unsigned long long... I> struct __CekMakeSeq : __CekMakeSeq<N - 1, N - 1, I...> {};
+template <unsigned long long... I> struct __CekMakeSeq<0, I...> { using type = __CekSeq<I...>; };
+template <class... P, unsigned long long... I>
+static inline __attribute__((always_inline)) void __cek_call_i(void (*f)(P...), void** a, __CekSeq<I...>) {
+  f(reinterpret_cast<P>(a[I])...);
+}
+template <class... P>
+static inline __attribute__((always_inline)) void __cek_call(void (*f)(P...), void** a) {
+  __cek_call_i(f, a, typename __CekMakeSeq<sizeof...(P)>::type{});
+}
 #define get_global_id(d) ((d) == 0 ? ((long long)blockIdx.x * (long long)blockDim.x + (long long)threadIdx.x + __cek_off) : 0ll)
 #define get_local_id(d) ((long long)((d) == 0 ? threadIdx.x : 0))
 #define get_group_id(d) ((long long)((d) == 0 ? blockIdx.x : 0))
@@ -460,21 +475,19 @@ std::string cpu_rewrite(const std::string& src) {
   for (auto& k : sites) {
     if (!seen.insert(k.sig.name).second) continue;
     const std::string& n = k.sig.name;
-    std::ostringstream call, ptype;
-    call << "reinterpret_cast<void (*)(";
-    for (int i = 0; i < k.sig.arity; ++i) call << (i ? ", " : "") << "void*";
-    call << ")>(&" << n << ")(";
-    for (int i = 0; i < k.sig.arity; ++i) call << (i ? ", " : "") << "args[" << i << "]";
-    call << ")";
-    std::string c = call.str();
+    std::string c = "__cek_call(&" + n + ", args)";
     if (!barriers) {
+      // whole work-groups per outer iteration (the pool hands out multiples
+      // of L), so the inner loop only advances threadIdx.x
       os << "extern \"C\" void __cek_run_" << n
          << "(void** args, long long off, long long gsize, long long first, long long count, int L) {\n"
-         << "  (void)args; __cek_off = off; __cek_gsize = gsize; blockDim.x = (unsigned)L;\n"
+         << "  __cek_off = off; __cek_gsize = gsize; blockDim.x = (unsigned)L;\n"
          << "  gridDim.x = (unsigned)(gsize / L);\n"
-         << "  for (long long i = first; i < first + count; ++i) {\n"
-         << "    long long r = i - off; blockIdx.x = (unsigned)(r / L); threadIdx.x = (unsigned)(r % L);\n"
-         << "    " << c << ";\n  }\n}\n";
+         << "  for (long long g0 = first; g0 < first + count; g0 += L) {\n"
+         << "    blockIdx.x = (unsigned)((g0 - off) / L);\n"
+         << "    const int n_items = (int)std::min<long long>(L, first + count - g0);\n"
+         << "    for (int t = 0; t < n_items; ++t) { threadIdx.x = (unsigned)t; " << c << "; }\n"
+         << "  }\n}\n";
     } else {
       // Fiber runner: whole groups only (first/count multiples of L).
       os << "static thread_local void** __cek_args_" << n << ";\n"
@@ -581,7 +594,14 @@ bool compile_cpu(const std::string& rsrc, const std::vector<std::string>& option
   const char* cxx_env = getenv("CEK_CXX");
   std::string cxx = cxx_env && *cxx_env ? cxx_env : "g++";
   // -ffp-contract=off: results match the host reference (numpy) bit-for-bit.
-  std::string flags = "-O3 -march=native -ffp-contract=off -fPIC -shared -std=c++17 -w";
+  // -fno-semantic-interposition: the runner's call of an extern "C" kernel
+  // in the same .so is a direct, inlinable call (not through the PLT), so
+  // the work-item loop vectorizes; -ftls-model=local-dynamic: the work-item
+  // index variables (thread_local) cost one __tls_get_addr per runner call
+  // instead of one per work item.
+  std::string flags =
+      "-O3 -march=native -ffp-contract=off -fPIC -shared -std=c++17 -w -fno-semantic-interposition "
+      "-ftls-model=local-dynamic";
   for (auto& o : options) flags += " " + o;
   std::string key = hash_hex(rsrc + "\x01" + cxx + "\x01" + flags);
   std::string dir = cache_dir();
