@@ -316,6 +316,7 @@ def bench_node_configs(world: int) -> dict:
     for name, cmd in (("nbody_pipeline", [sys.executable, "nbody_pipeline.py", "--gpus", str(world), "--pushes", "14"]),
                       ("task_pool", [sys.executable, "task_pool.py", "--gpus", str(world)]),
                       ("saxpy_1m_cpu", [sys.executable, "saxpy_cpu.py"]),
+                      ("wave_cpu_gpu", [sys.executable, "wave_cpu_gpu.py"]),
                       ("sgemm_host_resident_rccl", rccl)):
         # own session: a timeout kills the whole process group (torchrun's ranks too)
         p = subprocess.Popen(cmd, cwd=os.path.join(ROOT, "bench"), env=env, stdout=subprocess.PIPE,
@@ -436,6 +437,7 @@ def main(argv=None) -> int:
                 "nbody_pipeline": node.get("nbody_pipeline"),
                 "task_pool": node.get("task_pool"),
                 "saxpy_1m_cpu": node.get("saxpy_1m_cpu"),
+                "wave_cpu_gpu": node.get("wave_cpu_gpu"),
                 "sgemm_host_resident_rccl": node.get("sgemm_host_resident_rccl"),
             },
         }

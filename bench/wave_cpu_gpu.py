@@ -1,0 +1,48 @@
+"""The reference's only published speed claim, measured: the Unity wave
+example on 224×256 = 57,344 vertices, local 64, "3× as fast" with CPU+GPU
+than CPU-only (Kamera.cs:266, devices from devicesAmd(true, true)).
+
+Frames per second of WaveSurface.update() (one compute per frame, the
+displaced vertices downloaded every frame, as the Unity loop uses them) on
+the CPU device alone, the GPU alone, and GPU + CPU with the load balancer
+splitting the vertices.  Steady state after the balancer has converged."""
+import argparse
+import time
+
+import numpy as np
+
+from common import emit
+
+import cekirdekler_amd as ck
+from cekirdekler_amd.models.wave import WaveSurface, grid_mesh
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--frames", type=int, default=200)
+ap.add_argument("--nx", type=int, default=224)
+ap.add_argument("--ny", type=int, default=256)
+a = ap.parse_args()
+plats = ck.ClPlatforms.all()
+cpu, gpus = plats.cpus(True), plats.gpus()
+base, normals = grid_mesh(a.nx, a.ny)
+configs = [("cpu", cpu)]
+if len(gpus):
+    configs += [("gpu", gpus[0]), ("gpu+cpu", gpus[0] + cpu)]
+out = {"config": "wave_cpu_gpu", "vertices": len(base), "local": 64}
+for name, devs in configs:
+    w = WaveSurface(base, normals, devices=devs)
+    for _ in range(40):  # balancer converges, buffers resident
+        w.update()
+    t = time.perf_counter()
+    for _ in range(a.frames):
+        w.update()
+    ms = (time.perf_counter() - t) * 1e3 / a.frames
+    err = float(np.abs(w.update()["z"] - w.reference()["z"]).max())
+    out[f"{name}_ms_per_frame"] = ms
+    out[f"{name}_max_abs_err"] = err
+    if name == "gpu+cpu":
+        out["gpu+cpu_shares"] = [r / sum(w.cr.ranges(1)) for r in w.cr.ranges(1)]
+    w.cr.dispose()
+if "gpu+cpu_ms_per_frame" in out:
+    out["speedup_gpu+cpu_over_cpu"] = out["cpu_ms_per_frame"] / out["gpu+cpu_ms_per_frame"]
+    out["speedup_gpu_over_cpu"] = out["cpu_ms_per_frame"] / out["gpu_ms_per_frame"]
+emit(out)
