@@ -19,6 +19,41 @@ GPU_PLATFORM = "AMD ROCm HIP"
 CPU_PLATFORM = "Host CPU"
 
 
+def usable_cpus() -> int:
+    """CPUs this process may actually use: the smallest of its affinity
+    mask, the cgroup CPU quota (v2 ``cpu.max``, v1 ``cfs_quota_us``) and
+    ``OMP_NUM_THREADS`` when set.  ``os.cpu_count()`` reports the whole
+    machine, and a pool sized to it on a container with a CPU share
+    oversubscribes the share many times over."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0 and per > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota:
+        n = min(n, max(1, int(quota + 0.999)))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 class ClDevice:
     """One selectable device plus its selection flags."""
 
@@ -65,7 +100,7 @@ class ClDevice:
         """DeviceInfo handed to the native runtime (CPU pool sized here)."""
         if not self.is_cpu:
             return self.info
-        hw = os.cpu_count() or 1
+        hw = usable_cpus()
         threads = hw - 1 if (self.partition and hw > 1) else hw
         if self.max_cpu_cores > 0:
             threads = min(threads, self.max_cpu_cores)

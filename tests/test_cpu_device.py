@@ -276,3 +276,19 @@ def test_license_text_names_gpl():
     text = cekirdekler_amd.license_text()
     assert "GNU General Public License" in text
     assert "Cekirdekler" in text
+
+
+def test_usable_cpus_respects_share(monkeypatch):
+    """The CPU device's pool is sized to the CPUs the process may use
+    (affinity, cgroup quota, OMP_NUM_THREADS), not the machine's count."""
+    import os
+
+    from cekirdekler_amd.hardware import usable_cpus
+
+    n = usable_cpus()
+    assert 1 <= n <= (os.cpu_count() or 1)
+    monkeypatch.setenv("OMP_NUM_THREADS", "2")
+    assert usable_cpus() <= 2
+    dev = ck.ClPlatforms.all().cpus(True).device(0)
+    monkeypatch.delenv("CEK_CPU_THREADS", raising=False)
+    assert dev.native_info().cpu_threads <= 2
