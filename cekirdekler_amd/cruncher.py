@@ -422,6 +422,17 @@ class ClNumberCruncher:
                 "h2d_bytes": r.h2d_bytes, "d2h_bytes": r.d2h_bytes, "p2p_bytes": r.p2p_bytes,
                 "pipelined": r.pipelined}
 
+    # ------------------------------------------------------------ compute graphs
+    def capture(self) -> "ComputeGraph":
+        """Record the computes issued inside ``with cr.capture() as g:`` into
+        one hipGraph per GPU instead of running them; ``g.replay(n)``
+        launches the whole sequence n times back to back (one
+        ``hipGraphLaunch`` per GPU per replay).  The split of every compute
+        id is frozen at its current value, host transfers happen at replay
+        time (pinned / registered host arrays), and the computes must have
+        run once before (buffers exist).  GPU devices only."""
+        return ComputeGraph(self)
+
     # ------------------------------------------------------------ xGMI read fan-out
     @property
     def peer_reads(self) -> bool:
@@ -634,3 +645,32 @@ class Cores:
 
     def dispose(self) -> None:
         self.cruncher.dispose()
+
+
+class ComputeGraph:
+    """A captured sequence of computes (see :meth:`ClNumberCruncher.capture`)."""
+
+    def __init__(self, cruncher: "ClNumberCruncher"):
+        self.cruncher = cruncher
+        self.id: Optional[int] = None
+
+    def __enter__(self) -> "ComputeGraph":
+        self.cruncher.cores.capture_begin()
+        return self
+
+    def __exit__(self, exc_type, exc, tb) -> None:
+        gid = self.cruncher.cores.capture_end()
+        if exc_type is None:
+            self.id = gid
+        else:
+            self.cruncher.cores.graph_destroy(gid)
+
+    def replay(self, times: int = 1, sync: bool = True) -> None:
+        if self.id is None:
+            raise RuntimeError("graph was not captured")
+        self.cruncher.cores.graph_launch(self.id, int(times), bool(sync))
+
+    def destroy(self) -> None:
+        if self.id is not None:
+            self.cruncher.cores.graph_destroy(self.id)
+            self.id = None

@@ -324,6 +324,12 @@ PYBIND11_MODULE(_cek, m) {
       .def("last_marker", &Cores::last_marker)
       .def("marker_word", &Cores::marker_word)
       .def("finish", &Cores::finish, py::call_guard<py::gil_scoped_release>())
+      .def("capture_begin", &Cores::capture_begin, py::call_guard<py::gil_scoped_release>())
+      .def("capture_end", &Cores::capture_end, py::call_guard<py::gil_scoped_release>())
+      .def("graph_launch", &Cores::graph_launch, py::arg("id"), py::arg("times") = 1, py::arg("sync") = true,
+           py::call_guard<py::gil_scoped_release>())
+      .def("graph_destroy", &Cores::graph_destroy, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("capturing", &Cores::capturing)
       .def("release_array", &Cores::release_array)
       .def("device_bytes", &Cores::device_bytes)
       .def("device_pointer", &Cores::device_pointer)

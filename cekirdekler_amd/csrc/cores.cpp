@@ -55,6 +55,22 @@ Cores::~Cores() {
     finish();
   } catch (...) {
   }
+  if (capturing_) {
+    for (auto& w : workers_) {
+      w->set_device();
+      hipGraph_t g = nullptr;
+      if (hipStreamEndCapture(w->main_stream(), &g) == hipSuccess && g) (void)hipGraphDestroy(g);
+      (void)hipGetLastError();
+    }
+    capturing_ = false;
+  }
+  for (auto& kv : graphs_)
+    for (size_t i = 0; i < kv.second.size() && i < workers_.size(); ++i)
+      if (kv.second[i]) {
+        workers_[i]->set_device();
+        (void)hipGraphExecDestroy(kv.second[i]);
+      }
+  graphs_.clear();
   for (size_t w = 0; w < spans_.size() && w < workers_.size(); ++w) {
     workers_[w]->set_device();
     for (auto& p : spans_[w].pool) {
@@ -173,6 +189,7 @@ void Cores::set_distributed(std::shared_ptr<Exchanger> ex, std::shared_ptr<Comm>
 
 void Cores::set_enqueue_mode(bool on) {
   std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
+  if (capturing_) throw Error("enqueue mode cannot change during a graph capture");
   if (on && !enqueue_mode_) {
     enqueue_t0_ = now_ms();
   } else if (!on && enqueue_mode_) {
@@ -257,8 +274,109 @@ long long Cores::markers_issued() {
   return r;
 }
 
+void Cores::capture_begin() {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
+  if (capturing_) throw Error("capture_begin: already capturing");
+  for (auto& w : workers_)
+    if (!w->gpu()) throw Error("compute graphs need GPU devices only (the CPU device runs computes at once)");
+  if (debug_checks_) throw Error("compute graphs cannot be captured with debug checks on (they synchronise)");
+  for (auto& w : workers_) {
+    w->wait();
+    w->sync_all();
+  }
+  cap_saved_ = {device_spans, peer_reads, async_enqueue, fine_grained, enqueue_mode_, record_timeline,
+                graph_min_launches};
+  device_spans = false;
+  record_timeline = false;
+  peer_reads = false;
+  async_enqueue = false;
+  fine_grained = false;
+  graph_min_launches = 0;
+  enqueue_mode_ = true;  // split frozen, no syncs (state is restored by capture_end)
+  for (auto& w : workers_) {
+    w->set_device();
+    CEK_HIP(hipStreamBeginCapture(w->main_stream(), hipStreamCaptureModeRelaxed));
+  }
+  capturing_ = true;
+}
+
+int Cores::capture_end() {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
+  if (!capturing_) throw Error("capture_end: not capturing");
+  for (auto& w : workers_) w->wait();
+  std::vector<hipGraphExec_t> execs(workers_.size(), nullptr);
+  std::string err;
+  for (size_t i = 0; i < workers_.size(); ++i) {
+    Worker& w = *workers_[i];
+    w.set_device();
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(w.main_stream(), &g);
+    if (e != hipSuccess || !g) {
+      (void)hipGetLastError();
+      err = std::string("stream capture failed on ") + w.dev().name + ": " + hipGetErrorString(e);
+      continue;
+    }
+    e = hipGraphInstantiate(&execs[i], g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      err = std::string("graph instantiation failed on ") + w.dev().name + ": " + hipGetErrorString(e);
+    }
+  }
+  capturing_ = false;
+  device_spans = cap_saved_.device_spans;
+  peer_reads = cap_saved_.peer_reads;
+  async_enqueue = cap_saved_.async_enqueue;
+  fine_grained = cap_saved_.fine_grained;
+  graph_min_launches = cap_saved_.graph_min_launches;
+  enqueue_mode_ = cap_saved_.enqueue_mode;
+  record_timeline = cap_saved_.record_timeline;
+  for (auto& sp : spans_) sp.used = 0;
+  if (!err.empty()) {
+    for (size_t i = 0; i < execs.size(); ++i)
+      if (execs[i]) {
+        workers_[i]->set_device();
+        (void)hipGraphExecDestroy(execs[i]);
+      }
+    throw Error(err);
+  }
+  const int id = next_graph_id_++;
+  graphs_[id] = std::move(execs);
+  return id;
+}
+
+void Cores::graph_launch(int id, int times, bool sync) {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
+  auto it = graphs_.find(id);
+  if (it == graphs_.end()) throw Error("graph_launch: unknown graph id");
+  for (size_t i = 0; i < workers_.size(); ++i) {
+    if (!it->second[i]) continue;
+    Worker& w = *workers_[i];
+    w.set_device();
+    for (int r = 0; r < times; ++r) CEK_HIP(hipGraphLaunch(it->second[i], w.main_stream()));
+  }
+  if (sync)
+    for (size_t i = 0; i < workers_.size(); ++i) {
+      workers_[i]->set_device();
+      CEK_HIP(hipStreamSynchronize(workers_[i]->main_stream()));
+    }
+}
+
+void Cores::graph_destroy(int id) {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
+  auto it = graphs_.find(id);
+  if (it == graphs_.end()) return;
+  for (size_t i = 0; i < it->second.size(); ++i)
+    if (it->second[i]) {
+      workers_[i]->set_device();
+      (void)hipGraphExecDestroy(it->second[i]);
+    }
+  graphs_.erase(it);
+}
+
 void Cores::finish() {
   std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
+  if (capturing_) throw Error("finish() during a graph capture (end the capture first)");
   for (auto& w : workers_) {
     w->wait();
     w->sync_all();

@@ -243,6 +243,23 @@ class Cores {
   void copy_between(int src_dev, const ArraySpec& src, int dst_dev, const ArraySpec& dst,
                     uint64_t bytes);  // device→device (peer/xGMI) copy, sync
 
+  // ---- compute graphs (hipGraph capture of a sequence of computes) ----
+  // capture_begin() puts every GPU's main stream into (relaxed) stream
+  // capture; the computes that follow are recorded, not run: enqueue-mode
+  // semantics (split frozen, no host syncs), main stream only, no markers,
+  // device spans, peer-read staging or nested repeat graphs.  capture_end()
+  // instantiates one graph per GPU and returns its id; graph_launch(id, n)
+  // replays it n times back to back on each GPU's main stream — one
+  // hipGraphLaunch per GPU per replay instead of one host call per kernel
+  // and copy.  Host transfers inside the graph read / write the host
+  // arrays at replay time (pinned or registered memory only).  Buffers must
+  // exist before capture: run the computes once first.
+  void capture_begin();
+  int capture_end();
+  void graph_launch(int id, int times, bool sync);
+  void graph_destroy(int id);
+  bool capturing() const { return capturing_; }
+
   // ---- distributed ----
   void set_distributed(std::shared_ptr<Exchanger> ex, std::shared_ptr<Comm> comm,
                        int global_devices, int global_base);
@@ -326,6 +343,13 @@ class Cores {
   int error_code_ = 0;
   double build_ms_ = 0;
   bool enqueue_mode_ = false;
+  bool capturing_ = false;
+  struct CaptureSaved {
+    bool device_spans, peer_reads, async_enqueue, fine_grained, enqueue_mode, record_timeline;
+    int graph_min_launches;
+  } cap_saved_{};
+  std::map<int, std::vector<hipGraphExec_t>> graphs_;  // id -> one exec per local worker (null: CPU)
+  int next_graph_id_ = 1;
   double enqueue_t0_ = 0;
   int last_id_ = 0;
   // ---- device-time spans for the balancer ----
