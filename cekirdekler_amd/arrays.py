@@ -69,7 +69,9 @@ def _resolve_dtype(dtype) -> tuple[np.dtype, bool]:
 
 _uid_counter = itertools.count(1)
 _live_cores: "weakref.WeakSet" = weakref.WeakSet()
-_live_lock = threading.Lock()
+# re-entrant: a garbage collection inside the locked region can run a
+# ClArray.__del__ that releases its uid on the same thread
+_live_lock = threading.RLock()
 
 
 def _register_cores(c) -> None:

@@ -166,6 +166,76 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
+  } else if constexpr (PIPE >= 6 && PIPE <= 8) {
+    // PIPE 5 with the K-tile's barrier moved in front of its last MFMA
+    // group(s) (BARG): every fragment of this K-tile is in registers by then,
+    // so the next K-tile's block-0 fragment reads fly under those MFMAs
+    // instead of stalling both waves of the SIMD after the barrier.  The
+    // LDS-DMA pieces are spread over groups 0..DMAG-1 (piece p in group
+    // p·DMAG/NGLDS), leaving BARG-DMAG groups for them to land.
+    // PIPE 6: BARG 7, DMAG 4; PIPE 7: BARG 6, DMAG 4; PIPE 8: BARG 7, DMAG 7
+    constexpr int NGLDS = A_INSTR + B_INSTR;
+    constexpr int BARG = PIPE == 7 ? 6 : 7;
+    constexpr int DMAG = PIPE == 8 ? 7 : 4;
+    constexpr int NRD = FM + FN, PER_RD = (NRD + 3) / 4;
+    auto stage_one = [&](int buf, int kt, int g) {
+      char* base = smem + buf * STAGE;
+      if (g < A_INSTR) {
+        const char* src = a_wave + ((size_t)g * 8 * K + (size_t)kt * BK) * 4;
+        __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
+                                         (lds_void*)(base + (wave * A_INSTR + g) * 1024), 16, 0, 0);
+      } else {
+        const int j = g - A_INSTR;
+        const char* src = b_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 4;
+        __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
+                                         (lds_void*)(base + A_BYTES + (wave * B_INSTR + j) * 1024), 16, 0, 0);
+      }
+    };
+    f32x4 fa[2][FM], fb[2][FN];
+    ld(fa[0], fb[0], smem, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      const char* base = smem + cur * STAGE;
+      const bool pre = kt + 1 < nk;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int sq = 0; sq < 8; ++sq) {
+        const int sb = sq / 4, q = sq % 4;
+        if (sq < 4) {
+#pragma unroll
+          for (int r = 0; r < PER_RD; ++r) {
+            const int x = sq * PER_RD + r;
+            if (x < FN)
+              fb[1][x] = *(const f32x4*)(base + b_off[1] + x * 2048);
+            else if (x < NRD)
+              fa[1][x - FN] = *(const f32x4*)(base + a_off[1] + (x - FN) * 2048);
+          }
+        }
+        if (pre) {
+#pragma unroll
+          for (int p = 0; p < NGLDS; ++p)
+            if (p * DMAG / NGLDS == sq) stage_one(cur ^ 1, kt + 1, p);
+        }
+        if (sq == BARG) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          if (pre) ld(fa[0], fb[0], smem + (cur ^ 1) * STAGE, 0);
+        }
+        // row-block by row-block (all four k of FM/4 rows per group), so a
+        // block's A fragments die group by group and free the registers the
+        // other block's fragment reads load into
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+          for (int ii = 0; ii < FM / 4; ++ii)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+              const int i = q * (FM / 4) + ii;
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[sb][i][qq], fb[sb][j][qq], acc[i][j], 0, 0, 0);
+            }
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
   } else if constexpr (PIPE == 2) {
     // both 16-deep k blocks' fragments are read up front: the second block's
     // ds_reads fly under the first block's MFMAs (2 fragment sets live, no
@@ -535,6 +605,11 @@ CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q3, 2, 2, 8, 8, 3)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256i, 2, 4, 8, 4, 3)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ie, 2, 4, 8, 4, 4)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ir, 2, 4, 8, 4, 5)
+// "ir" with the barrier ahead of the last MFMA group(s): next K-tile's block-0
+// fragment reads under this K-tile's tail MFMAs (PIPE 6 / 7 / 8)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ib, 2, 4, 8, 4, 6)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ib6, 2, 4, 8, 4, 7)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ib7, 2, 4, 8, 4, 8)
 // same with nontemporal C stores
 extern "C" __global__ __launch_bounds__(512) void cek_sgemm_f32_256x256irn(
     const int* dims, const float* A, const float* Bt, float* C, CEK_HIDDEN) {

@@ -95,6 +95,11 @@ F32_TILES = {
     # "i" with block 1's fragment reads between block 0's MFMA groups
     "256x256ir": (256, 256, 512, "cek_sgemm_f32_256x256ir"),
     "256x256irn": (256, 256, 512, "cek_sgemm_f32_256x256irn"),  # + nontemporal C stores
+    # "ir" with the barrier ahead of the last MFMA group (ib6: last two), so the
+    # next K-tile's first fragment reads overlap MFMAs; ib7 spreads the DMA wider
+    "256x256ib": (256, 256, 512, "cek_sgemm_f32_256x256ib"),
+    "256x256ib6": (256, 256, 512, "cek_sgemm_f32_256x256ib6"),
+    "256x256ib7": (256, 256, 512, "cek_sgemm_f32_256x256ib7"),
 }
 
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)

@@ -292,3 +292,24 @@ def test_usable_cpus_respects_share(monkeypatch):
     dev = ck.ClPlatforms.all().cpus(True).device(0)
     monkeypatch.delenv("CEK_CPU_THREADS", raising=False)
     assert dev.native_info().cpu_threads <= 2
+
+
+def test_array_release_inside_locked_region_does_not_deadlock():
+    """A garbage collection inside ``_release_uid``'s locked region runs
+    ``ClArray.__del__`` on the same thread, which releases its own uid: the
+    registry lock must be re-entrant (this hung a GPU test run)."""
+    import threading
+
+    from cekirdekler_amd import arrays
+
+    done = threading.Event()
+
+    def nested():
+        with arrays._live_lock:
+            arrays._release_uid(-1)
+        done.set()
+
+    t = threading.Thread(target=nested, daemon=True)
+    t.start()
+    t.join(10)
+    assert done.is_set()
