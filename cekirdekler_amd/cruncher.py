@@ -138,6 +138,7 @@ class ClNumberCruncher:
                 "(GPU-resident child levels, see ClNumberCruncher.device_enqueue_errors)")
         cfg = cek.CoresConfig()
         cfg.queue_concurrency = int(queue_concurrency)
+        self._queue_concurrency = max(1, min(16, int(queue_concurrency)))
         cfg.no_pipelining = bool(no_pipelining)
         cfg.smooth = bool(smooth)
         cfg.options = list(options or [])
@@ -187,6 +188,21 @@ class ClNumberCruncher:
     @property
     def number_of_devices(self) -> int:
         return self._cores.num_global_devices if self._cores else 0
+
+    @property
+    def compute_queue_concurrency(self) -> int:
+        """Streams per device that async enqueue rotates over
+        (``computeQueueConcurrency``, ClNumberCruncher.cs:313, ≤ 16)."""
+        return self._queue_concurrency
+
+    @property
+    def last_used_compute_id(self) -> int:
+        """Compute id of the latest compute() (Cores.cs:961); -1 before any."""
+        return int(self._cores.last_compute_id) if self._cores else -1
+
+    computeQueueConcurrency = compute_queue_concurrency
+    lastUsedComputeId = last_used_compute_id
+    numberOfDevices = number_of_devices
 
     # ------------------------------------------------------------ modes
     def _prop(name):  # noqa: N805

@@ -313,3 +313,13 @@ def test_array_release_inside_locked_region_does_not_deadlock():
     t.start()
     t.join(10)
     assert done.is_set()
+
+
+def test_queue_concurrency_and_last_used_compute_id(cpu):
+    cr = ck.ClNumberCruncher(cpu, "__global__ void k(float* x) { x[get_global_id(0)] += 1.0f; }",
+                             queue_concurrency=40)
+    assert cr.computeQueueConcurrency == 16  # clamped like the reference's ≤ 16
+    x = ck.ClArray(np.zeros(256, np.float32))
+    x.compute(cr, 7, "k", 256, 64)
+    assert cr.lastUsedComputeId == 7 and cr.numberOfDevices == cr.number_of_devices
+    cr.dispose()
