@@ -293,17 +293,45 @@ void Cores::capture_begin() {
   fine_grained = false;
   graph_min_launches = 0;
   enqueue_mode_ = true;  // split frozen, no syncs (state is restored by capture_end)
-  for (auto& w : workers_) {
-    w->set_device();
-    CEK_HIP(hipStreamBeginCapture(w->main_stream(), hipStreamCaptureModeRelaxed));
+  cap_logs_.assign(workers_.size(), {});
+  for (size_t i = 0; i < workers_.size(); ++i) {
+    Worker& w = *workers_[i];
+    w.set_device();
+    hipError_t e = hipStreamBeginCapture(w.main_stream(), hipStreamCaptureModeRelaxed);
+    if (e != hipSuccess) {
+      // undo: end the captures already begun and restore the modes
+      (void)hipGetLastError();
+      for (size_t j = 0; j < i; ++j) {
+        workers_[j]->set_device();
+        hipGraph_t g = nullptr;
+        if (hipStreamEndCapture(workers_[j]->main_stream(), &g) == hipSuccess && g) (void)hipGraphDestroy(g);
+        workers_[j]->set_capture_log(nullptr);
+      }
+      restore_capture_state();
+      throw Error(std::string("hipStreamBeginCapture failed on ") + w.dev().name + ": " + hipGetErrorString(e));
+    }
+    w.set_capture_log(&cap_logs_[i]);
   }
   capturing_ = true;
+}
+
+void Cores::restore_capture_state() {
+  device_spans = cap_saved_.device_spans;
+  peer_reads = cap_saved_.peer_reads;
+  async_enqueue = cap_saved_.async_enqueue;
+  fine_grained = cap_saved_.fine_grained;
+  graph_min_launches = cap_saved_.graph_min_launches;
+  enqueue_mode_ = cap_saved_.enqueue_mode;
+  record_timeline = cap_saved_.record_timeline;
 }
 
 int Cores::capture_end() {
   std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   if (!capturing_) throw Error("capture_end: not capturing");
-  for (auto& w : workers_) w->wait();
+  for (auto& w : workers_) {
+    w->wait();
+    w->set_capture_log(nullptr);
+  }
   std::vector<hipGraphExec_t> execs(workers_.size(), nullptr);
   std::string err;
   for (size_t i = 0; i < workers_.size(); ++i) {
@@ -324,13 +352,7 @@ int Cores::capture_end() {
     }
   }
   capturing_ = false;
-  device_spans = cap_saved_.device_spans;
-  peer_reads = cap_saved_.peer_reads;
-  async_enqueue = cap_saved_.async_enqueue;
-  fine_grained = cap_saved_.fine_grained;
-  graph_min_launches = cap_saved_.graph_min_launches;
-  enqueue_mode_ = cap_saved_.enqueue_mode;
-  record_timeline = cap_saved_.record_timeline;
+  restore_capture_state();
   for (auto& sp : spans_) sp.used = 0;
   if (!err.empty()) {
     for (size_t i = 0; i < execs.size(); ++i)
@@ -342,6 +364,8 @@ int Cores::capture_end() {
   }
   const int id = next_graph_id_++;
   graphs_[id] = std::move(execs);
+  graph_bufs_[id] = std::move(cap_logs_);
+  cap_logs_.clear();
   return id;
 }
 
@@ -349,6 +373,13 @@ void Cores::graph_launch(int id, int times, bool sync) {
   std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   auto it = graphs_.find(id);
   if (it == graphs_.end()) throw Error("graph_launch: unknown graph id");
+  const auto& bufs = graph_bufs_[id];
+  for (size_t i = 0; i < bufs.size() && i < workers_.size(); ++i)
+    for (const auto& ub : bufs[i])
+      if (!workers_[i]->buffer_is(ub.first, ub.second))
+        throw Error("graph " + std::to_string(id) + " is stale: array " + std::to_string(ub.first) +
+                    " was released or reallocated on " + workers_[i]->dev().name +
+                    " since the capture (capture it again)");
   for (size_t i = 0; i < workers_.size(); ++i) {
     if (!it->second[i]) continue;
     Worker& w = *workers_[i];
@@ -372,6 +403,7 @@ void Cores::graph_destroy(int id) {
       (void)hipGraphExecDestroy(it->second[i]);
     }
   graphs_.erase(it);
+  graph_bufs_.erase(id);
 }
 
 void Cores::finish() {

@@ -344,11 +344,17 @@ class Cores {
   double build_ms_ = 0;
   bool enqueue_mode_ = false;
   bool capturing_ = false;
+  void restore_capture_state();  // the modes capture_begin saved
   struct CaptureSaved {
     bool device_spans, peer_reads, async_enqueue, fine_grained, enqueue_mode, record_timeline;
     int graph_min_launches;
   } cap_saved_{};
   std::map<int, std::vector<hipGraphExec_t>> graphs_;  // id -> one exec per local worker (null: CPU)
+  // buffers each worker handed out while capturing: (uid, pointer) — a graph
+  // replays those pointers, so graph_launch refuses to run once any of them
+  // was released or reallocated
+  std::vector<std::vector<std::pair<uint64_t, void*>>> cap_logs_;
+  std::map<int, std::vector<std::vector<std::pair<uint64_t, void*>>>> graph_bufs_;
   int next_graph_id_ = 1;
   double enqueue_t0_ = 0;
   int last_id_ = 0;

@@ -114,6 +114,26 @@ void Worker::set_device() const {
 }
 
 void* Worker::buffer(const ArraySpec& a) {
+  void* p = buffer_impl(a);
+  std::lock_guard<std::mutex> g(buf_mu_);
+  if (cap_log_) cap_log_->emplace_back(a.uid, p);
+  return p;
+}
+
+void Worker::set_capture_log(std::vector<std::pair<uint64_t, void*>>* log) {
+  std::lock_guard<std::mutex> g(buf_mu_);
+  cap_log_ = log;
+}
+
+bool Worker::buffer_is(uint64_t uid, const void* ptr) {
+  std::lock_guard<std::mutex> g(buf_mu_);
+  auto it = bufs_.find(uid);
+  if (it != bufs_.end()) return it->second.first == ptr;
+  auto z = zc_ptr_.find(uid);
+  return z != zc_ptr_.end() && z->second == ptr;
+}
+
+void* Worker::buffer_impl(const ArraySpec& a) {
   if (!gpu()) return a.host;
   if (a.zc) {
     // The array owns its registration (ClArray registers once, unregisters
@@ -123,7 +143,7 @@ void* Worker::buffer(const ArraySpec& a) {
       throw Error("zero-copy array is neither pinned nor registered with HIP");
     std::lock_guard<std::mutex> g(buf_mu_);
     zc_[a.uid] = true;
-    return host_device_ptr(a.host);
+    return zc_ptr_[a.uid] = host_device_ptr(a.host);
   }
   std::lock_guard<std::mutex> g(buf_mu_);
   auto it = bufs_.find(a.uid);
@@ -189,6 +209,7 @@ void Worker::release(uint64_t uid) {
   }
   guarded_.erase(uid);
   zc_.erase(uid);
+  zc_ptr_.erase(uid);
 }
 
 void Worker::release_all() {
@@ -200,6 +221,7 @@ void Worker::release_all() {
   bufs_.clear();
   guarded_.clear();
   zc_.clear();
+  zc_ptr_.clear();
   bytes_allocated_ = 0;
 }
 

@@ -84,6 +84,10 @@ class Worker {
 
   // --- buffers ---------------------------------------------------------
   void* buffer(const ArraySpec& a);  // device-visible pointer for a
+  // graph capture: while a log is set, every (uid, pointer) handed out is
+  // appended to it; buffer_is() tells whether uid still has that pointer
+  void set_capture_log(std::vector<std::pair<uint64_t, void*>>* log);
+  bool buffer_is(uint64_t uid, const void* ptr);
   void release(uint64_t uid);
   void release_all();
   uint64_t bytes_allocated() const { return bytes_allocated_; }
@@ -159,6 +163,9 @@ class Worker {
   std::unordered_map<uint64_t, std::pair<void*, uint64_t>> bufs_;
   std::unordered_map<uint64_t, bool> zc_;
   std::unordered_map<uint64_t, uint64_t> guarded_;  // uid -> guard offset (bytes)
+  std::unordered_map<uint64_t, void*> zc_ptr_;      // zero-copy uid -> device view of its host memory
+  std::vector<std::pair<uint64_t, void*>>* cap_log_ = nullptr;
+  void* buffer_impl(const ArraySpec& a);
   void check_guards(hipStream_t s, const std::string& kernel, const std::vector<ArraySpec>& arrs);
   uint64_t bytes_allocated_ = 0;
   std::mutex buf_mu_;

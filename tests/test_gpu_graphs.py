@@ -89,3 +89,21 @@ def test_capture_refuses_cpu_device():
         with cr.capture():
             pass
     cr.dispose()
+
+
+def test_replay_refuses_a_graph_whose_buffers_were_released():
+    """A graph replays the device pointers it captured: once an array it
+    uses is disposed, replay must raise instead of touching freed memory."""
+    cr = ck.ClNumberCruncher(ck.ClPlatforms.all().gpus()[0], SRC)
+    n = 1 << 16
+    x = ck.ClArray(np.zeros(n, np.float32))
+    x.compute(cr, 3, "inc", n, 256)
+    x.read = x.write = False
+    with cr.capture() as g:
+        x.compute(cr, 3, "inc", n, 256)
+    g.replay(2)
+    x.dispose()
+    with pytest.raises(Exception, match="stale"):
+        g.replay(1)
+    g.destroy()
+    cr.dispose()
