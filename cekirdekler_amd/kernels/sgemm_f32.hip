@@ -602,6 +602,8 @@ CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q, 2, 2, 8, 8, 1)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q0, 2, 2, 8, 8, 0)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q2, 2, 2, 8, 8, 2)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q3, 2, 2, 8, 8, 3)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256qr, 2, 2, 8, 8, 5)
+CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256qb7, 2, 2, 8, 8, 8)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256i, 2, 4, 8, 4, 3)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ie, 2, 4, 8, 4, 4)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ir, 2, 4, 8, 4, 5)

@@ -100,6 +100,9 @@ F32_TILES = {
     "256x256ib": (256, 256, 512, "cek_sgemm_f32_256x256ib"),
     "256x256ib6": (256, 256, 512, "cek_sgemm_f32_256x256ib6"),
     "256x256ib7": (256, 256, 512, "cek_sgemm_f32_256x256ib7"),
+    # the 4-wave 128×128-per-wave layout (one wave per SIMD) with the ir / ib7 schedules
+    "256x256qr": (256, 256, 256, "cek_sgemm_f32_256x256qr"),
+    "256x256qb7": (256, 256, 256, "cek_sgemm_f32_256x256qb7"),
 }
 
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)

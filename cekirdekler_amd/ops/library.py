@@ -34,7 +34,8 @@ LIBRARY = {
                   "cek_sgemm_f32_256x256q3", "cek_sgemm_f32_256x256i",
                   "cek_sgemm_f32_256x256ie", "cek_sgemm_f32_256x128ie",
                   "cek_sgemm_f32_256x256ir", "cek_sgemm_f32_256x256irn",
-                  "cek_sgemm_f32_256x256ib", "cek_sgemm_f32_256x256ib6", "cek_sgemm_f32_256x256ib7"],
+                  "cek_sgemm_f32_256x256ib", "cek_sgemm_f32_256x256ib6", "cek_sgemm_f32_256x256ib7",
+                  "cek_sgemm_f32_256x256qr", "cek_sgemm_f32_256x256qb7"],
     "mandelbrot": ["cek_mandelbrot_f32", "cek_mandelbrot_pool16_f32", "cek_mandelbrot_pool8_f32",
                    "cek_mandelbrot_pk16_f32", "cek_mandelbrot_pk32_f32", "cek_mandelbrot_blk16_f32",
                    "cek_mandelbrot_blk64_f32", "cek_mandelbrot_blk8_f32"],

@@ -228,7 +228,8 @@ def test_nbody_steps_two_logical_devices(resident):
 
 @pytest.mark.parametrize("tile", ["128x128", "256x128", "256x256", "128x128p", "256x128p", "256x256w", "256x128w", "128x128w",
                                   "256x256h", "256x128h", "256x256pb", "256x128pb", "256x256i", "256x256ir",
-                                  "256x256ib", "256x256ib6", "256x256ib7"])
+                                  "256x256ib", "256x256ib6", "256x256ib7",
+                                  "256x256qr", "256x256qb7"])
 @pytest.mark.parametrize("shape", [(512, 512, 256), (768, 512, 96), (512, 256, 32)])
 def test_gemm_f32_matches_fp64(tile, shape):
     """fp32 matrix-core GEMM (v_mfma_f32_16x16x4_f32) against a float64 host
