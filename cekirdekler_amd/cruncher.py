@@ -449,6 +449,21 @@ class ClNumberCruncher:
         run once before (buffers exist).  GPU devices only."""
         return ComputeGraph(self)
 
+    # ------------------------------------------------------------ kernel downloads
+    @property
+    def kernel_d2h(self) -> bool:
+        """Download slices of pinned / registered host arrays (≥ 1 MiB,
+        16-byte aligned) with a copy kernel that writes straight into the host
+        pages, instead of ``hipMemcpyAsync``.  Keeps downloads off the SDMA
+        engines the uploads use, so a download waiting for its kernel never
+        holds up an upload queued behind it (streamed host-resident calls;
+        ``profiles/hostres_streaming.md``).  Env ``CEK_KERNEL_D2H=1``."""
+        return bool(self._cores.kernel_d2h) if self._cores else False
+
+    @kernel_d2h.setter
+    def kernel_d2h(self, on: bool) -> None:
+        self._cores.kernel_d2h = bool(on)
+
     # ------------------------------------------------------------ xGMI read fan-out
     @property
     def peer_reads(self) -> bool:

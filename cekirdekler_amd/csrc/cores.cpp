@@ -44,6 +44,7 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
   global_devices_ = static_cast<int>(workers_.size());
   spans_.resize(workers_.size());
   if (const char* e = std::getenv("CEK_DEVICE_SPANS")) device_spans = std::string(e) != "0";
+  if (const char* e = std::getenv("CEK_KERNEL_D2H")) set_kernel_d2h(std::string(e) != "0");
   time_scale_.assign(workers_.size(), 1.0);
   enabled_.assign(workers_.size(), true);
   inject_.assign(workers_.size(), 0);

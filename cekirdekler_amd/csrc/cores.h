@@ -199,6 +199,17 @@ class Cores {
   // debug checks: guard tails on new buffers, synchronous checked launches
   void set_debug_checks(bool on);
   bool debug_checks() const { return debug_checks_; }
+  // downloads of pinned / registered host memory by a copy kernel instead
+  // of hipMemcpyAsync (Worker::kernel_d2h; env CEK_KERNEL_D2H)
+  void set_kernel_d2h(bool on) {
+    for (auto& w : workers_) w->kernel_d2h = on;
+  }
+  bool kernel_d2h() const { return !workers_.empty() && workers_[0]->kernel_d2h.load(); }
+  uint64_t kernel_d2h_bytes() const {
+    uint64_t b = 0;
+    for (auto& w : workers_) b += w->kernel_d2h_bytes();
+    return b;
+  }
   int device_enqueue_errors();
   // ---- device timeline ----
   // With record_timeline on, the kernels of every compute are bracketed by

@@ -1,5 +1,7 @@
 #include "worker.h"
 
+#include <algorithm>
+
 #include "memory.h"
 
 namespace cek {
@@ -342,7 +344,47 @@ void Worker::d2h(hipStream_t s, const ArraySpec& a, uint64_t elem_begin, uint64_
   if (off >= a.bytes) return;
   if (off + n > a.bytes) n = a.bytes - off;
   char* d = static_cast<char*>(buffer(a));
+  if (kernel_d2h.load(std::memory_order_relaxed) && d2h_by_kernel(s, a.host, off, d + off, n)) return;
   CEK_HIP(hipMemcpyAsync(static_cast<char*>(a.host) + off, d + off, n, hipMemcpyDeviceToHost, s));
+}
+
+// 16 bytes per lane per iteration; a grid of at most 64 work-groups: PCIe
+// (≈ 55 GB/s) is the limit, so the copy leaves the rest of the chip to the
+// kernels it overlaps
+static const char* kCopySrc = R"CEK(
+typedef unsigned int cek_u32x4 __attribute__((ext_vector_type(4)));
+__global__ void cek_copy16_to_host(const cek_u32x4* src, cek_u32x4* dst, long long n16) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (; i < n16; i += stride) dst[i] = src[i];
+}
+)CEK";
+
+bool Worker::d2h_by_kernel(hipStream_t s, void* host_base, uint64_t off, const void* src_dev, uint64_t n) {
+  char* dst_host = static_cast<char*>(host_base) + off;
+  if (n < kKernelD2HMinBytes || (reinterpret_cast<uintptr_t>(dst_host) | reinterpret_cast<uintptr_t>(src_dev) | n) & 15)
+    return false;
+  if (!host_is_pinned(host_base)) return false;  // pinned / registered: looked up by the array's base
+  set_device();
+  char* base_dev = static_cast<char*>(host_device_ptr(host_base));
+  if (!base_dev) return false;
+  void* dst = base_dev + off;
+  {
+    std::lock_guard<std::mutex> g(copy_mu_);
+    if (!copy_fn_) {
+      copy_prog_ = Program::build(dev_, kCopySrc, {}, {});
+      if (!copy_prog_->ok()) throw Error("kernel-D2H copy kernel failed to build: " + copy_prog_->log());
+      copy_fn_ = copy_prog_->gpu_fn("cek_copy16_to_host");
+    }
+  }
+  long long n16 = static_cast<long long>(n / 16), hidden_off = 0, gs = n16;
+  const void* src = src_dev;
+  void* params[] = {&src, &dst, &n16, &hidden_off, &gs};
+  const long long per_group = 256ll * 16;  // 16 iterations of 256 lanes per work-group at least
+  const unsigned groups = static_cast<unsigned>(std::max(1ll, std::min(64ll, (n16 + per_group - 1) / per_group)));
+  CEK_HIP(hipModuleLaunchKernel(copy_fn_, groups, 1, 1, 256, 1, 1, 0, s, params, nullptr));
+  kernel_d2h_bytes_ += n;
+  return true;
 }
 
 void Worker::launch(hipStream_t s, const std::string& kernel, const std::vector<ArraySpec>& arrs,

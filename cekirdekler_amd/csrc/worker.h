@@ -119,6 +119,14 @@ class Worker {
   static constexpr unsigned char kGuardByte = 0xCE;
   // atomic: Cores::set_debug_checks flips it while job threads read it
   std::atomic<bool> debug_checks{false};
+  // D2H of pinned / registered host memory by a copy kernel on the stream
+  // (device writes straight into the host pages) instead of
+  // hipMemcpyAsync, for copies of at least kKernelD2HMinBytes with 16-byte
+  // aligned ends: keeps downloads off the SDMA rings the uploads use, so a
+  // download gated on a kernel never blocks an upload queued behind it
+  std::atomic<bool> kernel_d2h{false};
+  static constexpr uint64_t kKernelD2HMinBytes = 1ull << 20;
+  uint64_t kernel_d2h_bytes() const { return kernel_d2h_bytes_; }
   int device_enqueue_errors();
 
   // --- markers (fine-grained queue control, ClCommandQueue.cs:103-112) ---
@@ -165,6 +173,11 @@ class Worker {
   std::unordered_map<uint64_t, uint64_t> guarded_;  // uid -> guard offset (bytes)
   std::unordered_map<uint64_t, void*> zc_ptr_;      // zero-copy uid -> device view of its host memory
   std::vector<std::pair<uint64_t, void*>>* cap_log_ = nullptr;
+  std::shared_ptr<Program> copy_prog_;  // the kernel-D2H copy kernel, built on first use
+  hipFunction_t copy_fn_ = nullptr;
+  std::mutex copy_mu_;
+  std::atomic<uint64_t> kernel_d2h_bytes_{0};
+  bool d2h_by_kernel(hipStream_t s, void* host_base, uint64_t off, const void* src_dev, uint64_t n);
   void* buffer_impl(const ArraySpec& a);
   void check_guards(hipStream_t s, const std::string& kernel, const std::vector<ArraySpec>& arrs);
   uint64_t bytes_allocated_ = 0;

@@ -69,3 +69,24 @@ def test_pinned_wrapped_d2h_does_not_block_enqueue_mode():
     assert dt_pin < 0.25 * total_pin, (dt_pin, total_pin)
     assert dt_page > 0.5 * total_page, (dt_page, total_page)  # pageable: blocked
     cr.dispose()
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_kernel_d2h_downloads_match(pipeline):
+    """``kernel_d2h``: slices of registered (and hipHostMalloc) host arrays
+    come down through the runtime's copy kernel, on two logical devices,
+    serial and through the event pipeline; unaligned or small copies fall
+    back to hipMemcpyAsync."""
+    src = "__global__ void k(float* y) { long long i = get_global_id(0); y[i] = (float)(i % 9973) + 0.5f; }"
+    g0 = ck.ClPlatforms.all().gpus()[0]
+    cr = ck.ClNumberCruncher(g0 + g0, src)
+    cr.kernel_d2h = True
+    assert cr.kernel_d2h
+    n = 1 << 22  # 16 MiB
+    for y in (ck.ClArray(np.zeros(n, np.float32)), ck.ClArray(n, np.float32)):
+        y.read = False
+        y.compute(cr, 1, "k", n, 256, pipeline=pipeline, pipeline_blobs=4)
+        np.testing.assert_array_equal(y.array, (np.arange(n) % 9973).astype(np.float32) + 0.5)
+        y.dispose()
+    assert cr.cores.kernel_d2h_bytes >= 2 * n * 4
+    cr.dispose()
