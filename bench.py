@@ -158,12 +158,11 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     err = _max_over_ranks(ctx, g.verify(compute_id=1))
     timeouts = int(_sum_over_ranks(ctx, g.spin_timeouts()))
     host_steps = max(2, min(steps, 5))
-    # host-resident: serial upload / compute / download.  The streamed event
-    # pipeline (GemmBf16.run(stream_blobs=8)) reaches 7.9-8.2 ms when calls
-    # run back to back, but after a device-wide sync (the bench's bracket)
-    # its copies stall for ~6 ms per call on this image (14 ms,
-    # profiles/hostres_streaming.md), so the bench reports the serial path.
-    blobs = 0
+    # host-resident: A and B uploaded and C downloaded on every call, through
+    # the event-driven read/compute/write pipeline in 8 blobs (B a full
+    # read, A row panels and C tiles streamed; profiles/hostres_streaming.md).
+    # Falls back to the serial 3-phase path when the tile cannot stream.
+    blobs = HOST_RESIDENT_BLOBS if g.can_stream() else 0
     host_calls = []
 
     host_piped = []
@@ -175,6 +174,8 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
         host_piped.append(cr.last_record()["pipelined"])
 
     ms_host = timed(ctx, host_step, host_steps, 2)
+    # the streamed host-resident output: this rank's tiles of the host C
+    err_host = _max_over_ranks(ctx, g.verify(compute_id=2, host=True))
     cr.dispose()
     for a in (g.A, g.B, g.C, g.dims):
         a.dispose()  # release 0.5 GB of pinned host memory before the next config
@@ -183,7 +184,8 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
             "host_resident_ms": ms_host, "host_resident_gflops": g.flops / (ms_host * 1e-3) / 1e9,
             "host_resident_blobs": blobs, "host_resident_calls_ms": [round(x, 3) for x in host_calls],
             "host_resident_pipelined": host_piped,
-            "ranges": ranges, "max_rel_err": err, "spin_timeouts": timeouts, "device": "gpu"}
+            "ranges": ranges, "max_rel_err": max(err, err_host), "max_rel_err_host_resident": err_host,
+            "spin_timeouts": timeouts, "device": "gpu"}
 
 
 CPU_GEMM_SRC = """
@@ -337,6 +339,7 @@ def bench_node_configs(world: int) -> dict:
 
 
 MAX_REL_ERR = 5e-3
+HOST_RESIDENT_BLOBS = 8
 
 
 def _free_port() -> int:
@@ -427,6 +430,7 @@ def main(argv=None) -> int:
                 "sgemm_host_resident_stream_blobs": sg.get("host_resident_blobs", 0),
                 "sgemm_host_resident_calls_ms": sg.get("host_resident_calls_ms", []),
                 "sgemm_host_resident_pipelined": sg.get("host_resident_pipelined", []),
+                "sgemm_host_resident_max_rel_err": sg.get("max_rel_err_host_resident"),
                 "sgemm_max_rel_err": sg["max_rel_err"],
                 "sgemm_spin_timeouts": sg["spin_timeouts"],
                 "sgemm_balancer_setup_calls": sg["balancer_setup_calls"],

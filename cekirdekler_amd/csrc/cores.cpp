@@ -966,7 +966,9 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
   // Interleave the two half-pipelines' chunks so both read streams start early.
   for (long long k = 0; k < per_half; ++k) {
     for (int h = 0; h < halves; ++h) {
-      hipStream_t rs = wk.pipe_stream(h, 0), ks = wk.pipe_stream(h, 1);
+      // reads_on_main_stream: every blob's upload follows the full reads on
+      // the main stream (one in-order chain of copies)
+      hipStream_t rs = pipeline_reads_on_main_stream ? m : wk.pipe_stream(h, 0), ks = wk.pipe_stream(h, 1);
       // writes_on_compute_stream: a blob's D2H follows its kernel on the same
       // stream (in-stream order) instead of a write stream gated by an event
       hipStream_t ws = pipeline_writes_on_compute_stream ? ks : wk.pipe_stream(h, 2);

@@ -292,6 +292,13 @@ class Cores {
   bool peer_reads = true;
   // event pipeline: issue each blob's D2H on its compute stream
   bool pipeline_writes_on_compute_stream = false;
+  // event pipeline: issue every blob's uploads on the main stream, after the
+  // full reads (one in-order chain; the copies share the SDMA engine
+  // anyway).  With separate read streams, the first call after any
+  // device-wide sync left the uploads idle ~5 ms after the full reads and
+  // some processes stayed at 14 ms per streamed GEMM call instead of 8
+  // (profiles/hostres_streaming.md, tools/hostres_stall_probe.py)
+  bool pipeline_reads_on_main_stream = true;
   uint64_t peer_read_min_bytes = 1u << 20;
 
  private:

@@ -293,12 +293,15 @@ class GemmBf16:
             total += int(self.counters.array[-1])
         return total
 
-    def verify(self, compute_id: int = 1, tiles_per_device: int = 8, seed: int = 1) -> float:
+    def verify(self, compute_id: int = 1, tiles_per_device: int = 8, seed: int = 1,
+               host: bool = False) -> float:
         """Max relative error of the device-resident C of ``compute_id``
         against a float64 host product, over sampled output tiles of this
         process's devices' ranges: the first and last tile of each range plus
         random ones.  Relative to ``max |ref|`` of each tile.  Downloads each
-        local device's C replica (device memory is not changed)."""
+        local device's C replica (device memory is not changed).
+        ``host=True`` checks the host C instead (a host-resident call's
+        downloaded slices), without downloading."""
         ranges = self.cr.ranges(compute_id)
         refs = self.cr.references(compute_id)
         unit = self.L * self.split_k
@@ -315,7 +318,8 @@ class GemmBf16:
             t0, nt = refs[g] // unit, ranges[g] // unit
             if nt == 0:
                 continue
-            self.cr.download(self.C, dev)
+            if not host:
+                self.cr.download(self.C, dev)
             picks = {t0, t0 + nt - 1}
             picks.update((t0 + rng.choice(nt, size=min(nt, tiles_per_device), replace=False)).tolist())
             picks = np.array(sorted(picks))

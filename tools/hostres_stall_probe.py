@@ -31,6 +31,8 @@ dev = ck.ClPlatforms.all().gpus()[0]
 def make():
     cr = ck.ClNumberCruncher(dev, "", prebuilt=library(*GEMM_LIBS))
     cr.kernel_d2h = kd2h
+    cr.cores.pipeline_reads_on_main_stream = "rms" in sys.argv[3:]
+    cr.cores.pipeline_writes_on_compute_stream = "wcs" in sys.argv[3:]
     return GemmBf16(size, size, size, cruncher=cr, tile="256x256pb")
 
 
@@ -72,6 +74,7 @@ for t, r, c in zip(picks, tm, tn):
     err = max(err, float(np.abs(got - ref).max() / np.abs(ref).max()))
 out["max_rel_err"] = err
 out["kernel_d2h"] = kd2h
+out["opts"] = sys.argv[3:]
 out["kernel_d2h_MiB"] = g2.cr.cores.kernel_d2h_bytes / 2 ** 20
 print(json.dumps(out), flush=True)
 g.cr.dispose()
