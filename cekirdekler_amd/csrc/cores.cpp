@@ -973,7 +973,8 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
       // stream (in-stream order) instead of a write stream gated by an event
       hipStream_t ws = pipeline_writes_on_compute_stream ? ks : wk.pipe_stream(h, 2);
       long long off = ref + h * (range / halves) + k * chunk;
-      const int rsid = 17 + 3 * h, ksid = rsid + 1, wsid = rsid + 2;
+      const int ksid = 17 + 3 * h + 1, wsid = pipeline_writes_on_compute_stream ? ksid : ksid + 1;
+      const int rsid = pipeline_reads_on_main_stream ? 0 : ksid - 1;  // as logged for the schedule checker
       for (auto& a : c.arrays) {
         if (a.zc || !a.partial) continue;
         uint64_t b, n;
