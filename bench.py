@@ -176,6 +176,18 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     ms_host = timed(ctx, host_step, host_steps, 2)
     # the streamed host-resident output: this rank's tiles of the host C
     err_host = _max_over_ranks(ctx, g.verify(compute_id=2, host=True))
+    ms_blobs, mode = ms_host, f"blob pipeline, {blobs} blobs" if blobs else "serial 3-phase"
+    ms_shells = None
+    panels = HOST_RESIDENT_PANELS
+    if ctx.world == 1 and g.split_k == 1 and size % panels == 0 and (size // panels) % max(g.BM, g.BN) == 0:
+        # one GPU holds the whole problem: the square-shell stream
+        # (Cores::gemm_host_shells), whose first kernels need two panels
+        # instead of all of B; reported when it is the faster path
+        ms_shells = timed(ctx, lambda: g.run_host_shells(panels), host_steps, 2)
+        err_shells = g.verify_shells(panels)
+        err_host = max(err_host, err_shells)
+        if ms_shells < ms_host:
+            ms_host, mode = ms_shells, f"square shells, {panels} panels"
     cr.dispose()
     for a in (g.A, g.B, g.C, g.dims):
         a.dispose()  # release 0.5 GB of pinned host memory before the next config
@@ -183,7 +195,8 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
             "sync_per_step_ms": ms_sync, "sync_per_step_gflops": g.flops / (ms_sync * 1e-3) / 1e9,
             "host_resident_ms": ms_host, "host_resident_gflops": g.flops / (ms_host * 1e-3) / 1e9,
             "host_resident_blobs": blobs, "host_resident_calls_ms": [round(x, 3) for x in host_calls],
-            "host_resident_pipelined": host_piped,
+            "host_resident_pipelined": host_piped, "host_resident_mode": mode,
+            "host_resident_blob_pipeline_ms": ms_blobs, "host_resident_shells_ms": ms_shells,
             "ranges": ranges, "max_rel_err": max(err, err_host), "max_rel_err_host_resident": err_host,
             "spin_timeouts": timeouts, "device": "gpu"}
 
@@ -340,6 +353,7 @@ def bench_node_configs(world: int) -> dict:
 
 MAX_REL_ERR = 5e-3
 HOST_RESIDENT_BLOBS = 8
+HOST_RESIDENT_PANELS = 16
 
 
 def _free_port() -> int:
@@ -431,6 +445,9 @@ def main(argv=None) -> int:
                 "sgemm_host_resident_calls_ms": sg.get("host_resident_calls_ms", []),
                 "sgemm_host_resident_pipelined": sg.get("host_resident_pipelined", []),
                 "sgemm_host_resident_max_rel_err": sg.get("max_rel_err_host_resident"),
+                "sgemm_host_resident_mode": sg.get("host_resident_mode"),
+                "sgemm_host_resident_blob_pipeline_ms": sg.get("host_resident_blob_pipeline_ms"),
+                "sgemm_host_resident_shells_ms": sg.get("host_resident_shells_ms"),
                 "sgemm_max_rel_err": sg["max_rel_err"],
                 "sgemm_spin_timeouts": sg["spin_timeouts"],
                 "sgemm_balancer_setup_calls": sg["balancer_setup_calls"],

@@ -308,6 +308,7 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("record_timeline", &Cores::record_timeline)
       .def("set_device_enqueue_levels", &Cores::set_device_enqueue_levels)
       .def_property("debug_checks", &Cores::debug_checks, &Cores::set_debug_checks)
+      .def("gemm_host_shells", &Cores::gemm_host_shells, py::call_guard<py::gil_scoped_release>())
       .def_property("kernel_d2h", &Cores::kernel_d2h, &Cores::set_kernel_d2h)
       .def_property_readonly("kernel_d2h_bytes", &Cores::kernel_d2h_bytes)
       .def("device_enqueue_errors", &Cores::device_enqueue_errors, py::call_guard<py::gil_scoped_release>())

@@ -81,6 +81,11 @@ Cores::~Cores() {
     if (spans_[w].gap_a) (void)hipEventDestroy(spans_[w].gap_a);
     if (spans_[w].gap_b) (void)hipEventDestroy(spans_[w].gap_b);
   }
+  for (size_t w = 0; w < shell_dims_.size() && w < workers_.size(); ++w)
+    if (shell_dims_[w]) {
+      workers_[w]->set_device();
+      (void)hipFree(shell_dims_[w]);
+    }
   for (size_t w = 0; w < peer_ev_.size() && w < workers_.size(); ++w) {
     if (!peer_ev_[w].up) continue;
     workers_[w]->set_device();

@@ -268,6 +268,11 @@ class Cores {
   void capture_begin();
   int capture_end();
   void graph_launch(int id, int times, bool sync);
+  // Host-resident GEMM C = A·Bᵀ streamed in square shells of P row panels
+  // (csrc/shell_gemm.cpp): uploads, kernels and downloads of consecutive
+  // shells overlap; C comes back shell by shell.  Synchronous.
+  void gemm_host_shells(int local_dev, const std::string& kernel, const ArraySpec& A, const ArraySpec& B,
+                        const ArraySpec& C, int M, int N, int K, int panels, int group_m, int BM, int BN, int L);
   void graph_destroy(int id);
   bool capturing() const { return capturing_; }
 
@@ -362,6 +367,8 @@ class Cores {
   double build_ms_ = 0;
   bool enqueue_mode_ = false;
   bool capturing_ = false;
+  std::vector<void*> shell_dims_;         // gemm_host_shells: per-kernel dims, per worker
+  std::vector<size_t> shell_dims_cap_;
   void restore_capture_state();  // the modes capture_begin saved
   struct CaptureSaved {
     bool device_spans, peer_reads, async_enqueue, fine_grained, enqueue_mode, record_timeline;

@@ -270,6 +270,54 @@ class GemmBf16:
             granularity=gran)
         self._uploaded = True
 
+    def run_host_shells(self, panels: int = 8, device: int = 0) -> None:
+        """One host-resident call streamed in square shells
+        (``Cores::gemm_host_shells``, ``csrc/shell_gemm.cpp``): A and B go up
+        in ``panels`` row panels each (A0 B0 A1 B1 …), shell s's two GEMMs
+        (``A_s·B[0..s]ᵀ`` and ``A[0..s-1]·B_sᵀ``) run once panels s have
+        landed, and each shell's C comes down while later panels go up.
+        Unlike the 1-D blob pipeline, the first kernels need only two panels
+        instead of all of B.  One GPU of the cruncher; the host C is in shell
+        layout (:meth:`shells_result`)."""
+        if self.split_k != 1:
+            raise ValueError("shell streaming runs single-pass tiles (split_k == 1)")
+        pm, pn = self.M // max(1, panels), self.N // max(1, panels)
+        if panels < 1 or self.M % panels or self.N % panels or pm % self.BM or pn % self.BN:
+            raise ValueError(f"M and N must split into {panels} panels of whole {self.BM}x{self.BN} tiles")
+        self.cr.cores.gemm_host_shells(device, self.kernel, self.A._spec(), self.B._spec(), self.C._spec(),
+                                       self.M, self.N, self.K, panels, self.group_m, self.BM, self.BN, self.L)
+
+    def shells_result(self, panels: int = 8) -> np.ndarray:
+        """Row-major fp32 C from the host C of :meth:`run_host_shells`
+        (shell by shell: ``R_s`` then ``C_s``, each tile-major)."""
+        pm, pn = self.M // panels, self.N // panels
+        out = np.empty((self.M, self.N), np.float32)
+        c, off = self.C.array, 0
+        for s in range(panels):
+            m, n = pm, (s + 1) * pn
+            out[s * pm:(s + 1) * pm, :n] = untile(c[off:off + m * n], m, n, self.BM, self.BN, self.group_m)
+            off += m * n
+            if s:
+                m, n = s * pm, pn
+                out[:s * pm, s * pn:(s + 1) * pn] = untile(c[off:off + m * n], m, n, self.BM, self.BN, self.group_m)
+                off += m * n
+        return out
+
+    def verify_shells(self, panels: int = 8, samples: int = 16, seed: int = 2) -> float:
+        """Max relative error of sampled 256-row × 256-column blocks of
+        :meth:`shells_result` against a float64 host product."""
+        c = self.shells_result(panels)
+        a = from_bf16_bits(self.A.array).reshape(self.M, self.K)
+        b = from_bf16_bits(self.B.array).reshape(self.N, self.K)
+        rng = np.random.default_rng(seed)
+        worst = 0.0
+        for _ in range(samples):
+            r = int(rng.integers(0, self.M // 256)) * 256
+            q = int(rng.integers(0, self.N // 256)) * 256
+            ref = a[r:r + 256].astype(np.float64) @ b[q:q + 256].astype(np.float64).T
+            worst = max(worst, float(np.abs(c[r:r + 256, q:q + 256] - ref).max() / max(np.abs(ref).max(), 1e-30)))
+        return worst
+
     def result(self, download: bool = True) -> np.ndarray:
         """Row-major fp32 C (downloads every device's slice when resident)."""
         if download:

@@ -269,3 +269,20 @@ def test_gemm_benchmarked_size_verify(tile, rows):
     cr.dispose()
     for a in (g.A, g.B, g.C, g.dims):
         a.dispose()
+
+
+@pytest.mark.parametrize("tile,panels", [("256x256pb", 4), ("256x256pb", 2), ("256x128pe", 4), ("256x256", 1)])
+def test_gemm_host_shells_matches_fp64(tile, panels):
+    """Host-resident GEMM streamed in square shells (Cores::gemm_host_shells)
+    against a float64 host product, every element; repeated calls reuse the
+    device buffers."""
+    from cekirdekler_amd.ops.gemm import GemmBf16
+
+    g = GemmBf16(2048, 2048, 512, devices=_gpu()[0], tile=tile, group_m=2)
+    for _ in range(2):
+        g.C.array[:] = 0
+        g.run_host_shells(panels)
+        got = g.shells_result(panels)
+        ref = g.reference()
+        assert float(np.abs(got - ref).max() / np.abs(ref).max()) < 1e-5
+    g.cr.dispose()
