@@ -976,9 +976,10 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
       hipStream_t rs = pipeline_reads_on_main_stream ? m : wk.pipe_stream(h, 0), ks = wk.pipe_stream(h, 1);
       // writes_on_compute_stream: a blob's D2H follows its kernel on the same
       // stream (in-stream order) instead of a write stream gated by an event
-      hipStream_t ws = pipeline_writes_on_compute_stream ? ks : wk.pipe_stream(h, 2);
+      hipStream_t ws = pipeline_writes_on_compute_stream ? ks : wk.pipe_stream(pipeline_writes_one_stream ? 0 : h, 2);
       long long off = ref + h * (range / halves) + k * chunk;
-      const int ksid = 17 + 3 * h + 1, wsid = pipeline_writes_on_compute_stream ? ksid : ksid + 1;
+      const int ksid = 17 + 3 * h + 1;
+      const int wsid = pipeline_writes_on_compute_stream ? ksid : (pipeline_writes_one_stream ? 19 : ksid + 1);
       const int rsid = pipeline_reads_on_main_stream ? 0 : ksid - 1;  // as logged for the schedule checker
       for (auto& a : c.arrays) {
         if (a.zc || !a.partial) continue;

@@ -297,6 +297,8 @@ class Cores {
   bool peer_reads = true;
   // event pipeline: issue each blob's D2H on its compute stream
   bool pipeline_writes_on_compute_stream = false;
+  // event pipeline: every blob's D2H on one write stream (blob order)
+  bool pipeline_writes_one_stream = false;
   // event pipeline: issue every blob's uploads on the main stream, after the
   // full reads (one in-order chain; the copies share the SDMA engine
   // anyway).  With separate read streams, the first call after any
