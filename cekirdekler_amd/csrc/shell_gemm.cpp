@@ -36,10 +36,12 @@ void Cores::gemm_host_shells(int local_dev, const std::string& kernel, const Arr
   if (capturing_) throw Error("gemm_host_shells: not inside a graph capture");
   if (panels < 1 || M % panels || N % panels) throw Error("gemm_host_shells: M and N must split into panels");
   const int PM = M / panels, PN = N / panels;
-  if (PM % BM || PN % BN || K % 64 || L <= 0) throw Error("gemm_host_shells: panel sizes must be whole tiles");
-  if (A.bytes != 2ull * M * K || B.bytes != 2ull * N * K || C.bytes != 4ull * M * N || A.elem_size != 2 ||
-      B.elem_size != 2 || C.elem_size != 4)
-    throw Error("gemm_host_shells: A, B must be bf16 [M][K], [N][K] and C fp32 [M][N]");
+  const int es = A.elem_size;  // 2: bf16 operands (BK = 64), 4: fp32 operands (BK = 32)
+  if (PM % BM || PN % BN || L <= 0 || (es != 2 && es != 4) || K % (es == 2 ? 64 : 32))
+    throw Error("gemm_host_shells: panel sizes must be whole tiles and K whole K-tiles");
+  if (B.elem_size != es || A.bytes != 1ull * es * M * K || B.bytes != 1ull * es * N * K ||
+      C.bytes != 4ull * M * N || C.elem_size != 4)
+    throw Error("gemm_host_shells: A, B must be [M][K], [N][K] of one element type and C fp32 [M][N]");
   hipFunction_t fn = w.program().gpu_fn(kernel);
   w.wait();
   w.set_device();
@@ -84,8 +86,8 @@ void Cores::gemm_host_shells(int local_dev, const std::string& kernel, const Arr
       const long long tiles = static_cast<long long>(d[0] / BM) * (d[1] / BN);
       if (tiles == 0) continue;
       const void* pd = dd + (2 * s + part) * 8;
-      const void* pa = dA + 2 * (part == 0 ? s * a_panel : 0);
-      const void* pb = dB + 2 * (part == 0 ? 0 : s * b_panel);
+      const void* pa = dA + es * (part == 0 ? s * a_panel : 0);
+      const void* pb = dB + es * (part == 0 ? 0 : s * b_panel);
       void* pc = dC + 4 * c_off;
       long long off = 0, gs = tiles * L;
       void* params[] = {&pd, &pa, &pb, &pc, &off, &gs};

@@ -307,8 +307,9 @@ class GemmBf16:
         """Max relative error of sampled 256-row × 256-column blocks of
         :meth:`shells_result` against a float64 host product."""
         c = self.shells_result(panels)
-        a = from_bf16_bits(self.A.array).reshape(self.M, self.K)
-        b = from_bf16_bits(self.B.array).reshape(self.N, self.K)
+        a, b = self.A.array, self.B.array
+        a = (from_bf16_bits(a) if a.dtype == np.uint16 else a).reshape(self.M, self.K)
+        b = (from_bf16_bits(b) if b.dtype == np.uint16 else b).reshape(self.N, self.K)
         rng = np.random.default_rng(seed)
         worst = 0.0
         for _ in range(samples):

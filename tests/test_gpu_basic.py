@@ -286,3 +286,16 @@ def test_gemm_host_shells_matches_fp64(tile, panels):
         ref = g.reference()
         assert float(np.abs(got - ref).max() / np.abs(ref).max()) < 1e-5
     g.cr.dispose()
+
+
+def test_gemm_f32_host_shells_matches_fp64():
+    """The square-shell host-resident stream with fp32 operands (GemmF32)."""
+    from cekirdekler_amd.ops.gemm import GemmF32
+
+    g = GemmF32(1024, 1024, 256, devices=_gpu()[0], tile="256x256ir", group_m=2)
+    g.run_host_shells(2)
+    got = g.shells_result(2)
+    ref = g.reference()
+    assert float(np.abs(got - ref).max() / np.abs(ref).max()) < 1e-5
+    assert g.verify_shells(2, samples=4) < 1e-5
+    g.cr.dispose()
