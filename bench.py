@@ -162,7 +162,11 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     # the event-driven read/compute/write pipeline in 8 blobs (B a full
     # read, A row panels and C tiles streamed; profiles/hostres_streaming.md).
     # Falls back to the serial 3-phase path when the tile cannot stream.
-    blobs = HOST_RESIDENT_BLOBS if g.can_stream() else 0
+    # a blob holds whole tile groups (A row panels), and the runtime pipelines
+    # only when every rank's range splits into whole blobs: at N ranks each
+    # holds groups/N of them
+    groups = (g.M // g.BM) // max(1, g.group_m)
+    blobs = max(1, min(HOST_RESIDENT_BLOBS, groups // ctx.world)) if g.can_stream() else 0
     host_calls = []
 
     host_piped = []
