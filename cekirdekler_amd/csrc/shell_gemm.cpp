@@ -78,7 +78,8 @@ void Cores::gemm_host_shells(int local_dev, const std::string& kernel, const Arr
     w.h2d(up, B, s * b_panel, b_panel);
     hipEvent_t landed = w.event(slot++);
     CEK_HIP(hipEventRecord(landed, up));
-    hipStream_t ks = w.pipe_stream(s & 1, 1), ws = w.pipe_stream(s & 1, 2);
+    hipStream_t ks = w.pipe_stream(s & 1, 1);
+    hipStream_t ws = pipeline_writes_on_compute_stream ? ks : w.pipe_stream(s & 1, 2);
     CEK_HIP(hipStreamWaitEvent(ks, landed, 0));
     const uint64_t shell_begin = c_off;
     for (int part = 0; part < 2; ++part) {
@@ -95,12 +96,17 @@ void Cores::gemm_host_shells(int local_dev, const std::string& kernel, const Arr
                                     params, nullptr));
       c_off += static_cast<uint64_t>(d[0]) * d[1];
     }
-    hipEvent_t done = w.event(slot++);
-    CEK_HIP(hipEventRecord(done, ks));
-    CEK_HIP(hipStreamWaitEvent(ws, done, 0));
+    if (ws != ks) {
+      hipEvent_t done = w.event(slot++);
+      CEK_HIP(hipEventRecord(done, ks));
+      CEK_HIP(hipStreamWaitEvent(ws, done, 0));
+    }
     w.d2h(ws, C, shell_begin, c_off - shell_begin);
   }
-  for (int h = 0; h < 2 && h < panels; ++h) CEK_HIP(hipStreamSynchronize(w.pipe_stream(h, 2)));
+  for (int h = 0; h < 2 && h < panels; ++h) {
+    CEK_HIP(hipStreamSynchronize(w.pipe_stream(h, 1)));
+    CEK_HIP(hipStreamSynchronize(w.pipe_stream(h, 2)));
+  }
   CEK_HIP(hipStreamSynchronize(up));
 }
 

@@ -24,6 +24,8 @@ tile = sys.argv[3] if len(sys.argv) > 3 else "256x256pb"
 size = 8192
 cr = ck.ClNumberCruncher(ck.ClPlatforms.all().gpus()[0], "", prebuilt=library(*GEMM_LIBS))
 g = GemmBf16(size, size, size, cruncher=cr, tile=tile)
+# wcs: downloads on the compute streams, right behind each shell's kernels
+cr.cores.pipeline_writes_on_compute_stream = "wcs" in sys.argv[4:]
 out = {}
 
 
