@@ -96,3 +96,36 @@ def test_library_arity_covers_every_kernel():
     for names in LIBRARY.values():
         for k in names:
             assert k in ARITY, k
+
+
+def _tile_major(c, M, N, BM, BN, gm):
+    """Row-major [M][N] → tile-major in the kernels' grouped tile order."""
+    from cekirdekler_amd.ops.gemm import tile_coords
+
+    ntiles = (M // BM) * (N // BN)
+    tm, tn = tile_coords(np.arange(ntiles), M, N, BM, BN, gm)
+    return np.concatenate([c[r * BM:(r + 1) * BM, q * BN:(q + 1) * BN].ravel() for r, q in zip(tm, tn)])
+
+
+@pytest.mark.parametrize("panels,gm", [(1, 2), (2, 2), (4, 1), (4, 3)])
+def test_shell_layout_round_trip(panels, gm):
+    """The host C layout of the square-shell stream (Cores::gemm_host_shells:
+    shell by shell, R_s = rows of panel s × columns of panels 0..s, then
+    C_s = rows of panels 0..s-1 × columns of panel s, each tile-major) is
+    undone exactly by GemmBf16.shells_result."""
+    from types import SimpleNamespace
+
+    from cekirdekler_amd.ops.gemm import GemmBf16
+
+    M, N, BM, BN = 512, 1024, 64, 128
+    full = np.random.default_rng(0).standard_normal((M, N)).astype(np.float32)
+    pm, pn = M // panels, N // panels
+    parts = []
+    for s in range(panels):
+        parts.append(_tile_major(full[s * pm:(s + 1) * pm, :(s + 1) * pn], pm, (s + 1) * pn, BM, BN, gm))
+        if s:
+            parts.append(_tile_major(full[:s * pm, s * pn:(s + 1) * pn], s * pm, pn, BM, BN, gm))
+    host = np.concatenate(parts)
+    assert host.size == M * N
+    g = SimpleNamespace(M=M, N=N, BM=BM, BN=BN, group_m=gm, C=SimpleNamespace(array=host))
+    np.testing.assert_array_equal(GemmBf16.shells_result(g, panels), full)
