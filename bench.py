@@ -332,11 +332,20 @@ def bench_node_configs(world: int) -> dict:
     out = {}
     rccl = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
             "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "rccl_gemm.py"]
-    for name, cmd in (("nbody_pipeline", [sys.executable, "nbody_pipeline.py", "--gpus", str(world), "--pushes", "14"]),
-                      ("task_pool", [sys.executable, "task_pool.py", "--gpus", str(world)]),
-                      ("saxpy_1m_cpu", [sys.executable, "saxpy_cpu.py"]),
-                      ("wave_cpu_gpu", [sys.executable, "wave_cpu_gpu.py"]),
-                      ("sgemm_host_resident_rccl", rccl)):
+    import torch
+
+    configs = [("nbody_pipeline", [sys.executable, "nbody_pipeline.py", "--gpus", str(world), "--pushes", "14"]),
+               ("task_pool", [sys.executable, "task_pool.py", "--gpus", str(world)]),
+               ("saxpy_1m_cpu", [sys.executable, "saxpy_cpu.py"]),
+               ("wave_cpu_gpu", [sys.executable, "wave_cpu_gpu.py"])]
+    if world <= torch.cuda.device_count():
+        configs.append(("sgemm_host_resident_rccl", rccl))
+    else:
+        # a launcher rehearsal with ranks sharing a GPU: RCCL refuses two
+        # ranks on one device
+        out["sgemm_host_resident_rccl"] = {"skipped": f"{world} ranks on {torch.cuda.device_count()} GPU(s); "
+                                                      "RCCL needs one GPU per rank"}
+    for name, cmd in configs:
         # own session: a timeout kills the whole process group (torchrun's ranks too)
         p = subprocess.Popen(cmd, cwd=os.path.join(ROOT, "bench"), env=env, stdout=subprocess.PIPE,
                              stderr=subprocess.PIPE, text=True, start_new_session=True)
