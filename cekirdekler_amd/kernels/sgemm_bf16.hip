@@ -125,7 +125,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 
   const int nk = K / BK / S;
   unsigned my_xcc = 0;
-  if constexpr (XCH == 2) {
+  if constexpr (XCH == 2 || XCH == 5) {
     // publish this work-group's XCD for the partner split (flags[4t + 2 + s])
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(my_xcc));
     my_xcc &= 15u;
@@ -546,6 +546,87 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       // probe build: no hand-over at all (wrong sums), to time the
       // exchange's share of the epilogue
       if (wr != s) return;
+    } else if constexpr (XCH == 5) {
+      // Hand-over by L2 atomics: split s stores its own row half of its
+      // partial straight into C, then, once the partner has stored ITS half,
+      // adds the other half into C with return-less global_atomic_add_f32.
+      // On one XCD both land in the shared L2, so nothing is read back into
+      // the CU: 128 KiB of stores + 128 KiB of atomics per work-group, one
+      // flag wait, no partial round trip.  Partners on different XCDs (not
+      // produced by the remap, kept for safety) use the fenced W exchange.
+      constexpr int HALF = BM / 2 * BN;
+      constexpr int FPT = 4;
+      int* err = &tile_cnt[(size_t)FPT * ntm * ntn];
+      auto spin = [&](int* w) -> int {
+        int v, spins = 0;
+        while ((v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1 << 21)) {
+            __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return 0;
+          }
+        }
+        return v;
+      };
+      int* ok = reinterpret_cast<int*>(smem);
+      __syncthreads();  // every wave is past its last LDS fragment read
+      if (tid == 0) {
+        const int px = spin(&tile_cnt[4 * t + 2 + (1 - s)]);
+        tile_cnt[4 * t + 2 + (1 - s)] = 0;  // re-arm the partner's word
+        ok[0] = px != 0;
+        ok[1] = px == (int)my_xcc + 1;
+      }
+      __syncthreads();
+      const bool same = ok[1] != 0;
+      float* ct = C + (size_t)t * BM * BN;
+      f32x4* wh = reinterpret_cast<f32x4*>(W + (size_t)t * BM * BN + (size_t)wr * HALF);
+      if ((wr == s) == same) {  // one XCD: own half into C; else: the other half into W
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            if (same) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr] = acc[i][j][r];
+            } else {
+              wh[((wc * FM + i) * FN + j) * 64 + lane] = acc[i][j];
+            }
+          }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        int good = ok[0];
+        if (!same) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(&tile_cnt[FPT * t + (1 - s)], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (good) good = spin(&tile_cnt[FPT * t + s]) != 0;
+        tile_cnt[FPT * t + s] = 0;  // re-arm for the next call
+        ok[2] = good;
+      }
+      __syncthreads();
+      if (!ok[2]) return;  // timed out: counted in the error word
+      if (same) {
+        if (wr == s) return;  // own half already in C
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              unsafeAtomicAdd(&ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr],
+                              acc[i][j][r]);
+        return;
+      }
+      // across XCDs: the partner's half of our rows is in W; add it and fall
+      // through to the plain C store of our own half
+      if (wr != s) return;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const f32x4* rh = reinterpret_cast<const f32x4*>(W + (size_t)t * BM * BN + (size_t)s * HALF);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] += rh[((wc * FM + i) * FN + j) * 64 + lane];
     } else {
     constexpr int HALF = BM / 2 * BN;
     f32x4* wh = reinterpret_cast<f32x4*>(W + (size_t)t * BM * BN + (size_t)wr * HALF);
@@ -742,6 +823,12 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_syn(
     const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
   __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
   gemm_tile<2, 4, 8, 4, 4, true, false, 2, true>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
+}
+// same split, the hand-over by L2 atomics into C (flags: 4 per tile + 1)
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sa(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
+  gemm_tile<2, 4, 8, 4, 4, true, false, 5>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
 }
 extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pbn(
     const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
