@@ -168,7 +168,7 @@ def test_gemm_wave_granularity_two_logical_devices():
     assert GemmBf16(256, 256, 64, devices=g0, tile="256x256pb").granularity() == 512  # < 1 wave: per tile
 
 
-@pytest.mark.parametrize("kernel", ["quad", "pool8", "pool16", "pk16", "pk32", "blk16", "blk64", "blk8"])
+@pytest.mark.parametrize("kernel", ["quad", "pool8", "pool16", "pk16", "pk32", "blk16", "blk64", "blk8", "blk8f"])
 def test_mandelbrot_event_pipeline_matches_numpy(kernel):
     from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
 
@@ -177,6 +177,22 @@ def test_mandelbrot_event_pipeline_matches_numpy(kernel):
     ref = m.reference()
     mism = np.mean(img != ref)
     assert mism < 0.01, mism
+
+
+def test_mandelbrot_deferred_count_matches_blk8():
+    """blk8f (escape counted once, from the z frozen at the escape block's
+    start) against blk8 (counted every iteration), same arithmetic: equal
+    except where float rounding lets |z|² dip back to <= 4 after exceeding it
+    (blk8 then counts on; blk8f keeps the first escape, the reference's
+    definition)."""
+    from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
+
+    imgs = []
+    for k in ("blk8", "blk8f"):
+        m = MandelbrotRenderer(1024, 1024, max_iter=256, devices=_gpu()[0], kernel=k)
+        imgs.append(m.render(pipeline=False).copy())
+        m.cr.dispose()
+    assert np.mean(imgs[0] != imgs[1]) < 1e-4
 
 
 @pytest.mark.parametrize("kernel,per_item", [("cek_reduce_sum_f32", 8), ("cek_reduce_sum_f32_x32", 32)])

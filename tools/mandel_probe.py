@@ -20,10 +20,11 @@ ap.add_argument("--size", type=int, default=4096)
 ap.add_argument("--iters", type=int, default=256)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--extra", action="append", default=[])
+ap.add_argument("--only", default="", help="comma-separated kernel keys (default: all)")
 a = ap.parse_args()
 g0 = ck.ClPlatforms.all().gpus()[0]
 
-variants = [(k, None) for k in mb.KERNELS]
+variants = [(k, None) for k in mb.KERNELS if not a.only or k in a.only.split(",")]
 for e in a.extra:
     path, rest = e.split("|")
     name, ppw = rest.split(",")
