@@ -282,7 +282,38 @@ def bench_mandelbrot(ctx, steps, warmup):
     out = {"ms": ms, "gflops": flops / (ms * 1e-3) / 1e9, "flop_per_iter": 8, "kernel": m.kernel,
            "image_pinned": m.out.pinned}
     cr.dispose()
+    if ctx.rank == 0:
+        out["kernel_only"] = _mandelbrot_kernel_only()
     return out
+
+
+def _mandelbrot_kernel_only(kernel: str = "blk8g", reps: int = 20) -> dict:
+    """The fastest Mandelbrot kernel alone on this rank's GPU (image left in
+    device memory, no D2H): BASELINE's "kernel >= 50 % of FP32 peak" target.
+    The end-to-end number above is PCIe-bound and runs blk8 (the kernel does
+    not change it, tools/mandel_ab_probe.py)."""
+    import torch
+
+    from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
+    import cekirdekler_amd as ck
+
+    gpus = ck.ClPlatforms.all().gpus()
+    m = MandelbrotRenderer(4096, 4096, max_iter=256, devices=gpus[0], kernel=kernel)
+    m.render(1, pipeline=False)  # image downloaded once: its counts give the FLOPs
+    flops = m.flops()
+    m.out.write = False
+    for _ in range(3):
+        m.render(1, pipeline=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        m.render(1, pipeline=False)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    m.cr.dispose()
+    tf = flops / (ms * 1e-3) / 1e12
+    return {"kernel": m.kernel, "ms": round(ms, 4), "tflops": round(tf, 2),
+            "pct_fp32_peak_157_3": round(100 * tf / 157.3, 1)}
 
 
 def bench_lb_iters():

@@ -20,7 +20,7 @@ FLOP_PER_ITER = 8
 
 # kernel variants; the band kernels additionally need device and pipeline
 # chunk ranges made of whole 16-row bands (see kernels/mandelbrot.hip)
-BAND_ROWS = {"blk16": 16, "blk16w4": 16, "blk64": 16, "blk8": 8, "blk8f": 8}  # rows per band
+BAND_ROWS = {"blk16": 16, "blk16w4": 16, "blk64": 16, "blk8": 8, "blk8f": 8, "blk8g": 8}  # rows per band
 BAND_KERNELS = set(BAND_ROWS)
 KERNELS = {
     # name: (library kernel, pixels per work item, work-group size)
@@ -39,13 +39,14 @@ KERNELS = {
     # same block, escape counted once after the loop from the z frozen at the
     # escape block's start (5 instead of 8 packed instructions per iteration)
     "blk8f": ("cek_mandelbrot_blk8f_f32", 2, 64),
+    "blk8g": ("cek_mandelbrot_blk8g_f32", 2, 64),     # blk8f, zr chain reassociated (2 deep)
 }
 
 
 class MandelbrotRenderer:
     def __init__(self, width: int = 4096, height: int = 4096, max_iter: int = 256,
                  view=(-2.0, -1.5, 3.0, 3.0), devices=None, cruncher: ClNumberCruncher | None = None,
-                 kernel: str = "blk8f"):
+                 kernel: str = "blk8"):
         self.kernel, self.ppw, self.local = KERNELS[kernel]
         if (width * height) % (256 * self.ppw) or width * height >= 2 ** 31:
             raise ValueError(f"width*height must be a multiple of {256 * self.ppw} and below 2^31")

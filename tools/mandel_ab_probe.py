@@ -1,0 +1,41 @@
+"""GPU probe: Mandelbrot 4096² kernel variants end to end through the event
+pipeline (8 blobs), interleaved over rounds on one box (median ms), plus
+each variant's pixel mismatch against the float32 numpy reference on the
+first 1024 rows.
+
+    python tools/mandel_ab_probe.py blk8,blk8f,blk8g [rounds]
+"""
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+import cekirdekler_amd as ck  # noqa: E402
+from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer  # noqa: E402
+
+kernels = sys.argv[1].split(",")
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+gpu = ck.ClPlatforms.all().gpus()[0]
+ms = {k: [] for k in kernels}
+rs = {k: MandelbrotRenderer(4096, 4096, 256, devices=gpu, kernel=k) for k in kernels}
+for r in range(rounds):
+    for k, m in rs.items():
+        for _ in range(2):
+            m.render(1, pipeline=True, blobs=8)
+        ts = []
+        for _ in range(10):
+            t = time.perf_counter()
+            m.render(1, pipeline=True, blobs=8)
+            ts.append((time.perf_counter() - t) * 1e3)
+        ms[k].append(statistics.median(ts))
+ref = next(iter(rs.values())).reference(rows=1024)
+out = {}
+for k, m in rs.items():
+    img = m.out.array.reshape(4096, 4096)[:1024]
+    out[k] = {"e2e_ms_median": round(statistics.median(ms[k]), 4), "e2e_ms_min": round(min(ms[k]), 4),
+              "mismatch_vs_numpy_rows0_1023": float(np.mean(img != ref))}
+print(json.dumps(out), flush=True)
