@@ -125,7 +125,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 
   const int nk = K / BK / S;
   unsigned my_xcc = 0;
-  if constexpr (XCH == 2 || XCH == 5) {
+  if constexpr (XCH == 2 || XCH == 5 || XCH == 6) {
     // publish this work-group's XCD for the partner split (flags[4t + 2 + s])
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(my_xcc));
     my_xcc &= 15u;
@@ -627,6 +627,87 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] += rh[((wc * FM + i) * FN + j) * 64 + lane];
+    } else if constexpr (XCH == 6) {
+      // XCH 2's hand-over in two rounds of FM/2 row blocks (64 of the 128
+      // rows) through one 64 KiB slot per work-group, reused by round 1:
+      // the XCD's partials in flight are 2 MiB instead of its whole 4 MiB L2,
+      // so the read-back hits L2 and half as many dead partial lines are
+      // written back.  My flag word for the partner counts 1 (round-0 rows
+      // in my slot), 2 (I have read the partner's round-0 rows: its slot is
+      // free), 3 (round-1 rows in my slot); all three are monotone, so
+      // neither side can wait on the other's wait.
+      constexpr int HALF = BM / 2 * BN;
+      constexpr int FH = FM / 2;
+      constexpr int FPT = 4;
+      int* err = &tile_cnt[(size_t)FPT * ntm * ntn];
+      auto spin_ge = [&](int* w, int want) -> int {
+        int v, spins = 0;
+        while ((v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < want) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1 << 21)) {
+            __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return 0;
+          }
+        }
+        return v;
+      };
+      int* ok = reinterpret_cast<int*>(smem);
+      __syncthreads();  // every wave is past its last LDS fragment read
+      if (tid == 0) {
+        const int px = spin_ge(&tile_cnt[4 * t + 2 + (1 - s)], 1);
+        tile_cnt[4 * t + 2 + (1 - s)] = 0;  // re-arm the partner's word
+        ok[0] = px != 0;
+        ok[1] = px == (int)my_xcc + 1;
+      }
+      __syncthreads();
+      const bool same = ok[1] != 0;
+      int* inbox = &tile_cnt[FPT * t + s];        // written by the partner
+      int* outbox = &tile_cnt[FPT * t + (1 - s)];  // read by the partner
+      f32x4* wh = reinterpret_cast<f32x4*>(W + (size_t)t * BM * BN + (size_t)(1 - s) * HALF);
+      const f32x4* rh = reinterpret_cast<const f32x4*>(W + (size_t)t * BM * BN + (size_t)s * HALF);
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        if (wr != s) {
+#pragma unroll
+          for (int i = 0; i < FH; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) wh[((wc * FH + i) * FN + j) * 64 + lane] = acc[r * FH + i][j];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+          int good = ok[0];
+          if (!same) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          __hip_atomic_store(outbox, 2 * r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (good) good = spin_ge(inbox, 2 * r + 1) != 0;
+          ok[0] = good;
+        }
+        __syncthreads();
+        if (wr == s && ok[0]) {
+          if (!same) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          f32x4 part[FH][FN];
+#pragma unroll
+          for (int i = 0; i < FH; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) part[i][j] = rh[((wc * FH + i) * FN + j) * 64 + lane];
+#pragma unroll
+          for (int i = 0; i < FH; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[r * FH + i][j] += part[i][j];
+        }
+        if (r == 0) {
+          // the partner's slot is read (loads landed); wait until ours is
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          if (tid == 0) {
+            __hip_atomic_store(outbox, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (ok[0]) ok[0] = spin_ge(inbox, 2) != 0;
+          }
+          __syncthreads();
+        }
+      }
+      if (tid == 0) *inbox = 0;  // the partner's last word (3) has arrived: re-arm
+      if (wr != s) return;
     } else {
     constexpr int HALF = BM / 2 * BN;
     f32x4* wh = reinterpret_cast<f32x4*>(W + (size_t)t * BM * BN + (size_t)wr * HALF);
@@ -823,6 +904,13 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_syn(
     const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
   __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
   gemm_tile<2, 4, 8, 4, 4, true, false, 2, true>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
+}
+// same split, the hand-over in two rounds through one reused 64 KiB slot
+// (flags: 4 per tile + 1)
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sz(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
+  gemm_tile<2, 4, 8, 4, 4, true, false, 6>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
 }
 // same split, the hand-over by L2 atomics into C (flags: 4 per tile + 1)
 extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sa(

@@ -45,6 +45,8 @@ TILES = {
     "256x256pby": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sy"),
     # same split, other row half added into C by L2 atomics (no partial read-back)
     "256x256pba": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sa"),
+    # same split, the hand-over in two rounds through one reused slot (half the L2 footprint)
+    "256x256pbz": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sz"),
     # same with nontemporal C stores; probe-only: no C store / no hand-over
     "256x256pbyn": (256, 256, 512, "cek_sgemm_bf16_256x256pb_syn"),
     "256x256pby_nostore": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sy_nostore"),
@@ -110,7 +112,7 @@ F32_TILES = {
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
 SPLIT_K_TILES = {"256x256pp", "256x128pp", "256x256pb"}
 # tiles whose kernel always runs two K-splits that exchange row halves
-EXCHANGE_TILES = {"256x256pbx": 2, "256x256pby": 4, "256x256pba": 4, "256x256pbyn": 4, "256x256pby_nostore": 4,
+EXCHANGE_TILES = {"256x256pbx": 2, "256x256pby": 4, "256x256pba": 4, "256x256pbz": 4, "256x256pbyn": 4, "256x256pby_nostore": 4,
                   "256x256pby_noxch": 4}  # flag words per tile
 
 

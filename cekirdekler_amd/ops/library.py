@@ -17,7 +17,7 @@ LIBRARY = {
     "sgemm_bf16": ["cek_sgemm_bf16_256x256", "cek_sgemm_bf16_256x256p", "cek_sgemm_bf16_256x256pp", "cek_sgemm_bf16_256x256ps",
                    "cek_sgemm_bf16_256x128", "cek_sgemm_bf16_256x128p", "cek_sgemm_bf16_256x128pp", "cek_sgemm_bf16_256x128ps",
                    "cek_sgemm_bf16_128x128", "cek_sgemm_bf16_128x128p",
-                   "cek_sgemm_bf16_256x256pp_sk", "cek_sgemm_bf16_256x128pp_sk", "cek_sgemm_bf16_256x256pb_sk", "cek_sgemm_bf16_256x256pb_sx", "cek_sgemm_bf16_256x256pb_sy", "cek_sgemm_bf16_256x256pb_sa",
+                   "cek_sgemm_bf16_256x256pp_sk", "cek_sgemm_bf16_256x128pp_sk", "cek_sgemm_bf16_256x256pb_sk", "cek_sgemm_bf16_256x256pb_sx", "cek_sgemm_bf16_256x256pb_sy", "cek_sgemm_bf16_256x256pb_sa", "cek_sgemm_bf16_256x256pb_sz",
                    "cek_sgemm_bf16_256x256pb_sy_nostore", "cek_sgemm_bf16_256x256pb_sy_noxch", "cek_sgemm_bf16_256x256pb_syn",
                    "cek_sgemm_bf16_256x256pbn", "cek_sgemm_bf16_256x256i", "cek_sgemm_bf16_256x128i",
                    "cek_sgemm_bf16_256x256pp_nostore", "cek_sgemm_bf16_256x256pb", "cek_sgemm_bf16_256x128pb",
@@ -49,7 +49,7 @@ LIBRARY = {
 # "name:arity" so a compute() whose array list does not match the kernel's
 # signature is rejected on the host instead of faulting on the device.
 ARITY = {
-    **{k: (6 if k.endswith(("_sk", "_sx", "_sy", "_sa", "_sy_nostore", "_sy_noxch", "_syn")) else 4) for k in LIBRARY["sgemm_bf16"] + LIBRARY["sgemm8p_bf16"] + LIBRARY["sgemm_pp32_bf16"]},
+    **{k: (6 if k.endswith(("_sk", "_sx", "_sy", "_sa", "_sz", "_sy_nostore", "_sy_noxch", "_syn")) else 4) for k in LIBRARY["sgemm_bf16"] + LIBRARY["sgemm8p_bf16"] + LIBRARY["sgemm_pp32_bf16"]},
     **{k: 4 for k in LIBRARY["sgemm_f32"]},
     **{k: 3 for k in LIBRARY["mandelbrot"]},
     **{k: 4 for k in LIBRARY["nbody"] if "energy" not in k},
