@@ -498,3 +498,80 @@ extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8g_f32(const 
   const int ny = ey < 0 ? max_iter : min(ey + (int)(cnt.y + 0.5f), max_iter);
   out[((long long)row * W + col) >> 1] = make_int2(nx, ny);
 }
+
+// blk8g with two packed pairs per lane: a 16×16 block per one-wave
+// work-group (rows r and r + 8 of a 16-row band), twice the independent
+// work per wave for the same deferred-count iteration ("blk16g").
+extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk16g_f32(const float* view, const int* size,
+                                                                         int2* out, CEK_HIDDEN) {
+  const long long w = cek_global_id();
+  const int W = size[0], max_iter = size[2];
+  const long long band_items = 4LL * W;  // 16 rows × W px / 4 px per work item
+  const long long band = w / band_items;
+  const int q = (int)(w - band * band_items);
+  const int blk = q >> 6, l = q & 63;
+  const int row0 = (int)band * 16 + (l >> 3), col = blk * 16 + (l & 7) * 2;
+  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
+  const f32x2 cr = {x0 + col * dx, x0 + (col + 1) * dx};
+  const f32x2 two = {2.f, 2.f};
+  f32x2 civ[2], zr[2], zi[2], fr[2], fi[2];
+  int e[2][2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const float ci = y0 + (row0 + 8 * p) * dy;
+    civ[p] = f32x2{ci, ci};
+    zr[p] = zi[p] = fr[p] = fi[p] = f32x2{0.f, 0.f};
+    e[p][0] = e[p][1] = -1;
+  }
+  for (int it = 0; it < max_iter; it += 8) {
+    f32x2 sr[2], si[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      sr[p] = zr[p];
+      si[p] = zi[p];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const f32x2 zi2 = zi[p] * zi[p];
+        const f32x2 tz = zr[p] * zi[p];
+        zr[p] = __builtin_elementwise_fma(zr[p], zr[p], cr) - zi2;
+        zi[p] = __builtin_elementwise_fma(tz, two, civ[p]);
+      }
+    bool all = true;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const f32x2 m = __builtin_elementwise_fma(zr[p], zr[p], zi[p] * zi[p]);
+      if (e[p][0] < 0 && !(m.x <= 4.f)) {
+        e[p][0] = it;
+        fr[p].x = sr[p].x;
+        fi[p].x = si[p].x;
+      }
+      if (e[p][1] < 0 && !(m.y <= 4.f)) {
+        e[p][1] = it;
+        fr[p].y = sr[p].y;
+        fi[p].y = si[p].y;
+      }
+      all = all && e[p][0] >= 0 && e[p][1] >= 0;
+    }
+    if (all) break;
+  }
+  const f32x2 nbig = {-1048576.f, -1048576.f}, cbig = {4194304.f, 4194304.f};
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    f32x2 cnt = {0.f, 0.f}, ar = fr[p], ai = fi[p];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const f32x2 zi2 = ai * ai;
+      const f32x2 m = __builtin_elementwise_fma(ar, ar, zi2);
+      cnt += pk_fma_clamp(m, nbig, cbig);
+      const f32x2 tz = ar * ai;
+      ar = __builtin_elementwise_fma(ar, ar, cr) - zi2;
+      ai = __builtin_elementwise_fma(tz, two, civ[p]);
+    }
+    const int nx = e[p][0] < 0 ? max_iter : min(e[p][0] + (int)(cnt.x + 0.5f), max_iter);
+    const int ny = e[p][1] < 0 ? max_iter : min(e[p][1] + (int)(cnt.y + 0.5f), max_iter);
+    out[((long long)(row0 + 8 * p) * W + col) >> 1] = make_int2(nx, ny);
+  }
+}
