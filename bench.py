@@ -287,7 +287,7 @@ def bench_mandelbrot(ctx, steps, warmup):
     return out
 
 
-def _mandelbrot_kernel_only(kernel: str = "blk8g", reps: int = 20) -> dict:
+def _mandelbrot_kernel_only(kernel: str = "blk8h", reps: int = 20) -> dict:
     """The fastest Mandelbrot kernel alone on this rank's GPU (image left in
     device memory, no D2H): BASELINE's "kernel >= 50 % of FP32 peak" target.
     The end-to-end number above is PCIe-bound and runs blk8 (the kernel does

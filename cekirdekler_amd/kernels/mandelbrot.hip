@@ -575,3 +575,65 @@ extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk16g_f32(const
     out[((long long)(row0 + 8 * p) * W + col) >> 1] = make_int2(nx, ny);
   }
 }
+
+// blk8g with cheaper bookkeeping ("blk8h"): at each block's end a pixel
+// whose |z|² is still <= 4 records that z and the iteration (it + 8) as its
+// last known non-escaped point; an escaped pixel stops recording (escape is
+// monotone, inf/NaN fail `m <= 4`).  No start-of-block copies and no "already
+// escaped?" tests: 2 compares + 6 selects per block instead of 19 VALU ops.
+// The counting pass from the last recorded z adds the non-escaped iterations
+// of the escape block; a pixel that never escaped ends at ex = max_iter.
+extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8h_f32(const float* view, const int* size,
+                                                                        int2* out, CEK_HIDDEN) {
+  const long long w = cek_global_id();
+  const int W = size[0], max_iter = size[2];
+  const long long band_items = 4LL * W;
+  const long long band = w / band_items;
+  const int q = (int)(w - band * band_items);
+  const int blk = q >> 6, l = q & 63;
+  const int row = (int)band * 8 + (l >> 3), col = blk * 16 + (l & 7) * 2;
+  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
+  const float ci = y0 + row * dy;
+  const f32x2 cr = {x0 + col * dx, x0 + (col + 1) * dx}, civ = {ci, ci};
+  const f32x2 two = {2.f, 2.f};
+  f32x2 zr = {0.f, 0.f}, zi = {0.f, 0.f};
+  f32x2 fr = {0.f, 0.f}, fi = {0.f, 0.f};  // last z with |z|² <= 4 at a block boundary
+  int ex = 0, ey = 0;                      // its iteration
+  for (int it = 8; it <= max_iter; it += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const f32x2 zi2 = zi * zi;
+      const f32x2 tz = zr * zi;
+      zr = __builtin_elementwise_fma(zr, zr, cr) - zi2;
+      zi = __builtin_elementwise_fma(tz, two, civ);
+    }
+    const f32x2 m = __builtin_elementwise_fma(zr, zr, zi * zi);
+    const bool kx = m.x <= 4.f, ky = m.y <= 4.f;
+    if (kx) {
+      fr.x = zr.x;
+      fi.x = zi.x;
+      ex = it;
+    }
+    if (ky) {
+      fr.y = zr.y;
+      fi.y = zi.y;
+      ey = it;
+    }
+    if (!kx && !ky) break;
+  }
+  const f32x2 nbig = {-1048576.f, -1048576.f}, cbig = {4194304.f, 4194304.f};
+  f32x2 cnt = {0.f, 0.f};
+  zr = fr;
+  zi = fi;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const f32x2 zi2 = zi * zi;
+    const f32x2 m = __builtin_elementwise_fma(zr, zr, zi2);
+    cnt += pk_fma_clamp(m, nbig, cbig);
+    const f32x2 tz = zr * zi;
+    zr = __builtin_elementwise_fma(zr, zr, cr) - zi2;
+    zi = __builtin_elementwise_fma(tz, two, civ);
+  }
+  out[((long long)row * W + col) >> 1] =
+      make_int2(min(ex + (int)(cnt.x + 0.5f), max_iter), min(ey + (int)(cnt.y + 0.5f), max_iter));
+}

@@ -168,7 +168,7 @@ def test_gemm_wave_granularity_two_logical_devices():
     assert GemmBf16(256, 256, 64, devices=g0, tile="256x256pb").granularity() == 512  # < 1 wave: per tile
 
 
-@pytest.mark.parametrize("kernel", ["quad", "pool8", "pool16", "pk16", "pk32", "blk16", "blk64", "blk8", "blk8f", "blk8g", "blk16g"])
+@pytest.mark.parametrize("kernel", ["quad", "pool8", "pool16", "pk16", "pk32", "blk16", "blk64", "blk8", "blk8f", "blk8g", "blk16g", "blk8h"])
 def test_mandelbrot_event_pipeline_matches_numpy(kernel):
     from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
 
