@@ -302,17 +302,20 @@ def _mandelbrot_kernel_only(kernel: str = "blk8h", reps: int = 20) -> dict:
     m.render(1, pipeline=False)  # image downloaded once: its counts give the FLOPs
     flops = m.flops()
     m.out.write = False
-    for _ in range(3):
+    for _ in range(10):
         m.render(1, pipeline=False)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        m.render(1, pipeline=False)
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) * 1e3 / reps
+    runs = []
+    for _ in range(5):  # median of 5 runs of `reps` calls (clock settling)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            m.render(1, pipeline=False)
+        torch.cuda.synchronize()
+        runs.append((time.perf_counter() - t0) * 1e3 / reps)
+    ms = sorted(runs)[len(runs) // 2]
     m.cr.dispose()
     tf = flops / (ms * 1e-3) / 1e12
-    return {"kernel": m.kernel, "ms": round(ms, 4), "tflops": round(tf, 2),
+    return {"kernel": m.kernel, "ms": round(ms, 4), "ms_runs": [round(x, 4) for x in runs], "tflops": round(tf, 2),
             "pct_fp32_peak_157_3": round(100 * tf / 157.3, 1)}
 
 
