@@ -302,7 +302,7 @@ def _mandelbrot_kernel_only(kernel: str = "blk8h", reps: int = 20) -> dict:
     m.render(1, pipeline=False)  # image downloaded once: its counts give the FLOPs
     flops = m.flops()
     m.out.write = False
-    for _ in range(10):
+    for _ in range(100):  # ~15 ms: the clock settles (the first runs read 10 % slower)
         m.render(1, pipeline=False)
     runs = []
     for _ in range(5):  # median of 5 runs of `reps` calls (clock settling)
