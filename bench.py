@@ -379,12 +379,19 @@ def bench_node_configs(world: int) -> dict:
         # ranks on one device
         out["sgemm_host_resident_rccl"] = {"skipped": f"{world} ranks on {torch.cuda.device_count()} GPU(s); "
                                                       "RCCL needs one GPU per rank"}
+    t_start = time.monotonic()
     for name, cmd in configs:
+        # the extras share one time budget, so a hung config cannot push the
+        # whole run (headline included) past the driver's limit
+        left = NODE_CONFIGS_BUDGET_S - (time.monotonic() - t_start)
+        if left < 30:
+            out[name] = {"skipped": f"node-config time budget ({NODE_CONFIGS_BUDGET_S} s) spent"}
+            continue
         # own session: a timeout kills the whole process group (torchrun's ranks too)
         p = subprocess.Popen(cmd, cwd=os.path.join(ROOT, "bench"), env=env, stdout=subprocess.PIPE,
                              stderr=subprocess.PIPE, text=True, start_new_session=True)
         try:
-            so, se = p.communicate(timeout=180)
+            so, se = p.communicate(timeout=min(180, left))
             lines = [ln for ln in so.splitlines() if ln.startswith("{")]
             out[name] = json.loads(lines[-1]) if (p.returncode == 0 and lines) else {
                 "error": f"exit {p.returncode}: {(se or so)[-300:]}"}
@@ -399,6 +406,7 @@ def bench_node_configs(world: int) -> dict:
 
 
 MAX_REL_ERR = 5e-3
+NODE_CONFIGS_BUDGET_S = 360  # all of bench_node_configs' child processes together
 HOST_RESIDENT_BLOBS = 8
 HOST_RESIDENT_PANELS = 16
 
