@@ -960,5 +960,10 @@ CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128p, 4, 2, 4, 4, 1)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128pp, 4, 2, 4, 4, 2)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128ps, 4, 2, 4, 4, 3)
 // 128×128 tiles, 4 waves (2×2, 64×64 each), 64 KiB LDS, 2 blocks/CU.
+// 256×128 with four waves of 128×64 (one per SIMD): 96 KiB of fragment
+// reads per K-tile against 128 KiB for eight 64×64 waves, the layout
+// hipBLASLt picks for the 1024-row slice (MT256x128x64)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128w4, 2, 2, 8, 4, 0)
+CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128w4p, 2, 2, 8, 4, 1)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_128x128, 2, 2, 4, 4, 0)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_128x128p, 2, 2, 4, 4, 1)

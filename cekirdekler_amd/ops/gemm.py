@@ -31,6 +31,9 @@ TILES = {
     "256x128p": (256, 128, 512, "cek_sgemm_bf16_256x128p"),
     "256x128pp": (256, 128, 512, "cek_sgemm_bf16_256x128pp"),
     "256x128ps": (256, 128, 512, "cek_sgemm_bf16_256x128ps"),
+    # four waves of 128×64 (one per SIMD), fragments single / double-buffered
+    "256x128w4": (256, 128, 256, "cek_sgemm_bf16_256x128w4"),
+    "256x128w4p": (256, 128, 256, "cek_sgemm_bf16_256x128w4p"),
     "128x128": (128, 128, 256, "cek_sgemm_bf16_128x128"),
     "128x128p": (128, 128, 256, "cek_sgemm_bf16_128x128p"),
     # balanced-DMA ping-pong: G0 stages A, G1 stages Bt two K-tiles ahead
