@@ -33,7 +33,12 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
                                           char* smem, long long off, float* __restrict__ W = nullptr,
                                           int* __restrict__ tile_cnt = nullptr) {
   constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN, BK = 64;
-  constexpr int NWAVES = WM * WN, NT = 64 * NWAVES;
+  // MODE 8: two waves per output region (one per SIMD pair slot), each
+  // multiplying one 32-wide K half of every K-tile; summed through LDS at
+  // the end (an in-CU split-K: the four-wave layout's fragment traffic with
+  // two waves per SIMD to hide latency)
+  constexpr int NREG = WM * WN;
+  constexpr int NWAVES = (MODE == 8 || MODE == 9 ? 2 : 1) * NREG, NT = 64 * NWAVES;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   // MODE 0: one LDS stage in flight, all waves stage; MODE 1: + register
   // double-buffered fragments; MODE 2: ping-pong — the two halves of the
@@ -44,14 +49,14 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   // split — G0 stages the A tile during its read section, G1 stages the B
   // tile of the K-tile after next at the start of its MFMA section, so each
   // DMA has ~1.5 sections to land.
-  constexpr int STAGERS = (MODE >= 2 && MODE != 7) ? NWAVES / 2 : NWAVES;  // MODE 7: every wave stages
+  constexpr int STAGERS = (MODE >= 2 && MODE < 7) ? NWAVES / 2 : NWAVES;  // MODE 7-9: every wave stages
   constexpr int A_INSTR = A_BYTES / 1024 / STAGERS;
   constexpr int B_INSTR = B_BYTES / 1024 / STAGERS;
 
   const int M = dims[0], N = dims[1], K = dims[2], GM = dims[3] > 0 ? dims[3] : 1;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave / WN, wc = wave % WN;
+  const int wr = (wave % NREG) / WN, wc = (wave % NREG) % WN;
   // Split-K (SK): work-group u computes K-tiles [ks, ks + nk) of tile u / S;
   // the S work-groups of a tile are consecutive ids, so the XCD remap keeps
   // them on one XCD and the load balancer (granularity S·local) on one device.
@@ -79,7 +84,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
   // per-lane 32-bit byte offset + wave-uniform 64-bit base (saddr form)
   const unsigned lane_off = (unsigned)(lrow * K + lchunk * 8) * 2u;
-  const int sw = (MODE >= 2 && MODE != 7) ? wave % (NWAVES / 2) : wave;  // staging wave index
+  const int sw = (MODE >= 2 && MODE < 7) ? wave % (NWAVES / 2) : wave;  // staging wave index
   const char* a_wave = (const char*)(A + (size_t)(m0 + sw * A_INSTR * 8) * K);
   const char* b_wave = (const char*)(Bt + (size_t)(n0 + sw * B_INSTR * 8) * K);
 
@@ -156,6 +161,66 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
         __builtin_amdgcn_s_setprio(0);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else if constexpr (MODE == 8) {
+    const int s = wave / NREG;  // this wave's K half of every K-tile
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+      const char* base = smem + cur * STAGE;
+      bf16x8 a[FM], b[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else if constexpr (MODE == 9) {
+    // MODE 8 with a three-stage LDS ring: K-tile kt + 2 is issued while kt
+    // computes, and the barrier waits only for kt + 1 (the newest stage's
+    // A_INSTR + B_INSTR loads stay in flight)
+    const int s = wave / NREG;
+    constexpr int NEWEST = A_INSTR + B_INSTR;
+    stage(0, 0);
+    if (nk > 1) stage(1, 1);
+    if (nk > 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NEWEST) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt % 3;
+      const bool more = kt + 2 < nk;
+      if (more) stage((kt + 2) % 3, kt + 2);
+      const char* base = smem + cur * STAGE;
+      bf16x8 a[FM], b[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (more)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NEWEST) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
   } else if constexpr (MODE == 1) {
@@ -816,6 +881,24 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       }
     }
   }
+  if constexpr (MODE == 8 || MODE == 9) {
+    // the K-half-1 waves hand their partials to the K-half-0 waves of the
+    // same region through LDS (the loop ended on a barrier: LDS is free)
+    f32x4* red = reinterpret_cast<f32x4*>(smem);
+    const int reg = wave % NREG;
+    if (wave >= NREG) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) red[((reg * FM + i) * FN + j) * 64 + lane] = acc[i][j];
+    }
+    __syncthreads();
+    if (wave >= NREG) return;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] += red[((reg * FM + i) * FN + j) * 64 + lane];
+  }
   float* ct = C + (size_t)t * BM * BN;
   if constexpr (NOSTORE) {  // probe build: measures the epilogue's share
 #pragma unroll
@@ -965,5 +1048,18 @@ CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128ps, 4, 2, 4, 4, 3)
 // hipBLASLt picks for the 1024-row slice (MT256x128x64)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128w4, 2, 2, 8, 4, 0)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128w4p, 2, 2, 8, 4, 1)
+// the same four 128×64 regions, two waves each splitting every K-tile
+// (MODE 8, 512 threads); LDS: 96 KiB of stages, 128 KiB for the reduction
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x128k2(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 8 * 4 * 64 * 16];
+  gemm_tile<2, 2, 8, 4, 8>(dims, A, Bt, C, smem, __cek_off);
+}
+// same with a three-stage LDS ring (MODE 9): 144 KiB
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x128k3(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * (256 + 128) * 64 * 2];
+  gemm_tile<2, 2, 8, 4, 9>(dims, A, Bt, C, smem, __cek_off);
+}
 CEK_GEMM_KERNEL(cek_sgemm_bf16_128x128, 2, 2, 4, 4, 0)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_128x128p, 2, 2, 4, 4, 1)

@@ -34,6 +34,9 @@ TILES = {
     # four waves of 128×64 (one per SIMD), fragments single / double-buffered
     "256x128w4": (256, 128, 256, "cek_sgemm_bf16_256x128w4"),
     "256x128w4p": (256, 128, 256, "cek_sgemm_bf16_256x128w4p"),
+    # same regions, two waves per region each taking one K half of every K-tile (LDS-summed)
+    "256x128k2": (256, 128, 512, "cek_sgemm_bf16_256x128k2"),
+    "256x128k3": (256, 128, 512, "cek_sgemm_bf16_256x128k3"),  # same, three-stage LDS ring
     "128x128": (128, 128, 256, "cek_sgemm_bf16_128x128"),
     "128x128p": (128, 128, 256, "cek_sgemm_bf16_128x128p"),
     # balanced-DMA ping-pong: G0 stages A, G1 stages Bt two K-tiles ahead
