@@ -38,7 +38,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   // the end (an in-CU split-K: the four-wave layout's fragment traffic with
   // two waves per SIMD to hide latency)
   constexpr int NREG = WM * WN;
-  constexpr int NWAVES = (MODE == 8 || MODE == 9 ? 2 : 1) * NREG, NT = 64 * NWAVES;
+  constexpr int NWAVES = (MODE >= 8 ? 2 : 1) * NREG, NT = 64 * NWAVES;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   // MODE 0: one LDS stage in flight, all waves stage; MODE 1: + register
   // double-buffered fragments; MODE 2: ping-pong — the two halves of the
@@ -49,7 +49,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   // split — G0 stages the A tile during its read section, G1 stages the B
   // tile of the K-tile after next at the start of its MFMA section, so each
   // DMA has ~1.5 sections to land.
-  constexpr int STAGERS = (MODE >= 2 && MODE < 7) ? NWAVES / 2 : NWAVES;  // MODE 7-9: every wave stages
+  constexpr int STAGERS = ((MODE >= 2 && MODE < 7) || MODE == 10) ? NWAVES / 2 : NWAVES;  // MODE 7-9: every wave stages
   constexpr int A_INSTR = A_BYTES / 1024 / STAGERS;
   constexpr int B_INSTR = B_BYTES / 1024 / STAGERS;
 
@@ -84,7 +84,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
   // per-lane 32-bit byte offset + wave-uniform 64-bit base (saddr form)
   const unsigned lane_off = (unsigned)(lrow * K + lchunk * 8) * 2u;
-  const int sw = (MODE >= 2 && MODE < 7) ? wave % (NWAVES / 2) : wave;  // staging wave index
+  const int sw = ((MODE >= 2 && MODE < 7) || MODE == 10) ? wave % (NWAVES / 2) : wave;  // staging wave index
   const char* a_wave = (const char*)(A + (size_t)(m0 + sw * A_INSTR * 8) * K);
   const char* b_wave = (const char*)(Bt + (size_t)(n0 + sw * B_INSTR * 8) * K);
 
@@ -187,6 +187,45 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
+  } else if constexpr (MODE == 10) {
+    // MODE 2's ping-pong on the in-CU split-K: G0 (waves < NREG) multiplies
+    // K half 0 of every K-tile and G1 K half 1 of the same regions, so one
+    // group reads its half's fragments while the other multiplies; G0
+    // stages each next K-tile during its read section.  Same barrier
+    // sequence as MODE 2.
+    const bool g1 = wave >= NREG;
+    const int s = g1 ? 1 : 0;
+    bf16x8 fa[FM], fb[FN];
+    auto bar = [] {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    if (!g1) stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (g1) bar();  // stagger G1 by one section
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* base = smem + (kt & 1) * STAGE;
+      if (!g1 && kt + 1 < nk) stage((kt + 1) & 1, kt + 1);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bar();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (!g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+    }
+    if (!g1) bar();  // equal barrier counts for both groups
+    __syncthreads();  // both groups done with LDS before the reduction reuses it
   } else if constexpr (MODE == 9) {
     // MODE 8 with a three-stage LDS ring: K-tile kt + 2 is issued while kt
     // computes, and the barrier waits only for kt + 1 (the newest stage's
@@ -881,7 +920,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       }
     }
   }
-  if constexpr (MODE == 8 || MODE == 9) {
+  if constexpr (MODE >= 8) {
     // the K-half-1 waves hand their partials to the K-half-0 waves of the
     // same region through LDS (the loop ended on a barrier: LDS is free)
     f32x4* red = reinterpret_cast<f32x4*>(smem);
@@ -1054,6 +1093,12 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x128k2(
     const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
   __shared__ __attribute__((aligned(16))) char smem[4 * 8 * 4 * 64 * 16];
   gemm_tile<2, 2, 8, 4, 8>(dims, A, Bt, C, smem, __cek_off);
+}
+// ping-pong on the in-CU split-K (MODE 10): 128 KiB (96 of stages)
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x128kp(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 8 * 4 * 64 * 16];
+  gemm_tile<2, 2, 8, 4, 10>(dims, A, Bt, C, smem, __cek_off);
 }
 // same with a three-stage LDS ring (MODE 9): 144 KiB
 extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x128k3(

@@ -37,6 +37,7 @@ TILES = {
     # same regions, two waves per region each taking one K half of every K-tile (LDS-summed)
     "256x128k2": (256, 128, 512, "cek_sgemm_bf16_256x128k2"),
     "256x128k3": (256, 128, 512, "cek_sgemm_bf16_256x128k3"),  # same, three-stage LDS ring
+    "256x128kp": (256, 128, 512, "cek_sgemm_bf16_256x128kp"),  # same split, ping-pong groups
     "128x128": (128, 128, 256, "cek_sgemm_bf16_128x128"),
     "128x128p": (128, 128, 256, "cek_sgemm_bf16_128x128p"),
     # balanced-DMA ping-pong: G0 stages A, G1 stages Bt two K-tiles ahead

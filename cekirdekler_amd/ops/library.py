@@ -17,7 +17,7 @@ LIBRARY = {
     "sgemm_bf16": ["cek_sgemm_bf16_256x256", "cek_sgemm_bf16_256x256p", "cek_sgemm_bf16_256x256pp", "cek_sgemm_bf16_256x256ps",
                    "cek_sgemm_bf16_256x128", "cek_sgemm_bf16_256x128p", "cek_sgemm_bf16_256x128pp", "cek_sgemm_bf16_256x128ps",
                    "cek_sgemm_bf16_128x128", "cek_sgemm_bf16_128x128p",
-                   "cek_sgemm_bf16_256x256pp_sk", "cek_sgemm_bf16_256x128pp_sk", "cek_sgemm_bf16_256x256pb_sk", "cek_sgemm_bf16_256x256pb_sx", "cek_sgemm_bf16_256x256pb_sy", "cek_sgemm_bf16_256x256pb_sa", "cek_sgemm_bf16_256x256pb_sz", "cek_sgemm_bf16_256x128w4", "cek_sgemm_bf16_256x128w4p", "cek_sgemm_bf16_256x128k2", "cek_sgemm_bf16_256x128k3",
+                   "cek_sgemm_bf16_256x256pp_sk", "cek_sgemm_bf16_256x128pp_sk", "cek_sgemm_bf16_256x256pb_sk", "cek_sgemm_bf16_256x256pb_sx", "cek_sgemm_bf16_256x256pb_sy", "cek_sgemm_bf16_256x256pb_sa", "cek_sgemm_bf16_256x256pb_sz", "cek_sgemm_bf16_256x128w4", "cek_sgemm_bf16_256x128w4p", "cek_sgemm_bf16_256x128k2", "cek_sgemm_bf16_256x128k3", "cek_sgemm_bf16_256x128kp",
                    "cek_sgemm_bf16_256x256pb_sy_nostore", "cek_sgemm_bf16_256x256pb_sy_noxch", "cek_sgemm_bf16_256x256pb_syn",
                    "cek_sgemm_bf16_256x256pbn", "cek_sgemm_bf16_256x256i", "cek_sgemm_bf16_256x128i",
                    "cek_sgemm_bf16_256x256pp_nostore", "cek_sgemm_bf16_256x256pb", "cek_sgemm_bf16_256x128pb",
