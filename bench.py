@@ -374,7 +374,10 @@ def bench_node_configs(world: int) -> dict:
             "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "rccl_gemm.py"]
     import torch
 
-    configs = [("nbody_pipeline", [sys.executable, "nbody_pipeline.py", "--gpus", str(world), "--pushes", "14"]),
+    # config 4 is specified on 4 GPUs (2 + 1 + 1 placement); on fewer GPUs the
+    # same placement is rehearsed on 4 logical devices of GPU 0
+    nb_args = ["--gpus", str(min(world, 4))] if world >= 4 else ["--gpus", "4", "--logical", "4"]
+    configs = [("nbody_pipeline", [sys.executable, "nbody_pipeline.py", *nb_args, "--pushes", "14"]),
                ("task_pool", [sys.executable, "task_pool.py", "--gpus", str(world)]),
                ("saxpy_1m_cpu", [sys.executable, "saxpy_cpu.py"]),
                ("wave_cpu_gpu", [sys.executable, "wave_cpu_gpu.py"])]
@@ -415,6 +418,16 @@ MAX_REL_ERR = 5e-3
 NODE_CONFIGS_BUDGET_S = 360  # all of bench_node_configs' child processes together
 HOST_RESIDENT_BLOBS = 8
 HOST_RESIDENT_PANELS = 16
+
+
+def _peer_topology(world: int) -> dict:
+    """hipDeviceCanAccessPeer among this job's GPUs (query only) and the
+    device-to-device path the runtime takes between them."""
+    from cekirdekler_amd._native import cek
+
+    full = cek.can_access_peer_matrix()
+    m = [row[:world] for row in full[:world]]
+    return {"gpus_visible": len(full), "job_gpus": world, "can_access_peer": m, "path": cek.peer_path(m)}
 
 
 def _free_port() -> int:
@@ -476,6 +489,7 @@ def main(argv=None) -> int:
         dist.barrier()
         dist.destroy_process_group()  # the other ranks exit here; rank 0 goes on alone
     node = {} if (ctx.rank != 0 or args.skip_node_configs or not use_gpu) else bench_node_configs(ctx.world)
+    peers = _peer_topology(ctx.world) if (ctx.rank == 0 and use_gpu) else {}
     ok = sg["max_rel_err"] <= MAX_REL_ERR and sg["spin_timeouts"] == 0
     if ctx.rank == 0:
         size = args.size if use_gpu else min(args.size, 512)
@@ -521,6 +535,7 @@ def main(argv=None) -> int:
                 "saxpy_1m_cpu": node.get("saxpy_1m_cpu"),
                 "wave_cpu_gpu": node.get("wave_cpu_gpu"),
                 "sgemm_host_resident_rccl": node.get("sgemm_host_resident_rccl"),
+                "peer_topology": peers,
             },
         }
         print(json.dumps(out), flush=True)

@@ -18,11 +18,15 @@ every push advances one system by one step through all three stages.  The
 first stepped system is checked against a float64 host step on sampled
 bodies.
 
-Placement: with 3 or more GPUs the stages run on distinct GPUs (force on
-all but two, kick and energy on one each); with fewer, round-robin.  Stage
-times are device times from hipEvent timelines (``record_timeline``), so
-``overlap`` compares what the stages cost on their devices with the push
-wall time.  Kernels are user kernel strings JIT-compiled by hiprtc.
+Placement (BASELINE config 4: 4 GPUs): with 3 or more GPUs the stages run
+on distinct GPUs (force on all but two, kick and energy on one each: 2 + 1
++ 1 on four); with fewer, round-robin.  ``--logical 4`` rehearses the
+four-GPU placement on one GPU (four logical devices of GPU 0).  Stage times
+are device times from hipEvent timelines; the stage-transition copies are
+timed by hipEvents on the copy engine's streams, and both are put on one
+host-anchored clock, so ``copy_overlap`` measures how much of the transfer
+time ran while the force stage was computing (1.0 = fully hidden).  Kernels
+are user kernel strings JIT-compiled by hiprtc.
 """
 import argparse
 import time
@@ -165,8 +169,7 @@ s3.outputs[2].elements_per_group = 1
 s1.prepend_to_stage(s2)
 s2.prepend_to_stage(s3)
 pipe = s1.make_pipeline()
-for s in (s1, s2, s3):
-    s.cruncher.record_timeline = True
+pipe.record_timeline = True
 S = 3
 L = 2 * S                 # a push's data leaves the pipeline L pushes later
 M = L + 1                 # systems in rotation
@@ -211,19 +214,24 @@ steady = times[L:] if len(times) > L + 1 else times[2:]
 ms = float(np.median(steady))
 
 
-def stage_device_ms(stage, pushes):
-    """Median per-push kernel time of a stage: each push is one compute per
+tl = pipe.timeline()
+
+
+def stage_device_ms(i):
+    """Median per-push kernel time of stage i: each push is one compute per
     device; a push costs the stage its slowest device's span."""
-    spans = stage.cruncher.timeline()
     per_dev = {}
-    for sp in spans:
-        per_dev.setdefault(sp["device"], []).append(sp["end_ms"] - sp["begin_ms"])
-    rows = [max(v[i] for v in per_dev.values() if i < len(v)) for i in range(min(len(v) for v in per_dev.values()))]
+    for st, d, b, e in tl["kernels"]:
+        if st == i:
+            per_dev.setdefault(d, []).append(e - b)
+    rows = [max(v[k] for v in per_dev.values()) for k in range(min(len(v) for v in per_dev.values()))]
     rows = rows[-len(steady):] if len(rows) > len(steady) else rows
     return float(np.median(rows))
 
 
-stage_ms = [stage_device_ms(s, a.pushes) for s in (s1, s2, s3)]
+stage_ms = [stage_device_ms(i) for i in range(3)]
+ov_force = pipe.copy_overlap(tl, stage=0)
+ov_any = pipe.copy_overlap(tl)
 xfer = pipe.transfer_stats()
 emit({"config": "nbody_pipeline_3stage", "n": n, "systems_in_flight": M, "gpus_used": ng,
       "stage_gpus": [len(d) if hasattr(d, "__len__") else 1 for d in devs], "push_ms_median": ms,
@@ -232,6 +240,12 @@ emit({"config": "nbody_pipeline_3stage", "n": n, "systems_in_flight": M, "gpus_u
       "force_stage_pct_fp32_peak": 100 * 20 * n * n / (stage_ms[0] * 1e-3) / 1e12 / FP32_PEAK_TFLOPS / len(devs[0]),
       "overlap_efficiency": max(stage_ms) / ms, "serial_over_push": sum(stage_ms) / ms,
       "steps_per_system": steps, "step_check_max_rel_err": check,
+      "logical_rehearsal": a.logical > 1, "placement": [[d.device(k).name + f"#{d.device(k).info.ordinal}"
+                                                           for k in range(len(d))] for d in devs],
+      "copy_ms_per_push": ov_any["copy_ms"] / a.pushes,
+      "copy_overlap": {"with_force_stage": round(ov_force["fraction"], 4),
+                       "with_any_stage": round(ov_any["fraction"], 4),
+                       "copy_ms_total": round(ov_any["copy_ms"], 3), "copies": len(tl["copies"])},
       "transfer_bytes": xfer, "kinetic_energy_system0": kinetic.get(0, [])})
 pipe.dispose()
 if check is None or not check < 1e-3:

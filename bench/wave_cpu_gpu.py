@@ -5,7 +5,10 @@ than CPU-only (Kamera.cs:266, devices from devicesAmd(true, true)).
 Frames per second of WaveSurface.update() (one compute per frame, the
 displaced vertices downloaded every frame, as the Unity loop uses them) on
 the CPU device alone, the GPU alone, and GPU + CPU with the load balancer
-splitting the vertices.  Steady state after the balancer has converged."""
+splitting the vertices.  Steady state after the balancer has converged.
+``gpu+cpu_fit`` is the same pair with the opt-in overhead-aware balancer
+(``overhead_aware_balancer``: t = a + b·range per device), which may leave
+the CPU out when its share does not pay for the second device's fixed cost."""
 import argparse
 import time
 
@@ -26,10 +29,12 @@ cpu, gpus = plats.cpus(True), plats.gpus()
 base, normals = grid_mesh(a.nx, a.ny)
 configs = [("cpu", cpu)]
 if len(gpus):
-    configs += [("gpu", gpus[0]), ("gpu+cpu", gpus[0] + cpu)]
+    configs += [("gpu", gpus[0]), ("gpu+cpu", gpus[0] + cpu), ("gpu+cpu_fit", gpus[0] + cpu)]
 out = {"config": "wave_cpu_gpu", "vertices": len(base), "local": 64}
 for name, devs in configs:
     w = WaveSurface(base, normals, devices=devs)
+    if name.endswith("_fit"):
+        w.cr.overhead_aware_balancer = True
     for _ in range(40):  # balancer converges, buffers resident
         w.update()
     t = time.perf_counter()
@@ -39,10 +44,14 @@ for name, devs in configs:
     err = float(np.abs(w.update()["z"] - w.reference()["z"]).max())
     out[f"{name}_ms_per_frame"] = ms
     out[f"{name}_max_abs_err"] = err
-    if name == "gpu+cpu":
-        out["gpu+cpu_shares"] = [r / sum(w.cr.ranges(1)) for r in w.cr.ranges(1)]
+    if name.startswith("gpu+cpu"):
+        out[f"{name}_shares"] = [r / sum(w.cr.ranges(1)) for r in w.cr.ranges(1)]
+    if name.endswith("_fit"):
+        out[f"{name}_predictor"] = {k: v for k, v in w.cr.balancer_predictor_info(1).items()}
     w.cr.dispose()
 if "gpu+cpu_ms_per_frame" in out:
     out["speedup_gpu+cpu_over_cpu"] = out["cpu_ms_per_frame"] / out["gpu+cpu_ms_per_frame"]
     out["speedup_gpu_over_cpu"] = out["cpu_ms_per_frame"] / out["gpu_ms_per_frame"]
+    out["speedup_gpu+cpu_fit_over_cpu"] = out["cpu_ms_per_frame"] / out["gpu+cpu_fit_ms_per_frame"]
+    out["fit_not_slower_than_gpu_alone"] = out["gpu+cpu_fit_ms_per_frame"] <= 1.02 * out["gpu_ms_per_frame"]
 emit(out)

@@ -252,6 +252,10 @@ class ClArray:
         # as reduction partials); the slice of a device is then
         # [ref/L·N, (ref+r)/L·N)
         self.elements_per_group = 0
+        # extension: keep-resident gather — after the
+        # kernels every device's slice of this array is copied into every
+        # other device's replica (GPU↔GPU over xGMI, RCCL across ranks)
+        self.gather_resident = False
         self._registered = False
         self._disposed = False
 
@@ -484,19 +488,33 @@ class ClArray:
     def alignmentBytes(self) -> int:  # noqa: N802
         return self.alignment_bytes
 
+    @property
+    def gather(self) -> bool:
+        """Alias of :attr:`gather_resident` (the ``gather`` readWrite token)."""
+        return self.gather_resident
+
+    @gather.setter
+    def gather(self, v: bool) -> None:
+        self.gather_resident = bool(v)
+
+    gatherResident = gather
+
     # ------------------------------------------------------------ native spec
-    def _spec(self):
+    def _spec(self, pin: bool = False):
+        """``pin``: register wrapped host memory of any size (a compute
+        captured into a graph replays its copies against the captured pages,
+        which must be pinned)."""
         # The native spec is cached per (storage uid, flags): the uid changes
         # whenever the host storage does, so the pointer inside stays valid.
         key = (self._uid, self._read, self._partial, self._write, self._write_all, self._ro, self._wo,
-               self.zero_copy, self.elements_per_work_item, self.elements_per_group)
+               self.zero_copy, self.elements_per_work_item, self.elements_per_group, self.gather_resident, pin)
         cached = getattr(self, "_spec_cache", None)
         if cached is not None and cached[0] == key:
             return cached[1]
         arr = self.array
         moves = self._read or self._partial or self._write or self._write_all
         if self._fast is None and not self._registered and (
-                self.zero_copy or (moves and arr.nbytes >= ClArray.auto_pin_min_bytes > 0)):
+                self.zero_copy or (moves and (pin or arr.nbytes >= ClArray.auto_pin_min_bytes > 0))):
             # Page-lock wrapped host memory on first use (the reference pins
             # every array for each compute, Cores.cs:535-541): a copy from
             # pageable memory is staged by the runtime and a D2H blocks the
@@ -511,7 +529,7 @@ class ClArray:
         spec = cek.ArraySpec(self._uid, arr.ctypes.data, arr.nbytes, arr.itemsize,
                              self._read, self._partial, self._write, self._write_all,
                              self._ro, self._wo, zc, int(self.elements_per_work_item),
-                             int(self.elements_per_group))
+                             int(self.elements_per_group), bool(self.gather_resident))
         self._spec_cache = (key, spec)
         return spec
 

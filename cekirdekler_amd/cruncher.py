@@ -425,10 +425,12 @@ class ClNumberCruncher:
         """Kernel spans recorded while ``record_timeline`` was on: one dict per
         compute per device (``device``, ``compute_id``, ``begin_ms``,
         ``end_ms``), timed by hipEvents on the stream the kernels ran on and
-        relative to that device's first span.  Waits for the recorded work and
-        clears the list."""
-        return [{"device": d, "compute_id": cid, "begin_ms": b, "end_ms": e}
-                for d, cid, b, e in self._cores.timeline()]
+        relative to that device's first span; ``abs_begin_ms``/``abs_end_ms``
+        put every device on the host clock (each GPU's event clock anchored
+        once), so spans of different GPUs can be compared.  Waits for the
+        recorded work and clears the list."""
+        return [{"device": d, "compute_id": cid, "begin_ms": b, "end_ms": e, "abs_begin_ms": ab, "abs_end_ms": ae}
+                for d, cid, b, e, ab, ae in self._cores.timeline()]
 
     def last_record(self) -> dict:
         """Structured record of the last compute (observability)."""
@@ -436,7 +438,22 @@ class ClNumberCruncher:
         return {"compute_id": r.compute_id, "wall_ms": r.wall_ms, "ranges": list(r.ranges),
                 "references": list(r.references), "device_ms": list(r.device_ms),
                 "h2d_bytes": r.h2d_bytes, "d2h_bytes": r.d2h_bytes, "p2p_bytes": r.p2p_bytes,
+                "gather_bytes": r.gather_bytes, "staged_bytes": r.staged_bytes, "p2p_path": r.p2p_path,
                 "pipelined": r.pipelined}
+
+    # ------------------------------------------------------------ peer topology
+    def peer_topology(self) -> dict:
+        """The device set's GPU-to-GPU links: the
+        distinct GPU ordinals, ``hipDeviceCanAccessPeer`` among them (peer
+        access is enabled at construction when they span two or more GPUs)
+        and the resulting path — ``none`` (one GPU), ``xgmi`` (every pair
+        peers) or ``staged`` (some pair cannot; the read fan-out then uploads
+        over PCIe per device)."""
+        if self._cores is None:
+            return {"ordinals": [], "matrix": [], "path": "none"}
+        return {"ordinals": list(self._cores.peer_ordinals),
+                "matrix": [list(r) for r in self._cores.peer_matrix],
+                "path": self._cores.p2p_path}
 
     # ------------------------------------------------------------ compute graphs
     def capture(self) -> "ComputeGraph":
@@ -545,7 +562,8 @@ class ClNumberCruncher:
         call.kernels = names
         call.repeats = max(1, int(self.repeat_count))
         call.repeat_kernel = self.repeat_kernel_name if self.repeat_count > 1 else ""
-        call.arrays = specs if specs is not None else [a._spec() for a in group.arrays]
+        pin = bool(self._cores is not None and self._cores.capturing)
+        call.arrays = specs if specs is not None else [a._spec(pin=pin) for a in group.arrays]
         call.global_range = G
         call.local_range = L
         call.global_offset = int(global_offset)
@@ -588,6 +606,32 @@ class ClNumberCruncher:
         heterogeneity for load-balancer convergence measurements)."""
         self._cores.set_time_scale(device, float(scale))
 
+    def set_time_offset(self, device: int, ms: float) -> None:
+        """Test/bench hook: a fixed cost of ``ms`` host milliseconds per
+        compute on a device (spent before its work, counted in its time)."""
+        self._cores.set_time_offset(device, float(ms))
+
+    @property
+    def overhead_aware_balancer(self) -> bool:
+        """Opt-in balancing that models each device's time as fixed cost +
+        per-item cost (t = a + b·range, fitted from this compute id's
+        history) instead of the reference's proportional law, and leaves a
+        device out when its share would not pay for its fixed cost — so
+        adding a device never makes a compute slower (the predictor slot
+        the reference stubs out, HelperFunctions.cs:163-178).  The exact law
+        stays the default; single-process crunchers only."""
+        return bool(self._cores.balancer_predictor) if self._cores else False
+
+    @overhead_aware_balancer.setter
+    def overhead_aware_balancer(self, on: bool) -> None:
+        self._cores.balancer_predictor = bool(on)
+
+    def balancer_predictor_info(self, compute_id: int) -> dict:
+        """The predictor's last decision for a compute id (``law`` while it
+        gathers samples, ``multi``, ``single`` or ``probe``), its fits and
+        the measured multi-/single-device overheads."""
+        return dict(self._cores.predictor_info(int(compute_id)))
+
     # ------------------------------------------------------------ lifecycle
     def dispose(self) -> None:
         if self._cores is not None:
@@ -611,6 +655,7 @@ class Cores:
     """Reference "usage type 2" API: ``Cores(types, src, names, ...)`` then
     ``compute(names, repeats, syncKernel, arrays, readWrite, epw, G, id, ...)``
     with the readWrite token strings ``partial read write all ro wo zc``
+    (plus the extension token ``gather``: keep-resident all-gather)
     (ClArray.cs:611-629, Cores.cs:471)."""
 
     def __init__(self, device_types, kernel_source: str, kernel_names=None, default_queue: bool = False,
@@ -639,6 +684,7 @@ class Cores:
             a._read = "read" in toks
             a._write = "write" in toks
             a._write_all = "all" in toks
+            a.gather_resident = "gather" in toks
             a._ro = "ro" in toks
             a._wo = "wo" in toks
             a.zero_copy = "zc" in toks
@@ -690,11 +736,15 @@ class ComputeGraph:
         return self
 
     def __exit__(self, exc_type, exc, tb) -> None:
-        gid = self.cruncher.cores.capture_end()
-        if exc_type is None:
-            self.id = gid
-        else:
-            self.cruncher.cores.graph_destroy(gid)
+        if exc_type is not None:
+            # the body failed: end the capture, but never let a capture error
+            # replace the user's exception
+            try:
+                self.cruncher.cores.graph_destroy(self.cruncher.cores.capture_end())
+            except Exception:
+                pass
+            return
+        self.id = self.cruncher.cores.capture_end()
 
     def replay(self, times: int = 1, sync: bool = True) -> None:
         if self.id is None:

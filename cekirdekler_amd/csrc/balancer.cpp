@@ -1,6 +1,7 @@
 #include "balancer.h"
 
 #include <algorithm>
+#include <cmath>
 #include <numeric>
 
 namespace cek {
@@ -65,6 +66,139 @@ void load_balance(const std::vector<double>& bench, bool smooth,
   auto sum = [&]() { return std::accumulate(ranges.begin(), ranges.end(), 0LL); };
   while (sum() > total) ranges[argmax(ranges)] -= step;
   while (sum() < total) ranges[argmax(ranges)] += step;
+}
+
+static void quantize_fix(std::vector<long long>& ranges, const std::vector<double>& target, long long total,
+                         long long step) {
+  const size_t n = ranges.size();
+  for (size_t i = 0; i < n; ++i) {
+    long long t = static_cast<long long>(std::max(0.0, target[i]));
+    long long rem = t % step;
+    ranges[i] = rem < step / 2 ? t - rem : t + (step - rem);
+  }
+  auto sum = [&]() { return std::accumulate(ranges.begin(), ranges.end(), 0LL); };
+  while (sum() > total) ranges[argmax(ranges)] -= step;
+  while (sum() < total) ranges[argmax(ranges)] += step;
+}
+
+bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_ms, long long total,
+                   std::vector<long long>& ranges, long long step) {
+  const size_t n = ranges.size();
+  if (n == 0) return false;
+  if (step <= 0) step = 1;
+  if (fs.samples.size() != n) fs.samples.assign(n, {});
+  // 1) record this compute: a sample per computing device, keyed by range
+  //    (a repeated range refreshes its time: an EWMA, so old noise fades)
+  int active = 0;
+  double tmax = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (ranges[i] <= 0 || i >= bench.size() || bench[i] <= 0) continue;
+    ++active;
+    tmax = std::max(tmax, bench[i]);
+    auto& v = fs.samples[i];
+    const double r = static_cast<double>(ranges[i]);
+    auto it = std::find_if(v.begin(), v.end(), [&](const std::pair<double, double>& p) {
+      return std::abs(p.first - r) <= 0.01 * r;
+    });
+    if (it != v.end()) {
+      it->second = 0.5 * it->second + 0.5 * bench[i];
+    } else {
+      v.emplace_back(r, bench[i]);
+      if (static_cast<int>(v.size()) > kFitSamples) v.erase(v.begin());
+    }
+  }
+  if (active > 0 && wall_ms > 0) {
+    const double ov = std::max(0.0, wall_ms - tmax);
+    double& o = active >= 2 ? fs.o_multi : fs.o_single;
+    o = o < 0 ? ov : 0.7 * o + 0.3 * ov;
+  }
+  // 2) fits t = a + b·r (least squares over distinct ranges)
+  fs.a.assign(n, 0.0);
+  fs.b.assign(n, 0.0);
+  for (size_t i = 0; i < n; ++i) {
+    const auto& v = fs.samples[i];
+    if (v.size() < 2) {
+      fs.decision = "law";
+      return false;
+    }
+    double sx = 0, sy = 0, sxx = 0, sxy = 0;
+    for (auto& p : v) {
+      sx += p.first;
+      sy += p.second;
+      sxx += p.first * p.first;
+      sxy += p.first * p.second;
+    }
+    const double k = static_cast<double>(v.size());
+    const double den = k * sxx - sx * sx;
+    if (den <= 0) {
+      fs.decision = "law";
+      return false;
+    }
+    double b = (k * sxy - sx * sy) / den;
+    double a = (sy - b * sx) / k;
+    if (b <= 0) {  // flat or noisy: all fixed cost, a tiny slope keeps the split defined
+      a = sy / k;
+      b = 1e-9 * std::max(a, 1e-6);
+    }
+    if (a < 0) {  // proportional: refit through the origin
+      a = 0;
+      b = sxy / sxx;
+    }
+    fs.a[i] = a;
+    fs.b[i] = b;
+  }
+  // 3) water-filling: equal predicted finish time T over the devices kept
+  std::vector<char> keep(n, 1);
+  double T = 0;
+  for (;;) {
+    double inv = 0, ab = 0;
+    for (size_t i = 0; i < n; ++i)
+      if (keep[i]) {
+        inv += 1.0 / fs.b[i];
+        ab += fs.a[i] / fs.b[i];
+      }
+    T = (static_cast<double>(total) + ab) / inv;
+    // drop the device with the largest fixed cost whose share is under a step
+    int drop = -1;
+    for (size_t i = 0; i < n; ++i)
+      if (keep[i] && (T - fs.a[i]) / fs.b[i] < static_cast<double>(step) &&
+          (drop < 0 || fs.a[i] > fs.a[drop]))
+        drop = static_cast<int>(i);
+    if (drop < 0) break;
+    keep[drop] = 0;
+  }
+  int kept = 0;
+  for (char c : keep) kept += c;
+  size_t best = 0;  // the best single device
+  for (size_t i = 1; i < n; ++i)
+    if (fs.a[i] + fs.b[i] * total < fs.a[best] + fs.b[best] * total) best = i;
+  const double single_dev = fs.a[best] + fs.b[best] * static_cast<double>(total);
+  std::vector<double> target(n, 0.0);
+  bool single = kept < 2;
+  if (!single) {
+    const double om = fs.o_multi >= 0 ? fs.o_multi : 0.0;
+    if (fs.o_single < 0) {
+      // the single-device overhead is unknown: probe it once when it could win
+      if (!fs.probed && single_dev <= 1.25 * (T + om)) {
+        fs.probed = true;
+        fs.probe_left = 3;
+      }
+      single = fs.probe_left > 0;
+    } else {
+      single = single_dev + fs.o_single <= T + om;
+    }
+  }
+  if (fs.probe_left > 0) --fs.probe_left;
+  if (single) {
+    target[best] = static_cast<double>(total);
+    fs.decision = fs.o_single < 0 ? "probe" : "single";
+  } else {
+    for (size_t i = 0; i < n; ++i)
+      if (keep[i]) target[i] = (T - fs.a[i]) / fs.b[i];
+    fs.decision = "multi";
+  }
+  quantize_fix(ranges, target, total, step);
+  return true;
 }
 
 void initial_split(int devices, bool smooth, std::vector<std::vector<double>>& history,

@@ -6,9 +6,38 @@
 // exchanged timings.
 #pragma once
 #include <cstdint>
+#include <string>
 #include <vector>
 
 namespace cek {
+
+// Opt-in overhead-aware predictor, in the slot the reference left for one
+// (HelperFunctions.cs:163-178: PID / derivative predictors that return null).
+// The reference law assumes time ∝ range, so a device with a large fixed
+// cost per compute (launch + sync latency, host-thread fan-out) keeps a share
+// that makes the compute slower than leaving it out.  The predictor fits
+// t_i = a_i + b_i·r_i per device from the (range, time) samples of this
+// compute id, splits by water-filling (equal predicted finish time; a device
+// whose best share is below one step gets none), and compares that split with
+// the best single device using the measured per-compute overhead of multi- and
+// single-device computes (wall time − slowest device), probing the single
+// device once to learn it.  Until every device has a fit it defers to the law.
+struct FitState {
+  std::vector<std::vector<std::pair<double, double>>> samples;  // per device: (range, ms), distinct ranges
+  double o_multi = -1, o_single = -1;  // EWMA of wall − max device ms (−1: not measured)
+  int probe_left = 0;                  // computes left in a single-device probe
+  bool probed = false;
+  std::string decision = "law";        // law | multi | single | probe
+  std::vector<double> a, b;            // last fits (ms, ms per work item)
+};
+
+constexpr int kFitSamples = 8;
+
+// Records the last compute of this id (its ranges, per-device ms and wall ms)
+// and, when every device has a fit, writes the next split into `ranges`
+// (returns true); false = apply the reference law instead.
+bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_ms, long long total,
+                   std::vector<long long>& ranges, long long step);
 
 struct BalancerState {
   std::vector<long long> ranges;      // work-items per device
@@ -19,6 +48,8 @@ struct BalancerState {
   long long global_range = 0;
   long long local_range = 0;
   long long global_offset = 0;
+  double last_wall_ms = 0;  // wall time of the last compute of this id
+  FitState fit;             // overhead-aware predictor (opt-in)
 };
 
 constexpr int kHistoryDepth = 10;     // Cores.cs:1065 performanceHistoryDepth

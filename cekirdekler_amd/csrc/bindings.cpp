@@ -71,6 +71,25 @@ PYBIND11_MODULE(_cek, m) {
   m.def("gpu_info", &gpu_info);
   m.def("cpu_info", &cpu_info, py::arg("threads") = -1);
   m.def("enable_peer_access", &enable_peer_access);
+  m.def("enable_peer_access_among", &enable_peer_access_among, py::arg("ordinals"));
+  m.def("peer_path", &peer_path, py::arg("matrix"));
+  // query only (no context is created, nothing is enabled): hipDeviceCanAccessPeer
+  // between every pair of visible GPUs
+  m.def("can_access_peer_matrix", []() {
+    const int n = gpu_count();
+    std::vector<std::vector<int>> m(n, std::vector<int>(n, 1));
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        if (i == j) continue;
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, i, j) != hipSuccess) {
+          (void)hipGetLastError();
+          can = 0;
+        }
+        m[i][j] = can;
+      }
+    return m;
+  });
 
   py::class_<KernelSig>(m, "KernelSig")
       .def_readonly("name", &KernelSig::name)
@@ -116,7 +135,26 @@ PYBIND11_MODULE(_cek, m) {
       .def_readonly("h2d_bytes", &CopyEngine::h2d_bytes)
       .def_readonly("d2h_bytes", &CopyEngine::d2h_bytes)
       .def_readonly("host_bytes", &CopyEngine::host_bytes)
-      .def_readonly("copies", &CopyEngine::copies);
+      .def_readonly("copies", &CopyEngine::copies)
+      .def_readwrite("record_timeline", &CopyEngine::record_timeline)
+      .def("timeline", [](CopyEngine& e) {
+        std::vector<CopyEngine::Span> spans;
+        {
+          py::gil_scoped_release nogil;
+          spans = e.timeline();
+        }
+        py::list out;
+        for (auto& s : spans) {
+          py::dict d;
+          d["device"] = s.ordinal;
+          d["kind"] = s.kind;
+          d["bytes"] = s.bytes;
+          d["abs_begin_ms"] = s.abs_begin_ms;
+          d["abs_end_ms"] = s.abs_end_ms;
+          out.append(d);
+        }
+        return out;
+      });
   m.def("device_synchronize", [](int ordinal) {
     py::gil_scoped_release r;
     if (gpu_count() == 0) return;
@@ -133,6 +171,20 @@ PYBIND11_MODULE(_cek, m) {
     load_balance(bench, smooth, history, total, ranges, step);
     return py::make_tuple(ranges, history);
   });
+  m.def("predict_split", [](std::vector<double> bench, double wall, long long total, std::vector<long long> ranges,
+                            long long step, py::object state) {
+    // pure form for tests: `state` is an opaque capsule from new_fit_state()
+    auto* fs = state.cast<FitState*>();
+    bool ok = predict_split(*fs, bench, wall, total, ranges, step);
+    return py::make_tuple(ok, ranges, fs->decision);
+  });
+  py::class_<FitState>(m, "FitState")
+      .def(py::init<>())
+      .def_readonly("decision", &FitState::decision)
+      .def_readonly("a", &FitState::a)
+      .def_readonly("b", &FitState::b)
+      .def_readonly("o_multi", &FitState::o_multi)
+      .def_readonly("o_single", &FitState::o_single);
   m.def("initial_split", [](int devices, bool smooth, std::vector<std::vector<double>> history,
                             long long total, long long step) {
     std::vector<long long> ranges;
@@ -144,7 +196,7 @@ PYBIND11_MODULE(_cek, m) {
   py::class_<ArraySpec>(m, "ArraySpec")
       .def(py::init<>())
       .def(py::init([](uint64_t uid, uint64_t host, uint64_t bytes, int elem_size, bool read, bool partial,
-                       bool write, bool write_all, bool ro, bool wo, bool zc, int epw, int epg) {
+                       bool write, bool write_all, bool ro, bool wo, bool zc, int epw, int epg, bool gather) {
              ArraySpec a;
              a.uid = uid;
              a.host = reinterpret_cast<void*>(host);
@@ -159,11 +211,13 @@ PYBIND11_MODULE(_cek, m) {
              a.zc = zc;
              a.epw = epw;
              a.epg = epg;
+             a.gather = gather;
              return a;
            }),
            py::arg("uid"), py::arg("host"), py::arg("bytes"), py::arg("elem_size"), py::arg("read") = true,
            py::arg("partial") = false, py::arg("write") = true, py::arg("write_all") = false,
-           py::arg("ro") = false, py::arg("wo") = false, py::arg("zc") = false, py::arg("epw") = 1, py::arg("epg") = 0)
+           py::arg("ro") = false, py::arg("wo") = false, py::arg("zc") = false, py::arg("epw") = 1, py::arg("epg") = 0,
+           py::arg("gather") = false)
       .def_readwrite("uid", &ArraySpec::uid)
       .def_property("host", [](const ArraySpec& a) { return reinterpret_cast<uint64_t>(a.host); },
                     [](ArraySpec& a, uint64_t p) { a.host = reinterpret_cast<void*>(p); })
@@ -177,7 +231,8 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("wo", &ArraySpec::wo)
       .def_readwrite("zc", &ArraySpec::zc)
       .def_readwrite("epw", &ArraySpec::epw)
-      .def_readwrite("epg", &ArraySpec::epg);
+      .def_readwrite("epg", &ArraySpec::epg)
+      .def_readwrite("gather", &ArraySpec::gather);
 
   py::class_<ComputeCall>(m, "ComputeCall")
       .def(py::init<>())
@@ -211,6 +266,9 @@ PYBIND11_MODULE(_cek, m) {
       .def_readonly("h2d_bytes", &ComputeRecord::h2d_bytes)
       .def_readonly("d2h_bytes", &ComputeRecord::d2h_bytes)
       .def_readonly("p2p_bytes", &ComputeRecord::p2p_bytes)
+      .def_readonly("gather_bytes", &ComputeRecord::gather_bytes)
+      .def_readonly("staged_bytes", &ComputeRecord::staged_bytes)
+      .def_readonly("p2p_path", &ComputeRecord::p2p_path)
       .def_readonly("pipelined", &ComputeRecord::pipelined);
 
   py::class_<Exchanger, PyExchanger, std::shared_ptr<Exchanger>>(m, "Exchanger")
@@ -296,6 +354,19 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("dist_broadcast_reads", &Cores::dist_broadcast_reads)
       .def_readwrite("dist_split_reads", &Cores::dist_split_reads)
       .def("set_time_scale", &Cores::set_time_scale)
+      .def_readwrite("balancer_predictor", &Cores::balancer_predictor)
+      .def("set_time_offset", &Cores::set_time_offset)
+      .def("predictor_info", [](const Cores& c, int id) {
+        py::dict d;
+        const FitState* f = c.fit_state(id);
+        if (!f) return d;
+        d["decision"] = f->decision;
+        d["a_ms"] = f->a;
+        d["b_ms_per_item"] = f->b;
+        d["o_multi_ms"] = f->o_multi;
+        d["o_single_ms"] = f->o_single;
+        return d;
+      })
       .def("set_dynamic_lds", &Cores::set_dynamic_lds)
       .def("has_state", &Cores::has_state)
       .def("ranges", &Cores::ranges)
@@ -315,13 +386,14 @@ PYBIND11_MODULE(_cek, m) {
       .def("device_enqueue_errors", &Cores::device_enqueue_errors, py::call_guard<py::gil_scoped_release>())
       .def("timeline",
            [](Cores& c) {
-             std::vector<std::tuple<int, int, double, double>> out;
+             std::vector<std::tuple<int, int, double, double, double, double>> out;
              std::vector<Cores::TimelineSpan> spans;
              {
                py::gil_scoped_release nogil;
                spans = c.timeline();
              }
-             for (auto& s : spans) out.emplace_back(s.device, s.compute_id, s.begin_ms, s.end_ms);
+             for (auto& s : spans)
+               out.emplace_back(s.device, s.compute_id, s.begin_ms, s.end_ms, s.abs_begin_ms, s.abs_end_ms);
              return out;
            })
       .def("markers_reached", &Cores::markers_reached)
@@ -342,6 +414,10 @@ PYBIND11_MODULE(_cek, m) {
       .def("download", &Cores::download, py::call_guard<py::gil_scoped_release>())
       .def("copy_between", &Cores::copy_between, py::call_guard<py::gil_scoped_release>())
       .def("share_slices", &Cores::share_slices, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("peer_ordinals", &Cores::peer_ordinals)
+      .def_property_readonly("peer_matrix", &Cores::peer_matrix)
+      .def_property_readonly("p2p_path", &Cores::p2p_path)
+      .def("can_peer", &Cores::can_peer)
       .def("set_distributed", &Cores::set_distributed);
 
   py::class_<PoolTask>(m, "PoolTask")

@@ -13,6 +13,37 @@ CopyEngine::~CopyEngine() {
     (void)hipStreamSynchronize(streams_[i]);
     (void)hipStreamDestroy(streams_[i]);
   }
+  for (auto& p : pending_) free_events_.push_back({p.ordinal, p.b}), free_events_.push_back({p.ordinal, p.e});
+  for (auto& fe : free_events_) {
+    (void)hipSetDevice(fe.first);
+    (void)hipEventDestroy(fe.second);
+  }
+}
+
+hipEvent_t CopyEngine::timing_event(int ordinal) {
+  for (size_t i = 0; i < free_events_.size(); ++i)
+    if (free_events_[i].first == ordinal) {
+      hipEvent_t e = free_events_[i].second;
+      free_events_.erase(free_events_.begin() + static_cast<long>(i));
+      return e;
+    }
+  hipEvent_t e;
+  CEK_HIP(hipEventCreate(&e));
+  return e;
+}
+
+std::vector<CopyEngine::Span> CopyEngine::timeline() {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<Span> out;
+  for (auto& p : pending_) {
+    CEK_HIP(hipSetDevice(p.ordinal));
+    CEK_HIP(hipEventSynchronize(p.e));
+    out.push_back({p.ordinal, p.kind, p.bytes, event_host_ms(p.ordinal, p.b), event_host_ms(p.ordinal, p.e)});
+    free_events_.push_back({p.ordinal, p.b});
+    free_events_.push_back({p.ordinal, p.e});
+  }
+  pending_.clear();
+  return out;
 }
 
 hipStream_t CopyEngine::stream(int ordinal) {
@@ -34,21 +65,31 @@ void CopyEngine::copy(void* dst, int dst_dev, const void* src, int src_dev, uint
     host_bytes += bytes;
     return;
   }
+  const int on = dst_dev >= 0 ? dst_dev : src_dev;  // the GPU whose stream runs the copy
+  hipStream_t s = stream(on);
+  CEK_HIP(hipSetDevice(on));
+  Pending p{on, "", bytes, nullptr, nullptr};
+  if (record_timeline) {
+    p.b = timing_event(on);
+    p.e = timing_event(on);
+    CEK_HIP(hipEventRecord(p.b, s));
+  }
   if (dst_dev >= 0 && src_dev >= 0) {
-    hipStream_t s = stream(dst_dev);
-    CEK_HIP(hipSetDevice(dst_dev));
     CEK_HIP(hipMemcpyPeerAsync(dst, dst_dev, src, src_dev, bytes, s));
     p2p_bytes += bytes;
+    p.kind = "p2p";
   } else if (dst_dev >= 0) {
-    hipStream_t s = stream(dst_dev);
-    CEK_HIP(hipSetDevice(dst_dev));
     CEK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
     h2d_bytes += bytes;
+    p.kind = "h2d";
   } else {
-    hipStream_t s = stream(src_dev);
-    CEK_HIP(hipSetDevice(src_dev));
     CEK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
     d2h_bytes += bytes;
+    p.kind = "d2h";
+  }
+  if (record_timeline) {
+    CEK_HIP(hipEventRecord(p.e, s));
+    pending_.push_back(p);
   }
 }
 

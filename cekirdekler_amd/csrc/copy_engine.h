@@ -34,7 +34,28 @@ class CopyEngine {
   uint64_t copies = 0;
   void reset_counters() { p2p_bytes = h2d_bytes = d2h_bytes = host_bytes = copies = 0; }
 
+  // Copy timeline: with record_timeline on, every device copy is bracketed
+  // by timing events on its stream; timeline() waits for them and returns
+  // each copy's span on the host clock (event_host_ms), then clears the list.
+  bool record_timeline = false;
+  struct Span {
+    int ordinal;       // the GPU whose stream ran the copy
+    std::string kind;  // p2p | h2d | d2h
+    uint64_t bytes;
+    double abs_begin_ms, abs_end_ms;
+  };
+  std::vector<Span> timeline();
+
  private:
+  struct Pending {
+    int ordinal;
+    std::string kind;
+    uint64_t bytes;
+    hipEvent_t b, e;
+  };
+  std::vector<Pending> pending_;
+  std::vector<std::pair<int, hipEvent_t>> free_events_;
+  hipEvent_t timing_event(int ordinal);
   hipStream_t stream(int ordinal);
   std::mutex mu_;
   std::vector<hipStream_t> streams_;

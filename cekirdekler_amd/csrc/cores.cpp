@@ -6,6 +6,7 @@
 #include <map>
 #include <numeric>
 #include <sstream>
+#include <thread>
 
 #include "memory.h"
 #include "trace.h"
@@ -46,9 +47,166 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
   if (const char* e = std::getenv("CEK_DEVICE_SPANS")) device_spans = std::string(e) != "0";
   if (const char* e = std::getenv("CEK_KERNEL_D2H")) set_kernel_d2h(std::string(e) != "0");
   time_scale_.assign(workers_.size(), 1.0);
+  time_offset_.assign(workers_.size(), 0.0);
   enabled_.assign(workers_.size(), true);
   inject_.assign(workers_.size(), 0);
+  init_peer_topology();
+  all_gpu_ = std::all_of(workers_.begin(), workers_.end(), [](const std::unique_ptr<Worker>& w) { return w->gpu(); });
   build_ms_ = now_ms() - t0;
+}
+
+// Distinct GPUs of this device set: enable peer access among them (xGMI) so
+// the read fan-out, the keep-resident gather and copy_between move bytes
+// GPU↔GPU directly.  A pair that cannot peer is recorded: the read fan-out
+// then falls back to one PCIe upload per device, and gather copies between
+// that pair are counted as staged.
+void Cores::init_peer_topology() {
+  ord_index_.assign(workers_.size(), -1);
+  peer_ordinals_.clear();
+  for (size_t w = 0; w < workers_.size(); ++w) {
+    if (!workers_[w]->gpu()) continue;
+    const int o = workers_[w]->dev().ordinal;
+    auto it = std::find(peer_ordinals_.begin(), peer_ordinals_.end(), o);
+    ord_index_[w] = static_cast<int>(it - peer_ordinals_.begin());
+    if (it == peer_ordinals_.end()) peer_ordinals_.push_back(o);
+  }
+  if (peer_ordinals_.size() >= 2) {
+    peer_matrix_ = enable_peer_access_among(peer_ordinals_);
+  } else {
+    peer_matrix_.assign(peer_ordinals_.size(), std::vector<int>(peer_ordinals_.size(), 1));
+  }
+  p2p_path_ = peer_path(peer_matrix_);
+}
+
+bool Cores::can_peer(int w1, int w2) const {
+  const int a = ord_index_.at(w1), b = ord_index_.at(w2);
+  if (a < 0 || b < 0) return false;
+  return a == b || (peer_matrix_[a][b] && peer_matrix_[b][a]);
+}
+
+void Cores::count_d2d(int ws, int wd, uint64_t bytes) {
+  d2d_.bytes += bytes;
+  if (ord_index_[ws] == ord_index_[wd])
+    d2d_.local += bytes;
+  else if (can_peer(ws, wd))
+    d2d_.xgmi += bytes;
+  else
+    d2d_.staged += bytes;
+}
+
+// One device→device copy on stream s (of either device): a plain D2D copy
+// inside one GPU, a peer copy between GPUs (over xGMI when peer access is on;
+// the runtime stages it through host memory otherwise).
+uint64_t Cores::d2d_copy(int ws, int wd, char* dst, const char* src, uint64_t bytes, hipStream_t s) {
+  if (!bytes || dst == src) return 0;
+  const int os = workers_[ws]->dev().ordinal, od = workers_[wd]->dev().ordinal;
+  if (os == od)
+    CEK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+  else
+    CEK_HIP(hipMemcpyPeerAsync(dst, od, src, os, bytes, s));
+  count_d2d(ws, wd, bytes);
+  return bytes;
+}
+
+hipEvent_t Cores::gather_event(std::vector<hipEvent_t>& v, int w) {
+  if (v.size() < workers_.size()) v.resize(workers_.size(), nullptr);
+  if (!v[w]) {
+    workers_[w]->set_device();
+    CEK_HIP(hipEventCreateWithFlags(&v[w], hipEventDisableTiming));
+  }
+  return v[w];
+}
+
+// Work about to run on stream s of wk must see the last gather's copies, and
+// must not overwrite a slice the copies are still reading.
+void Cores::wait_gather(Worker& wk, hipStream_t s) {
+  if (!gather_pending_) return;
+  for (size_t g = 0; g < pushed_.size(); ++g) {
+    if (!pushed_[g]) continue;
+    if (wk.gpu())
+      CEK_HIP(hipStreamWaitEvent(s, pushed_[g], 0));
+    else
+      CEK_HIP(hipEventSynchronize(pushed_[g]));
+  }
+}
+
+// Keep-resident gather of the call's `arrays` (indices into c.arrays): each
+// device's slice (by this call's split) lands in every other device's replica.
+// Issued from the calling thread once every device has enqueued its kernels:
+// GPU g's main stream waits for the kernels of every GPU (no replica is
+// overwritten while a kernel of this call still reads it), pulls the CPU
+// device's slices from host memory, pushes its own slice to every other
+// replica (peer copies over xGMI), and records pushed_[g].  No host sync in
+// enqueue mode; otherwise the copies are complete when compute() returns.
+uint64_t Cores::issue_gather(const ComputeCall& c, const BalancerState& st, const std::vector<int>& arrays) {
+  const int n = num_devices();
+  std::vector<int> on;  // enabled local devices: they hold replicas
+  for (int w = 0; w < n; ++w)
+    if (enabled_[w]) on.push_back(w);
+  if (on.size() < 2 || arrays.empty()) return 0;
+  uint64_t moved = 0;
+  struct Piece {
+    std::vector<char*> ptr;
+    std::vector<uint64_t> off, len;
+  };
+  std::vector<Piece> pcs(arrays.size());
+  for (size_t i = 0; i < arrays.size(); ++i) {
+    const ArraySpec& a = c.arrays[arrays[i]];
+    Piece& p = pcs[i];
+    p.ptr.assign(n, nullptr);
+    p.off.assign(n, 0);
+    p.len.assign(n, 0);
+    for (int w : on) {
+      uint64_t b, k;
+      a.slice(st.references[global_base_ + w], st.ranges[global_base_ + w], c.local_range, b, k);
+      p.off[w] = std::min<uint64_t>(b * a.elem_size, a.bytes);
+      p.len[w] = std::min<uint64_t>(k * a.elem_size, a.bytes - p.off[w]);
+      workers_[w]->set_device();
+      p.ptr[w] = static_cast<char*>(workers_[w]->buffer(a));
+    }
+  }
+  std::vector<int> gpus;
+  for (int w : on)
+    if (workers_[w]->gpu()) gpus.push_back(w);
+  for (int g : gpus) {
+    Worker& wg = *workers_[g];
+    wg.set_device();
+    hipStream_t m = wg.main_stream();
+    for (int d : gpus)
+      if (kdone_.size() > static_cast<size_t>(d) && kdone_[d]) CEK_HIP(hipStreamWaitEvent(m, kdone_[d], 0));
+    for (size_t i = 0; i < arrays.size(); ++i) {
+      const ArraySpec& a = c.arrays[arrays[i]];
+      Piece& p = pcs[i];
+      for (int s : on) {  // the CPU device's slices: host → this replica
+        if (workers_[s]->gpu() || !p.len[s]) continue;
+        CEK_HIP(hipMemcpyAsync(p.ptr[g] + p.off[s], static_cast<const char*>(a.host) + p.off[s], p.len[s],
+                               hipMemcpyHostToDevice, m));
+        moved += p.len[s];
+      }
+      if (!p.len[g]) continue;
+      for (int d : on) {  // this GPU's slice → every other replica
+        if (d == g || p.ptr[d] == p.ptr[g]) continue;
+        if (workers_[d]->gpu()) {
+          moved += d2d_copy(g, d, p.ptr[d] + p.off[g], p.ptr[g] + p.off[g], p.len[g], m);
+          log_op(global_base_ + d, "gather", 0, static_cast<long long>(p.off[g]), static_cast<long long>(p.len[g]),
+                 global_base_ + g);
+        } else {
+          CEK_HIP(hipMemcpyAsync(p.ptr[d] + p.off[g], p.ptr[g] + p.off[g], p.len[g], hipMemcpyDeviceToHost, m));
+          moved += p.len[g];
+        }
+      }
+    }
+    CEK_HIP(hipEventRecord(gather_event(pushed_, g), m));
+  }
+  gather_pending_ = true;
+  if (!enqueue_mode_) {
+    for (int g : gpus) {
+      workers_[g]->set_device();
+      CEK_HIP(hipStreamSynchronize(workers_[g]->main_stream()));
+    }
+    gather_pending_ = false;
+  }
+  return moved;
 }
 
 Cores::~Cores() {
@@ -92,6 +250,12 @@ Cores::~Cores() {
     (void)hipEventDestroy(peer_ev_[w].up);
     (void)hipEventDestroy(peer_ev_[w].pulled);
   }
+  for (auto* v : {&peer_ready_, &kdone_, &pushed_})
+    for (size_t w = 0; w < v->size() && w < workers_.size(); ++w)
+      if ((*v)[w]) {
+        workers_[w]->set_device();
+        (void)hipEventDestroy((*v)[w]);
+      }
   workers_.clear();
 }
 
@@ -103,6 +267,11 @@ std::vector<KernelSig> Cores::kernels() const {
 void Cores::set_time_scale(int device, double scale) {
   if (device < 0 || device >= static_cast<int>(time_scale_.size())) throw Error("bad device index");
   time_scale_[device] = scale;
+}
+
+void Cores::set_time_offset(int device, double ms) {
+  if (device < 0 || device >= static_cast<int>(time_offset_.size())) throw Error("bad device index");
+  time_offset_[device] = ms;
 }
 
 void Cores::set_device_enabled(int device, bool on) {
@@ -137,7 +306,7 @@ void Cores::balance(BalancerState& st, bool first, long long G, long long step) 
   if (static_cast<int>(on.size()) == D) {
     if (first)
       initial_split(D, smooth, st.history, G, st.ranges, step);
-    else
+    else if (!(balancer_predictor && !ex_ && predict_split(st.fit, st.bench, st.last_wall_ms, G, st.ranges, step)))
       load_balance(st.bench, smooth, st.history, G, st.ranges, step);
     return;
   }
@@ -205,7 +374,8 @@ void Cores::set_enqueue_mode(bool on) {
     std::vector<double> ms(num_devices());
     for (int w = 0; w < num_devices(); ++w) {
       // GPU: union of this device's timed spans; CPU device: wall clock
-      const double dev = workers_[w]->gpu() ? enqueue_spans_ms(w) : -1.0;
+      double dev = workers_[w]->gpu() ? enqueue_spans_ms(w) : -1.0;
+      if (!all_gpu_) dev = -1.0;  // mixed CPU+GPU: one clock for everybody
       ms[w] = (dev > 0 ? dev : el) * time_scale_[w];
     }
     // every rank leaves enqueue mode together: exchange so all ranks keep the
@@ -419,6 +589,7 @@ void Cores::finish() {
     w->wait();
     w->sync_all();
   }
+  gather_pending_ = false;  // every gather copy (on the main streams) is done
 }
 
 void Cores::release_array(uint64_t uid) {
@@ -432,17 +603,21 @@ uint64_t Cores::device_pointer(int i, const ArraySpec& a) {
 }
 
 void Cores::upload(int i, const ArraySpec& a) {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   Worker& w = *workers_.at(i);
   w.set_device();
   hipStream_t s = w.main_stream();
+  wait_gather(w, s);
   w.h2d(s, a, 0, a.bytes / a.elem_size);
   if (w.gpu()) CEK_HIP(hipStreamSynchronize(s));
 }
 
 void Cores::download(int i, const ArraySpec& a) {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   Worker& w = *workers_.at(i);
   w.set_device();
   hipStream_t s = w.main_stream();
+  wait_gather(w, s);
   w.d2h(s, a, 0, a.bytes / a.elem_size);
   if (w.gpu()) CEK_HIP(hipStreamSynchronize(s));
 }
@@ -456,18 +631,31 @@ void Cores::copy_between(int src_dev, const ArraySpec& src, int dst_dev, const A
     std::memcpy(dst.host, src.host, bytes);
     return;
   }
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   if (ws.gpu() && wd.gpu()) {
+    // On the source's main stream after the destination's queued work; the
+    // destination's main stream then waits for the copy (no host sync in
+    // enqueue mode).
     ws.set_device();
     void* sp = ws.buffer(src);
     wd.set_device();
     void* dp = wd.buffer(dst);
+    hipEvent_t before = gather_event(kdone_, dst_dev);
+    CEK_HIP(hipEventRecord(before, wd.main_stream()));
     ws.set_device();
     hipStream_t s = ws.main_stream();
-    if (ws.dev().ordinal == wd.dev().ordinal)
-      CEK_HIP(hipMemcpyAsync(dp, sp, bytes, hipMemcpyDeviceToDevice, s));
-    else
-      CEK_HIP(hipMemcpyPeerAsync(dp, wd.dev().ordinal, sp, ws.dev().ordinal, bytes, s));
-    CEK_HIP(hipStreamSynchronize(s));
+    wait_gather(ws, s);
+    CEK_HIP(hipStreamWaitEvent(s, before, 0));
+    d2d_ = D2DCount();
+    d2d_copy(src_dev, dst_dev, static_cast<char*>(dp), static_cast<const char*>(sp), bytes, s);
+    hipEvent_t after = gather_event(pushed_, src_dev);
+    CEK_HIP(hipEventRecord(after, s));
+    wd.set_device();
+    CEK_HIP(hipStreamWaitEvent(wd.main_stream(), after, 0));
+    if (!enqueue_mode_) {
+      ws.set_device();
+      CEK_HIP(hipStreamSynchronize(s));
+    }
     return;
   }
   if (ws.gpu()) {  // GPU → CPU device (host memory)
@@ -484,49 +672,22 @@ void Cores::copy_between(int src_dev, const ArraySpec& src, int dst_dev, const A
 }
 
 void Cores::share_slices(int id, const ArraySpec& a, long long local_range) {
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   auto it = state_.find(id);
   if (it == state_.end()) throw Error("share_slices: unknown compute id");
-  const auto& st = it->second;
-  const int n = num_devices();
-  std::vector<uint64_t> off(n), len(n);
-  for (int w = 0; w < n; ++w) {
-    uint64_t b, c;
-    a.slice(st.references[global_base_ + w], st.ranges[global_base_ + w], local_range, b, c);
-    off[w] = b * a.elem_size;
-    len[w] = c * a.elem_size;
-    if (off[w] >= a.bytes) len[w] = 0;
-    else if (off[w] + len[w] > a.bytes) len[w] = a.bytes - off[w];
-  }
-  std::vector<char*> ptr(n);
-  for (int w = 0; w < n; ++w) {
+  if (capturing_) throw Error("share_slices during a graph capture");
+  // the copies follow whatever is queued on every GPU's main stream
+  for (int w = 0; w < num_devices(); ++w) {
+    if (!workers_[w]->gpu() || !enabled_[w]) continue;
     workers_[w]->set_device();
-    ptr[w] = static_cast<char*>(workers_[w]->buffer(a));
+    wait_gather(*workers_[w], workers_[w]->main_stream());
+    CEK_HIP(hipEventRecord(gather_event(kdone_, w), workers_[w]->main_stream()));
   }
-  for (int s = 0; s < n; ++s) {
-    Worker& ws = *workers_[s];
-    if (len[s] == 0) continue;
-    for (int d = 0; d < n; ++d) {
-      if (d == s) continue;
-      Worker& wd = *workers_[d];
-      if (ptr[d] == ptr[s]) continue;  // same memory (CPU devices share host arrays)
-      if (ws.gpu()) {
-        ws.set_device();
-        hipStream_t st_s = ws.main_stream();
-        if (wd.gpu() && wd.dev().ordinal != ws.dev().ordinal)
-          CEK_HIP(hipMemcpyPeerAsync(ptr[d] + off[s], wd.dev().ordinal, ptr[s] + off[s], ws.dev().ordinal,
-                                     len[s], st_s));
-        else
-          CEK_HIP(hipMemcpyAsync(ptr[d] + off[s], ptr[s] + off[s], len[s], hipMemcpyDefault, st_s));
-      } else if (wd.gpu()) {
-        wd.set_device();
-        CEK_HIP(hipMemcpyAsync(ptr[d] + off[s], ptr[s] + off[s], len[s], hipMemcpyHostToDevice,
-                               wd.main_stream()));
-      } else {
-        std::memcpy(ptr[d] + off[s], ptr[s] + off[s], len[s]);
-      }
-    }
-  }
-  for (auto& w : workers_) w->sync_all();
+  ComputeCall c;
+  c.arrays = {a};
+  c.local_range = local_range;
+  d2d_ = D2DCount();
+  issue_gather(c, it->second, {0});
 }
 
 // ------------------------------------------------------------- compute --
@@ -612,7 +773,7 @@ std::vector<Cores::TimelineSpan> Cores::timeline() {
   for (auto& sp : spans) epoch.emplace(sp.device, sp);
   for (auto& sp : spans) {
     const PendingSpan& e0 = epoch.at(sp.device);
-    TimelineSpan t{sp.device, sp.compute_id, 0, 0};
+    TimelineSpan t{sp.device, sp.compute_id, 0, 0, 0, 0};
     if (sp.begin) {
       CEK_HIP(hipEventSynchronize(sp.end));
       float b = 0, e = 0;
@@ -620,9 +781,14 @@ std::vector<Cores::TimelineSpan> Cores::timeline() {
       CEK_HIP(hipEventElapsedTime(&e, e0.begin, sp.end));
       t.begin_ms = b;
       t.end_ms = e;
+      const int ord = workers_[sp.device]->dev().ordinal;
+      t.abs_begin_ms = event_host_ms(ord, sp.begin);
+      t.abs_end_ms = event_host_ms(ord, sp.end);
     } else {
       t.begin_ms = sp.host_begin - e0.host_begin;
       t.end_ms = sp.host_end - e0.host_begin;
+      t.abs_begin_ms = sp.host_begin;
+      t.abs_end_ms = sp.host_end;
     }
     out.push_back(t);
   }
@@ -756,6 +922,14 @@ uint64_t Cores::stage_peer_reads(const ComputeCall& c, const std::vector<long lo
     if (workers_[w]->gpu() && enabled_[w] && ranges[global_base_ + w] > 0) part.push_back(w);
   const int P = static_cast<int>(part.size());
   if (P < 2) return 0;
+  // every pair of distinct GPUs must peer; otherwise each device uploads the
+  // whole array over its own PCIe link (reference behaviour), explicitly
+  for (int x = 0; x < P; ++x)
+    for (int y = 0; y < P; ++y)
+      if (!can_peer(part[x], part[y])) {
+        d2d_.pcie_fallback = true;
+        return 0;
+      }
   bool any = false;
   for (size_t i = 0; i < c.arrays.size(); ++i) {
     const auto& a = c.arrays[i];
@@ -815,13 +989,26 @@ uint64_t Cores::stage_peer_reads(const ComputeCall& c, const std::vector<long lo
         if (j == k || !len[j]) continue;
         Worker& ws = *workers_[part[j]];
         CEK_HIP(hipStreamWaitEvent(m, peer_ev_[part[j]].up, 0));
-        CEK_HIP(hipMemcpyPeerAsync(ptr[k] + off[j], wd.dev().ordinal, ptr[j] + off[j], ws.dev().ordinal, len[j], m));
-        p2p += len[j];
+        p2p += d2d_copy(part[j], part[k], ptr[k] + off[j], ptr[j] + off[j], len[j], m);
+        (void)ws;
         log_op(global_base_ + part[k], "p2p", 0, static_cast<long long>(off[j]), static_cast<long long>(len[j]),
                global_base_ + part[j]);
       }
       CEK_HIP(hipEventRecord(peer_ev_[part[k]].pulled, m));
     }
+  }
+  // 3) a GPU's kernels may modify a staged array in place (read without
+  //    write-back does not mean const): they start only once every peer has
+  //    pulled this GPU's chunk out of its replica
+  if (peer_ready_.size() < static_cast<size_t>(nloc)) peer_ready_.resize(nloc, nullptr);
+  for (int k = 0; k < P; ++k) {
+    Worker& wk = *workers_[part[k]];
+    wk.set_device();
+    hipStream_t m = wk.main_stream();
+    for (int j = 0; j < P; ++j)
+      if (j != k) CEK_HIP(hipStreamWaitEvent(m, peer_ev_[part[j]].pulled, 0));
+    if (!peer_ready_[part[k]]) CEK_HIP(hipEventCreateWithFlags(&peer_ready_[part[k]], hipEventDisableTiming));
+    CEK_HIP(hipEventRecord(peer_ready_[part[k]], m));
   }
   return p2p;
 }
@@ -830,7 +1017,7 @@ void Cores::full_reads(Worker& wk, hipStream_t s, const ComputeCall& c, uint64_t
   const bool dist = comm_ && dist_broadcast_reads;
   const int w = worker_index(wk);
   if (w >= 0 && w < static_cast<int>(staged_dev_.size()) && staged_dev_[w] && s != wk.main_stream())
-    CEK_HIP(hipStreamWaitEvent(s, peer_ev_[w].pulled, 0));  // staged on the main stream
+    CEK_HIP(hipStreamWaitEvent(s, peer_ready_[w], 0));  // staged on the main stream
   for (size_t i = 0; i < c.arrays.size(); ++i) {
     const auto& a = c.arrays[i];
     if (a.zc || a.partial || !a.read) continue;
@@ -871,8 +1058,15 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
   hipStream_t s = nullptr;
   if (wk.gpu())
     s = (enqueue_mode_ && async_enqueue) ? wk.compute_stream(wk.next_compute_queue()) : wk.main_stream();
+  if (wk.gpu() && s != wk.main_stream()) wait_gather(wk, s);
   span_begin(wk, s);
-  const bool gather = comm_ && dist_gather_writes;
+  // across ranks: written slices all-gathered by RCCL (every written array
+  // with dist_gather_writes, else the arrays flagged gather)
+  const bool gather = comm_ && (dist_gather_writes || std::any_of(c.arrays.begin(), c.arrays.end(),
+                                                                  [](const ArraySpec& a) { return a.gather; }));
+  auto gathered = [&](const ArraySpec& a) {
+    return comm_ && !a.zc && !a.write_all && (a.gather || (dist_gather_writes && (a.write || a.wo)));
+  };
   // phase 1: host → device (partial slice wins over full read)
   for (auto& a : c.arrays) {
     if (a.zc) continue;
@@ -886,11 +1080,15 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
   full_reads(wk, s, c, h2d);
   // phase 2: kernels
   launch_kernels(wk, s, c, ref, range);
+  if (call_gathers_ && wk.gpu()) {  // in-process gather: this device's kernels are enqueued
+    const int w = worker_index(wk);
+    CEK_HIP(hipEventRecord(gather_event(kdone_, w), s));
+  }
   // optional device-side all-gather of written slices (distributed keep-resident)
   if (gather) {
     auto& st = state_[c.compute_id];
     for (auto& a : c.arrays) {
-      if (a.zc || !(a.write || a.wo) || a.write_all) continue;
+      if (!gathered(a)) continue;
       std::vector<uint64_t> offs(global_devices_), sizes(global_devices_);
       for (int g = 0; g < global_devices_; ++g) {
         uint64_t b, n;
@@ -933,7 +1131,7 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
         wk.d2h(s, a, 0, a.bytes / a.elem_size);
         *d2h += a.bytes;
       }
-    } else if (gather) {
+    } else if (gathered(a)) {  // the replica holds every rank's slice
       wk.d2h(s, a, 0, a.bytes / a.elem_size);
       *d2h += a.bytes;
     } else {
@@ -1141,6 +1339,12 @@ void Cores::run_device_body(int w, const ComputeCall& c, long long ref, long lon
     throw Error("injected failure on device " + std::to_string(w));
   }
   double t0 = now_ms();
+  if (!wk.gpu()) wait_gather(wk, nullptr);  // host memory: the copies into it are done
+  const double offset = range > 0 ? time_offset_[w] : 0.0;
+  if (offset > 0) {  // injected fixed cost per compute (tests): real host time
+    const double until = now_ms() + offset;
+    while (now_ms() < until) std::this_thread::yield();
+  }
   if (range > 0) {
     wk.set_device();
     if (!pipelined)
@@ -1154,9 +1358,13 @@ void Cores::run_device_body(int w, const ComputeCall& c, long long ref, long lon
     run_3phase(wk, gidx, c, ref, 0, h2d, d2h);
   }
   double el = now_ms() - t0 - t_phase_wait;
-  if (range > 0 && wk.gpu() && !enqueue_mode_) {
+  // Device-time spans only when every local device is a GPU: a CPU device
+  // has only the host clock, and a GPU's span leaves out its launch, sync
+  // and staging overhead, so the two would not be comparable (the reference
+  // times every device with one host stopwatch, Worker.cs:779-807).
+  if (range > 0 && wk.gpu() && !enqueue_mode_ && all_gpu_) {
     const double dev = span_ms(w);  // the stream was drained: device time of this compute
-    if (dev > 0) el = dev;
+    if (dev > 0) el = dev + offset;
   }
   *out_ms = el * time_scale_[w];
 }
@@ -1268,7 +1476,15 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
     for (auto& a : c.arrays)
       if (!a.zc && a.read && !a.partial && a.write) hazard = true;
   // Pipelining eligibility (Cores.cs:624-652), decided per call for all devices.
-  bool pipelined = pipe_req && c.repeats <= 1 && !enqueue_mode_ && !hazard;
+  // keep-resident gather arrays (in process; across ranks RCCL does it)
+  std::vector<int> gather_idx;
+  for (size_t i = 0; i < c.arrays.size(); ++i)
+    if (c.arrays[i].gather && !c.arrays[i].zc) gather_idx.push_back(static_cast<int>(i));
+  if (!gather_idx.empty() && capturing_) throw Error("keep-resident gather arrays cannot be captured into a graph");
+  if (!gather_idx.empty() && ex_ && !comm_ && global_devices_ > nloc)
+    throw Error("gather across ranks needs an RCCL communicator (DistributedCruncher(comm=True))");
+  call_gathers_ = !gather_idx.empty() && !comm_ && nloc > 1;
+  bool pipelined = pipe_req && c.repeats <= 1 && !enqueue_mode_ && !hazard && gather_idx.empty();
   for (int i = 0; i < D && pipelined; ++i)
     if (st.ranges[i] != 0 && (st.ranges[i] % (B * U) != 0 || st.ranges[i] < B * U)) pipelined = false;
   if (comm_ && (dist_gather_writes || dist_broadcast_reads || dist_split_reads)) pipelined = false;
@@ -1278,7 +1494,14 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
   // xGMI fan-out of full reads, enqueued before the per-device work (its
   // time lands on the devices' streams, inside their measured span only
   // through the event waits in full_reads)
-  const uint64_t p2p = stage_peer_reads(c, st.ranges, h2d);
+  d2d_ = D2DCount();
+  if (gather_pending_)  // the last gather's copies finish before this call touches any replica
+    for (int w = 0; w < nloc; ++w)
+      if (workers_[w]->gpu()) {
+        workers_[w]->set_device();
+        wait_gather(*workers_[w], workers_[w]->main_stream());
+      }
+  stage_peer_reads(c, st.ranges, h2d);
   DeviceFailure failure;
   int participants = 0;
   for (int w = 0; w < nloc; ++w)
@@ -1316,8 +1539,14 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
     }
   }
   if (!failure.devices.empty()) {
+    call_gathers_ = false;
     if (!failed) throw Error(failure.what());
     *failed = failure;
+  }
+  uint64_t gathered = 0;
+  if (call_gathers_) {
+    call_gathers_ = false;
+    gathered = issue_gather(c, st, gather_idx);
   }
   last_id_ = c.compute_id;
   if (!enqueue_mode_) {
@@ -1328,12 +1557,20 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
   ++st.calls;
   last_record_.compute_id = c.compute_id;
   last_record_.wall_ms = now_ms() - wall0;
+  st.last_wall_ms = last_record_.wall_ms;
   last_record_.ranges = st.ranges;
   last_record_.references = st.references;
   last_record_.device_ms = st.bench;
   last_record_.h2d_bytes = std::accumulate(h2d.begin(), h2d.end(), 0ull);
   last_record_.d2h_bytes = std::accumulate(d2h.begin(), d2h.end(), 0ull);
-  last_record_.p2p_bytes = p2p;
+  last_record_.p2p_bytes = d2d_.bytes;
+  last_record_.gather_bytes = gathered;
+  last_record_.staged_bytes = d2d_.staged;
+  last_record_.p2p_path = d2d_.pcie_fallback ? "pcie"
+                          : d2d_.staged       ? "staged"
+                          : d2d_.xgmi         ? "xgmi"
+                          : d2d_.local        ? "local"
+                                              : "none";
   last_record_.pipelined = pipelined;
 }
 

@@ -62,7 +62,14 @@ struct ComputeRecord {  // structured per-call record (observability)
   std::vector<long long> ranges, references;
   std::vector<double> device_ms;
   uint64_t h2d_bytes = 0, d2h_bytes = 0;
-  uint64_t p2p_bytes = 0;  // device→device (xGMI peer) bytes of the read fan-out
+  uint64_t p2p_bytes = 0;     // device→device bytes (read fan-out + keep-resident gather)
+  uint64_t gather_bytes = 0;  // of which the keep-resident gather
+  uint64_t staged_bytes = 0;  // of p2p_bytes: between GPUs without peer access (host-bounced)
+  // where this call's device→device bytes went: "none" (no such copy),
+  // "local" (logical devices of one GPU), "xgmi" (peer copies between GPUs),
+  // "staged" (some pair without peer access), "pcie" (the read fan-out fell
+  // back to one PCIe upload per device because a pair cannot peer)
+  std::string p2p_path = "none";
   bool pipelined = false;
 };
 
@@ -161,6 +168,17 @@ class Cores {
   // enqueued afterwards starts only once ev.trigger() (ClUserEvent.cs:102-117).
   void gate(class UserEvent& ev, int device);
   void set_time_scale(int device, double scale);  // injected heterogeneity (tests/bench)
+  // injected fixed cost per compute on a device (ms of host time spent before
+  // its work, counted in its measured time): tests of the overhead-aware split
+  void set_time_offset(int device, double ms);
+  // Opt-in overhead-aware balancing (balancer.h predict_split): fits
+  // t = a + b·range per device and may leave a device out; single-process
+  // jobs only (the law stays the default and the distributed rule).
+  bool balancer_predictor = false;
+  const FitState* fit_state(int id) const {
+    auto it = state_.find(id);
+    return it == state_.end() ? nullptr : &it->second.fit;
+  }
   // ---- failure handling ----
   // A disabled device gets no range; the balancer runs over the others.
   void set_device_enabled(int device, bool on);
@@ -220,6 +238,7 @@ class Cores {
   struct TimelineSpan {
     int device, compute_id;
     double begin_ms, end_ms;
+    double abs_begin_ms, abs_end_ms;  // host clock (event_host_ms): comparable across devices
   };
   bool record_timeline = false;
   std::vector<TimelineSpan> timeline();
@@ -250,7 +269,16 @@ class Cores {
   // Keep-resident all-gather inside one process: every device's slice of
   // `a` (by the ranges of compute id `id`) is copied into every other
   // device's replica, GPU↔GPU as peer copies over xGMI (no host bounce).
+  // Event-ordered (no host sync in enqueue mode); later computes and
+  // downloads wait for the copies on the device.
   void share_slices(int id, const ArraySpec& a, long long local_range);
+  // ---- peer topology ----
+  // Distinct GPU ordinals of this Cores' devices and hipDeviceCanAccessPeer
+  // among them; access is enabled at construction when they span >= 2 GPUs.
+  const std::vector<int>& peer_ordinals() const { return peer_ordinals_; }
+  const std::vector<std::vector<int>>& peer_matrix() const { return peer_matrix_; }
+  const std::string& p2p_path() const { return p2p_path_; }
+  bool can_peer(int w1, int w2) const;  // local workers: same GPU, or peer access on
   void copy_between(int src_dev, const ArraySpec& src, int dst_dev, const ArraySpec& dst,
                     uint64_t bytes);  // device→device (peer/xGMI) copy, sync
 
@@ -339,15 +367,40 @@ class Cores {
     hipEvent_t pulled = nullptr;  // every other chunk pulled into this GPU
   };
   std::vector<PeerEvents> peer_ev_;
+  std::vector<hipEvent_t> peer_ready_;  // every participant pulled: kernels may modify the staged arrays
   std::vector<char> staged_arr_;  // by array index, for the current call
   std::vector<char> staged_dev_;  // by local worker, for the current call
   uint64_t stage_peer_reads(const ComputeCall& c, const std::vector<long long>& ranges,
                             std::vector<uint64_t>& h2d);
   int worker_index(const Worker& wk) const;
+  // peer topology
+  std::vector<int> peer_ordinals_;
+  std::vector<std::vector<int>> peer_matrix_;
+  std::string p2p_path_ = "none";
+  std::vector<int> ord_index_;  // local worker -> index into peer_ordinals_ (-1: CPU device)
+  void init_peer_topology();
+  // per-call device→device accounting
+  struct D2DCount {
+    uint64_t bytes = 0, xgmi = 0, local = 0, staged = 0;
+    bool pcie_fallback = false;
+  } d2d_;
+  void count_d2d(int ws, int wd, uint64_t bytes);
+  uint64_t d2d_copy(int ws, int wd, char* dst, const char* src, uint64_t bytes, hipStream_t s);
+  // keep-resident gather (ArraySpec::gather): kernels-done event per worker,
+  // copies-done event per GPU worker; later work waits on every copies-done
+  // event while gather_pending_
+  std::vector<hipEvent_t> kdone_, pushed_;
+  bool gather_pending_ = false;
+  bool all_gpu_ = true;  // every local device is a GPU (device-time spans feed the balancer)
+  bool call_gathers_ = false;  // the running call gathers in-process
+  hipEvent_t gather_event(std::vector<hipEvent_t>& v, int w);
+  void wait_gather(Worker& wk, hipStream_t s);
+  uint64_t issue_gather(const ComputeCall& c, const struct BalancerState& st, const std::vector<int>& arrays);
 
   std::vector<std::unique_ptr<Worker>> workers_;
   std::map<int, BalancerState> state_;
   std::vector<double> time_scale_;
+  std::vector<double> time_offset_;
   std::vector<bool> enabled_;
   // one compute()/state access at a time per Cores (Python releases the GIL
   // during compute, so two threads may call into the same cruncher)

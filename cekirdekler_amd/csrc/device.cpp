@@ -1,6 +1,8 @@
 #include "device.h"
 
 #include <fstream>
+#include <map>
+#include <mutex>
 #include <sstream>
 #include <thread>
 
@@ -106,25 +108,78 @@ std::vector<DeviceInfo> enumerate_devices() {
   return out;
 }
 
-std::vector<std::vector<int>> enable_peer_access() {
-  int n = gpu_count();
+std::vector<std::vector<int>> enable_peer_access_among(const std::vector<int>& ordinals) {
+  const int n = static_cast<int>(ordinals.size());
   std::vector<std::vector<int>> m(n, std::vector<int>(n, 0));
+  int cur = -1;
+  const bool restore = hipGetDevice(&cur) == hipSuccess;
   for (int i = 0; i < n; ++i) {
     for (int j = 0; j < n; ++j) {
-      if (i == j) {
+      if (ordinals[i] == ordinals[j]) {
         m[i][j] = 1;
         continue;
       }
       int can = 0;
-      if (hipDeviceCanAccessPeer(&can, i, j) == hipSuccess && can) {
-        CEK_HIP(hipSetDevice(i));
-        hipError_t e = hipDeviceEnablePeerAccess(j, 0);
+      if (hipDeviceCanAccessPeer(&can, ordinals[i], ordinals[j]) == hipSuccess && can) {
+        CEK_HIP(hipSetDevice(ordinals[i]));
+        hipError_t e = hipDeviceEnablePeerAccess(ordinals[j], 0);
         if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) m[i][j] = 1;
-        (void)hipGetLastError();
       }
+      (void)hipGetLastError();
     }
   }
+  if (restore && cur >= 0) (void)hipSetDevice(cur);
   return m;
+}
+
+std::vector<std::vector<int>> enable_peer_access() {
+  std::vector<int> all(gpu_count());
+  for (size_t i = 0; i < all.size(); ++i) all[i] = static_cast<int>(i);
+  return enable_peer_access_among(all);
+}
+
+std::string peer_path(const std::vector<std::vector<int>>& m) {
+  if (m.size() < 2) return "none";
+  for (size_t i = 0; i < m.size(); ++i)
+    for (size_t j = 0; j < m.size(); ++j)
+      if (!m[i][j] || !m[j][i]) return "staged";
+  return "xgmi";
+}
+
+namespace {
+struct Epoch {
+  hipEvent_t ev = nullptr;
+  double host_ms = 0;
+};
+std::mutex g_epoch_mu;
+std::map<int, Epoch> g_epochs;
+}  // namespace
+
+double event_host_ms(int ordinal, hipEvent_t ev) {
+  Epoch e;
+  {
+    std::lock_guard<std::mutex> g(g_epoch_mu);
+    auto it = g_epochs.find(ordinal);
+    if (it == g_epochs.end()) {
+      int cur = -1;
+      (void)hipGetDevice(&cur);
+      CEK_HIP(hipSetDevice(ordinal));
+      hipStream_t s;
+      CEK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      CEK_HIP(hipEventCreate(&e.ev));
+      CEK_HIP(hipEventRecord(e.ev, s));
+      CEK_HIP(hipEventSynchronize(e.ev));
+      e.host_ms = now_ms();
+      (void)hipStreamDestroy(s);
+      if (cur >= 0) (void)hipSetDevice(cur);
+      g_epochs[ordinal] = e;
+    } else {
+      e = it->second;
+    }
+  }
+  float ms = 0.f;
+  CEK_HIP(hipEventElapsedTime(&ms, e.ev, ev));
+  return e.host_ms + ms;
 }
 
 }  // namespace cek

@@ -40,5 +40,22 @@ DeviceInfo cpu_info(int threads = -1);
 
 // Peer access matrix between GPUs (xGMI); enables access where possible.
 std::vector<std::vector<int>> enable_peer_access();
+// The same among the given GPU ordinals only: m[i][j] = 1 when ordinals[i]
+// can access ordinals[j]'s memory (access enabled in both directions where
+// hipDeviceCanAccessPeer allows; the diagonal is 1).
+std::vector<std::vector<int>> enable_peer_access_among(const std::vector<int>& ordinals);
+// Device-to-device path of a device set from the peer matrix of its distinct
+// GPUs: "none" (at most one distinct GPU: copies stay inside one GPU),
+// "xgmi" (every pair peers: copies go over the xGMI links), "staged" (some
+// pair cannot peer: the runtime bounces those copies through host memory).
+std::string peer_path(const std::vector<std::vector<int>>& m);
+
+// Host-clock time (now_ms() scale) at which a completed timing event was
+// reached on GPU `ordinal`: each GPU's event clock is anchored once per
+// process to the host clock (an event recorded, synchronised, and the host
+// clock read right after; error ≈ the sync latency, tens of µs).  Puts
+// spans of different GPUs on one time line (overlap of copies with kernels
+// on other devices).
+double event_host_ms(int ordinal, hipEvent_t ev);
 
 }  // namespace cek

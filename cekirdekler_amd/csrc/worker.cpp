@@ -127,6 +127,22 @@ void Worker::set_capture_log(std::vector<std::pair<uint64_t, void*>>* log) {
   cap_log_ = log;
 }
 
+// A copy captured into a graph replays against the host pages it was
+// captured with; from pageable memory the runtime would stage it through a
+// bounce buffer at capture time, so the replay would not read (or write) the
+// array's current contents.  Only pinned / registered host memory may be
+// captured.
+void Worker::check_capturable(const ArraySpec& a) {
+  {
+    std::lock_guard<std::mutex> g(buf_mu_);
+    if (!cap_log_) return;
+  }
+  if (!host_is_pinned(a.host))
+    throw Error("graph capture: array " + std::to_string(a.uid) + " (" + std::to_string(a.bytes) +
+                " bytes) is pageable host memory; a captured copy needs pinned or registered memory "
+                "(use a FastArr-backed ClArray, or set ClArray.auto_pin_min_bytes below its size)");
+}
+
 bool Worker::buffer_is(uint64_t uid, const void* ptr) {
   std::lock_guard<std::mutex> g(buf_mu_);
   auto it = bufs_.find(uid);
@@ -331,6 +347,7 @@ int Worker::stream_slot(hipStream_t s) {
 
 void Worker::h2d(hipStream_t s, const ArraySpec& a, uint64_t elem_begin, uint64_t elem_count) {
   if (!gpu() || a.zc || elem_count == 0) return;
+  check_capturable(a);
   uint64_t off = elem_begin * a.elem_size, n = elem_count * a.elem_size;
   if (off >= a.bytes) return;
   if (off + n > a.bytes) n = a.bytes - off;
@@ -340,6 +357,7 @@ void Worker::h2d(hipStream_t s, const ArraySpec& a, uint64_t elem_begin, uint64_
 
 void Worker::d2h(hipStream_t s, const ArraySpec& a, uint64_t elem_begin, uint64_t elem_count) {
   if (!gpu() || a.zc || elem_count == 0) return;
+  check_capturable(a);
   uint64_t off = elem_begin * a.elem_size, n = elem_count * a.elem_size;
   if (off >= a.bytes) return;
   if (off + n > a.bytes) n = a.bytes - off;

@@ -37,6 +37,11 @@ struct ArraySpec {
   bool write_all = false; // device (index mod D) D2H the whole array
   bool ro = false, wo = false;  // access hints
   bool zc = false;        // zero-copy: kernel reads/writes host memory
+  // keep-resident gather: after the kernels, every device's written slice
+  // is copied into every other device's replica (event-ordered device→device
+  // copies over xGMI in one process, an RCCL all-gather across ranks), so an
+  // iterative kernel reads everybody's results without a host round trip
+  bool gather = false;
   int epw = 1;            // elements per work item
   int epg = 0;            // >0: elements per work-GROUP instead (per-group outputs)
   // Element slice [begin, begin+count) owned by work items [ref, ref+range).
@@ -179,6 +184,7 @@ class Worker {
   std::atomic<uint64_t> kernel_d2h_bytes_{0};
   bool d2h_by_kernel(hipStream_t s, void* host_base, uint64_t off, const void* src_dev, uint64_t n);
   void* buffer_impl(const ArraySpec& a);
+  void check_capturable(const ArraySpec& a);  // throws for pageable memory while capturing
   void check_guards(hipStream_t s, const std::string& kernel, const std::vector<ArraySpec>& arrs);
   uint64_t bytes_allocated_ = 0;
   std::mutex buf_mu_;

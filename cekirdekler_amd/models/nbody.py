@@ -5,8 +5,9 @@ runs the force kernel and the kick-drift kernel on the same balanced range.  Eve
 force pass, so after each step the position slices are made coherent again:
 
 * ``resident=True`` (MI355X-native): positions stay in device memory and each
-  device's updated slice is copied into the other devices' replicas
-  (:meth:`Cores.share_slices`: GPU↔GPU peer copies over xGMI);
+  device's updated slice is copied into the other devices' replicas by the
+  keep-resident gather flag (``ClArray.gather_resident``: event-ordered
+  GPU↔GPU peer copies over xGMI inside the compute, no host sync);
 * ``resident=False`` (reference semantics, Tester.cs:7759-7765): slices go
   device→host and the whole array host→device on the next step.
 """
@@ -78,6 +79,7 @@ class NBodySimulation:
         # positions: every device reads all of them
         self.pos.read = first or not self.resident
         self.pos.write = not self.resident
+        self.pos.gather_resident = self.resident
         self.vel.partial_read = not self.resident or first
         self.vel.read = False
         self.vel.write = not self.resident
@@ -89,6 +91,7 @@ class NBodySimulation:
         """Accelerations only (no integration)."""
         self._flags()
         self.pos.write = False
+        self.pos.gather_resident = False
         self.acc.write = True
         self.pos.next_param(self.vel, self.acc, self.params).compute(self.cr, compute_id, self.k_force,
                                                                     self.n // self.bpw, L)
@@ -99,13 +102,11 @@ class NBodySimulation:
         self._flags()
         self.pos.next_param(self.vel, self.acc, self.params).compute(
             self.cr, compute_id, f"{self.k_force} {self.k_integrate}", self.n // self.bpw, L)
-        if self.resident and self.cr.cores.num_devices > 1:
-            self.cr.cores.share_slices(compute_id, self.pos._spec(), L)
         self.steps += 1
 
     def download(self) -> None:
         """Bring device-resident state to the host (device 0 holds every
-        slice of pos after share_slices; vel/acc slices per device)."""
+        slice of pos after the gather; vel/acc slices per device)."""
         if not self.resident:
             return  # host arrays already hold every slice
         c = self.cr.cores

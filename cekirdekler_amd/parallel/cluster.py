@@ -494,7 +494,7 @@ class ClusterAccelerator(IComputeNode):
             self.mainframe = Cores(mainframe_types, kernels, names, False, local_range, num_gpus, stream, max_cpu)
         self.local_range = local_range
 
-    setupNodes = setup_cluster
+    setupNodes = setup_nodes  # both call forms: device string or explicit (host, port) list
 
     def compute(self, kernel_names: str, steps: int, step_fn: str, arrays, read_writes, epw,
                 global_range: int, compute_id: int, global_offset: int = 0, pipeline: bool = False,

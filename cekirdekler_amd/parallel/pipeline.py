@@ -334,6 +334,54 @@ class ClPipeline:
     def elapsed_times(self) -> List[float]:
         return [s.elapsed_time for s in self.stages]
 
+    # ---- measured overlap (stage kernels vs stage-transition copies) ---------
+    @property
+    def record_timeline(self) -> bool:
+        return bool(self.engine.record_timeline)
+
+    @record_timeline.setter
+    def record_timeline(self, on: bool) -> None:
+        """Time every stage's kernels (hipEvents on each device) and every
+        copy of the stage transitions (hipEvents on the copy streams), all
+        on one host-anchored clock."""
+        self.engine.record_timeline = bool(on)
+        for st in self.stages:
+            st.cruncher.record_timeline = bool(on)
+
+    def timeline(self) -> dict:
+        """``{"kernels": [(stage, device, begin, end)], "copies": [(kind,
+        device, bytes, begin, end)]}`` in host-clock ms since the first
+        recorded event; waits for the recorded work and clears it."""
+        ks = [(i, t["device"], t["abs_begin_ms"], t["abs_end_ms"])
+              for i, st in enumerate(self.stages) for t in st.cruncher.timeline()]
+        cs = [(c["kind"], c["device"], c["bytes"], c["abs_begin_ms"], c["abs_end_ms"]) for c in self.engine.timeline()]
+        t0 = min([k[2] for k in ks] + [c[3] for c in cs], default=0.0)
+        return {"kernels": [(i, d, b - t0, e - t0) for i, d, b, e in ks],
+                "copies": [(k, d, n, b - t0, e - t0) for k, d, n, b, e in cs]}
+
+    @staticmethod
+    def copy_overlap(tl: dict, stage: Optional[int] = None) -> dict:
+        """How much of the stage-transition copy time ran while kernels of
+        ``stage`` (default: every stage) were executing: ``copy_ms`` (busy
+        time of the copies, union), ``hidden_ms`` and ``fraction`` =
+        hidden / copy (1.0: transfers fully overlapped with compute)."""
+        ks = [(b, e) for i, _, b, e in tl["kernels"] if stage is None or i == stage]
+        cs = [(b, e) for _, _, _, b, e in tl["copies"]]
+        copy_ms = _coverage(cs)[0]
+        # hidden = |union(copies) ∩ union(kernels)|
+        union, cur = [], None
+        for b, e in sorted(cs):
+            if cur and b <= cur[1]:
+                cur[1] = max(cur[1], e)
+            else:
+                if cur:
+                    union.append(tuple(cur))
+                cur = [b, e]
+        if cur:
+            union.append(tuple(cur))
+        hidden = sum(_intersection(b, e, ks) for b, e in union)
+        return {"copy_ms": copy_ms, "hidden_ms": hidden, "fraction": hidden / copy_ms if copy_ms > 0 else 1.0}
+
     def dispose(self) -> None:
         self._pool.shutdown(wait=True)
         for s in self.stages:

@@ -1,0 +1,107 @@
+"""Opt-in overhead-aware balancing (``ClNumberCruncher.overhead_aware_balancer``,
+native ``predict_split``) against simulated and real fixed costs.  The
+reference law (HelperFunctions.cs:190-280) assumes time ∝ range; a device with
+a large fixed cost per compute keeps a share under it.  The predictor fits
+t = a + b·r and may leave that device out.  The law itself stays the default
+(tests/test_balancer.py checks it is unchanged)."""
+import numpy as np
+import pytest
+
+import cekirdekler_amd as ck
+from cekirdekler_amd._native import cek
+
+
+def _simulate(a, b, o_multi, o_single, G=102_400, step=256, calls=40, predictor=True, noise=0.0, seed=0):
+    """Run the balancer against devices whose time is a_i + b_i·r_i (ms) and a
+    compute whose wall time adds o_multi (≥ 2 devices) or o_single (1)."""
+    rng = np.random.default_rng(seed)
+    n = len(a)
+    hist = [[0.0] * n for _ in range(cek.HISTORY_DEPTH)]
+    ranges, hist = cek.initial_split(n, True, hist, G, step)
+    fs = cek.FitState()
+    walls, decisions = [], []
+    for _ in range(calls):
+        t = [(a[i] + b[i] * r) * (1 + noise * rng.standard_normal()) if r > 0 else 0.0 for i, r in enumerate(ranges)]
+        k = sum(1 for r in ranges if r > 0)
+        wall = max(t) + (o_multi if k >= 2 else o_single)
+        walls.append(wall)
+        if predictor:
+            ok, new, dec = cek.predict_split(t, wall, G, list(ranges), step, fs)
+            decisions.append(dec)
+            if ok:
+                ranges = new
+                continue
+        ranges, hist = cek.load_balance(t, True, hist, G, list(ranges), step)
+    return ranges, walls, decisions, fs
+
+
+def test_single_device_wins_over_a_costly_second_device():
+    a, b = [0.05, 9.0], [1e-4, 5e-5]
+    ranges, walls, dec, fs = _simulate(a, b, o_multi=2.0, o_single=0.1)
+    assert ranges == [102_400, 0], ranges
+    assert dec[-1] == "single"
+    assert walls[-1] == pytest.approx(0.05 + 10.24 + 0.1)
+    law, lwalls, _, _ = _simulate(a, b, 2.0, 0.1, predictor=False)
+    assert law[1] > 0 and min(lwalls[-5:]) > walls[-1]  # the law keeps the slow device and loses
+
+
+def test_water_filling_split_when_both_pay_off():
+    a, b = [0.05, 2.0], [1e-4, 5e-5]
+    ranges, walls, dec, fs = _simulate(a, b, o_multi=0.5, o_single=0.1)
+    assert dec[-1] == "multi"
+    T = (102_400 + 0.05 / 1e-4 + 2.0 / 5e-5) / (1 / 1e-4 + 1 / 5e-5)
+    assert abs(ranges[0] - (T - 0.05) / 1e-4) <= 512 and sum(ranges) == 102_400
+    assert fs.a[1] == pytest.approx(2.0, rel=1e-6) and fs.b[0] == pytest.approx(1e-4, rel=1e-6)
+    assert walls[-1] == pytest.approx(T + 0.5, rel=0.01)
+
+
+def test_three_devices_drop_only_the_one_that_does_not_pay():
+    a, b = [0.1, 0.1, 30.0], [1e-4, 1e-4, 1e-4]
+    ranges, walls, dec, _ = _simulate(a, b, o_multi=0.2, o_single=0.1)
+    assert ranges[2] == 0 and ranges[0] > 0 and ranges[1] > 0, ranges
+    assert abs(ranges[0] - ranges[1]) <= 256
+
+
+def test_noisy_timings_stay_near_the_optimum():
+    a, b = [0.05, 2.0], [1e-4, 5e-5]
+    _, walls, _, _ = _simulate(a, b, 0.5, 0.1, calls=60, noise=0.02, seed=3)
+    T = (102_400 + 0.05 / 1e-4 + 2.0 / 5e-5) / (1 / 1e-4 + 1 / 5e-5)
+    assert np.median(walls[-20:]) < 1.08 * (T + 0.5)
+
+
+def test_law_until_every_device_has_two_ranges():
+    fs = cek.FitState()
+    ok, r, dec = cek.predict_split([1.0, 1.0], 1.2, 4096, [2048, 2048], 256, fs)
+    assert not ok and dec == "law"
+
+
+SRC = """__global__ void k(float* x) { long long i = get_global_id(0); float v = x[i];
+    for (int j = 0; j < 64; ++j) v = v * 0.999f + 1.0f; x[i] = v; }"""
+
+
+def test_cores_drops_a_device_with_an_injected_fixed_cost():
+    """Two CPU devices; device 1 pays 25 ms per compute.  With the predictor
+    the compute ends up on device 0 alone and runs faster than under the law."""
+    cpu = ck.ClPlatforms.all().cpus(True)
+    n = 1 << 16
+
+    def run(predict):
+        cr = ck.ClNumberCruncher(cpu + cpu, SRC)
+        cr.set_time_offset(1, 25.0)
+        cr.overhead_aware_balancer = predict
+        x = ck.ClArray(np.zeros(n, np.float32))
+        walls = []
+        for _ in range(24):
+            x.compute(cr, 1, "k", n, 256)
+            walls.append(cr.last_record()["wall_ms"])
+        info = cr.balancer_predictor_info(1)
+        r = cr.ranges(1)
+        cr.dispose()
+        return r, walls, info
+
+    r_law, w_law, _ = run(False)
+    r_fit, w_fit, info = run(True)
+    assert r_law[1] > 0
+    assert r_fit == [n, 0], (r_fit, info)
+    assert info["decision"] in ("single", "probe")
+    assert np.median(w_fit[-5:]) < np.median(w_law[-5:]) - 10.0, (w_fit[-5:], w_law[-5:])
