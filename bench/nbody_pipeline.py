@@ -237,7 +237,9 @@ emit({"config": "nbody_pipeline_3stage", "n": n, "systems_in_flight": M, "gpus_u
       "stage_gpus": [len(d) if hasattr(d, "__len__") else 1 for d in devs], "push_ms_median": ms,
       "stage_device_ms": stage_ms, "ready_after_pushes": ready_at,
       "interactions_per_s": n * n / (ms * 1e-3), "tflops_20flop": 20 * n * n / (ms * 1e-3) / 1e12,
-      "force_stage_pct_fp32_peak": 100 * 20 * n * n / (stage_ms[0] * 1e-3) / 1e12 / FP32_PEAK_TFLOPS / len(devs[0]),
+      # per PHYSICAL GPU of the force stage (logical devices of one GPU share it)
+      "force_stage_pct_fp32_peak": 100 * 20 * n * n / (stage_ms[0] * 1e-3) / 1e12 / FP32_PEAK_TFLOPS
+      / len({devs[0].device(k).info.ordinal for k in range(len(devs[0]))}),
       "overlap_efficiency": max(stage_ms) / ms, "serial_over_push": sum(stage_ms) / ms,
       "steps_per_system": steps, "step_check_max_rel_err": check,
       "logical_rehearsal": a.logical > 1, "placement": [[d.device(k).name + f"#{d.device(k).info.ordinal}"

@@ -82,19 +82,25 @@ static void quantize_fix(std::vector<long long>& ranges, const std::vector<doubl
 }
 
 bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_ms, long long total,
-                   std::vector<long long>& ranges, long long step) {
+                   std::vector<long long>& ranges, long long step, bool warm) {
   const size_t n = ranges.size();
   if (n == 0) return false;
   if (step <= 0) step = 1;
-  if (fs.samples.size() != n) fs.samples.assign(n, {});
+  if (fs.samples.size() != n) {
+    fs.samples.assign(n, {});
+    fs.single_wall.assign(n, -1.0);
+    fs.probed.assign(n, 0);
+  }
   // 1) record this compute: a sample per computing device, keyed by range
   //    (a repeated range refreshes its time: an EWMA, so old noise fades)
-  int active = 0;
+  int active = 0, alone = -1;
   double tmax = 0;
   for (size_t i = 0; i < n; ++i) {
     if (ranges[i] <= 0 || i >= bench.size() || bench[i] <= 0) continue;
     ++active;
+    alone = static_cast<int>(i);
     tmax = std::max(tmax, bench[i]);
+    if (!warm) continue;
     auto& v = fs.samples[i];
     const double r = static_cast<double>(ranges[i]);
     auto it = std::find_if(v.begin(), v.end(), [&](const std::pair<double, double>& p) {
@@ -107,10 +113,14 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
       if (static_cast<int>(v.size()) > kFitSamples) v.erase(v.begin());
     }
   }
-  if (active > 0 && wall_ms > 0) {
-    const double ov = std::max(0.0, wall_ms - tmax);
-    double& o = active >= 2 ? fs.o_multi : fs.o_single;
-    o = o < 0 ? ov : 0.7 * o + 0.3 * ov;
+  if (warm && active > 0 && wall_ms > 0) {
+    if (active >= 2) {
+      const double ov = std::max(0.0, wall_ms - tmax);
+      fs.o_multi = fs.o_multi < 0 ? ov : 0.7 * fs.o_multi + 0.3 * ov;
+    } else {
+      double& w = fs.single_wall[alone];
+      w = w < 0 ? wall_ms : 0.5 * w + 0.5 * wall_ms;
+    }
   }
   // 2) fits t = a + b·r (least squares over distinct ranges)
   fs.a.assign(n, 0.0);
@@ -169,29 +179,35 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
   }
   int kept = 0;
   for (char c : keep) kept += c;
-  size_t best = 0;  // the best single device
+  size_t best = 0;  // the best single device by its fit
   for (size_t i = 1; i < n; ++i)
     if (fs.a[i] + fs.b[i] * total < fs.a[best] + fs.b[best] * total) best = i;
-  const double single_dev = fs.a[best] + fs.b[best] * static_cast<double>(total);
-  std::vector<double> target(n, 0.0);
+  const double pred_multi = T + std::max(0.0, fs.o_multi);
+  fs.predicted_multi_ms = pred_multi;
+  // 4) single device or split: the single device's MEASURED wall time against
+  //    the split's predicted one (a probe measures it, once)
   bool single = kept < 2;
   if (!single) {
-    const double om = fs.o_multi >= 0 ? fs.o_multi : 0.0;
-    if (fs.o_single < 0) {
-      // the single-device overhead is unknown: probe it once when it could win
-      if (!fs.probed && single_dev <= 1.25 * (T + om)) {
-        fs.probed = true;
-        fs.probe_left = 3;
+    if (fs.probe_left > 0) {
+      single = true;
+      best = static_cast<size_t>(fs.probe_dev);
+    } else if (fs.single_wall[best] < 0) {
+      const double guess = fs.a[best] + fs.b[best] * static_cast<double>(total);
+      if (!fs.probed[best] && guess <= 1.25 * pred_multi) {
+        fs.probed[best] = 1;
+        fs.probe_left = kProbeCalls;
+        fs.probe_dev = static_cast<int>(best);
+        single = true;
       }
-      single = fs.probe_left > 0;
     } else {
-      single = single_dev + fs.o_single <= T + om;
+      single = fs.single_wall[best] <= pred_multi;
     }
   }
-  if (fs.probe_left > 0) --fs.probe_left;
+  std::vector<double> target(n, 0.0);
   if (single) {
     target[best] = static_cast<double>(total);
-    fs.decision = fs.o_single < 0 ? "probe" : "single";
+    fs.decision = fs.probe_left > 0 ? "probe" : "single";
+    if (fs.probe_left > 0) --fs.probe_left;
   } else {
     for (size_t i = 0; i < n; ++i)
       if (keep[i]) target[i] = (T - fs.a[i]) / fs.b[i];

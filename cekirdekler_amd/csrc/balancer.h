@@ -17,27 +17,35 @@ namespace cek {
 // cost per compute (launch + sync latency, host-thread fan-out) keeps a share
 // that makes the compute slower than leaving it out.  The predictor fits
 // t_i = a_i + b_i·r_i per device from the (range, time) samples of this
-// compute id, splits by water-filling (equal predicted finish time; a device
-// whose best share is below one step gets none), and compares that split with
-// the best single device using the measured per-compute overhead of multi- and
-// single-device computes (wall time − slowest device), probing the single
-// device once to learn it.  Until every device has a fit it defers to the law.
+// compute id (warm calls only: the first computes of an id allocate and
+// upload), splits by water-filling (equal predicted finish time; a device
+// whose best share is below one step gets none) and predicts that split's
+// wall time as T + the measured multi-device overhead (wall − slowest
+// device).  The best single device is then run alone for a few calls, once,
+// when its predicted time is within 25 % of that, and from then on the
+// configuration with the lower wall time — measured for the single device,
+// predicted for the split — is used.  Until every device has a fit it defers
+// to the law.
 struct FitState {
   std::vector<std::vector<std::pair<double, double>>> samples;  // per device: (range, ms), distinct ranges
-  double o_multi = -1, o_single = -1;  // EWMA of wall − max device ms (−1: not measured)
-  int probe_left = 0;                  // computes left in a single-device probe
-  bool probed = false;
+  double o_multi = -1;                 // EWMA of wall − max device ms over multi-device calls
+  std::vector<double> single_wall;     // per device: EWMA wall ms of calls it ran alone (−1: never)
+  std::vector<char> probed;
+  int probe_left = 0, probe_dev = -1;
   std::string decision = "law";        // law | multi | single | probe
   std::vector<double> a, b;            // last fits (ms, ms per work item)
+  double predicted_multi_ms = 0;
 };
 
 constexpr int kFitSamples = 8;
+constexpr int kProbeCalls = 3;
 
-// Records the last compute of this id (its ranges, per-device ms and wall ms)
-// and, when every device has a fit, writes the next split into `ranges`
-// (returns true); false = apply the reference law instead.
+// Records the last compute of this id (its ranges, per-device ms and wall ms;
+// `warm` = not one of the id's first computes) and, when every device has a
+// fit, writes the next split into `ranges` (returns true); false = apply the
+// reference law instead.
 bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_ms, long long total,
-                   std::vector<long long>& ranges, long long step);
+                   std::vector<long long>& ranges, long long step, bool warm = true);
 
 struct BalancerState {
   std::vector<long long> ranges;      // work-items per device

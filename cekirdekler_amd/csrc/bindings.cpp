@@ -172,19 +172,21 @@ PYBIND11_MODULE(_cek, m) {
     return py::make_tuple(ranges, history);
   });
   m.def("predict_split", [](std::vector<double> bench, double wall, long long total, std::vector<long long> ranges,
-                            long long step, py::object state) {
-    // pure form for tests: `state` is an opaque capsule from new_fit_state()
+                            long long step, py::object state, bool warm) {
+    // pure form for tests: `state` is a FitState
     auto* fs = state.cast<FitState*>();
-    bool ok = predict_split(*fs, bench, wall, total, ranges, step);
+    bool ok = predict_split(*fs, bench, wall, total, ranges, step, warm);
     return py::make_tuple(ok, ranges, fs->decision);
-  });
+  }, py::arg("bench"), py::arg("wall"), py::arg("total"), py::arg("ranges"), py::arg("step"), py::arg("state"),
+     py::arg("warm") = true);
   py::class_<FitState>(m, "FitState")
       .def(py::init<>())
       .def_readonly("decision", &FitState::decision)
       .def_readonly("a", &FitState::a)
       .def_readonly("b", &FitState::b)
       .def_readonly("o_multi", &FitState::o_multi)
-      .def_readonly("o_single", &FitState::o_single);
+      .def_readonly("single_wall", &FitState::single_wall)
+      .def_readonly("predicted_multi_ms", &FitState::predicted_multi_ms);
   m.def("initial_split", [](int devices, bool smooth, std::vector<std::vector<double>> history,
                             long long total, long long step) {
     std::vector<long long> ranges;
@@ -364,7 +366,8 @@ PYBIND11_MODULE(_cek, m) {
         d["a_ms"] = f->a;
         d["b_ms_per_item"] = f->b;
         d["o_multi_ms"] = f->o_multi;
-        d["o_single_ms"] = f->o_single;
+        d["single_wall_ms"] = f->single_wall;
+        d["predicted_multi_ms"] = f->predicted_multi_ms;
         return d;
       })
       .def("set_dynamic_lds", &Cores::set_dynamic_lds)

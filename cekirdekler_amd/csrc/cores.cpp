@@ -306,7 +306,7 @@ void Cores::balance(BalancerState& st, bool first, long long G, long long step) 
   if (static_cast<int>(on.size()) == D) {
     if (first)
       initial_split(D, smooth, st.history, G, st.ranges, step);
-    else if (!(balancer_predictor && !ex_ && predict_split(st.fit, st.bench, st.last_wall_ms, G, st.ranges, step)))
+    else if (!(balancer_predictor && !ex_ && predict_split(st.fit, st.bench, st.last_wall_ms, G, st.ranges, step, st.calls >= 2)))
       load_balance(st.bench, smooth, st.history, G, st.ranges, step);
     return;
   }
