@@ -371,7 +371,8 @@ def bench_node_configs(world: int) -> dict:
                         "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
     out = {}
     rccl = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "rccl_gemm.py"]
+            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "rccl_gemm.py",
+            "--expect-world", str(world)]
     import torch
 
     # config 4 is specified on 4 GPUs (2 + 1 + 1 placement); on fewer GPUs the

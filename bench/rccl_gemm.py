@@ -28,8 +28,11 @@ from cekirdekler_amd.parallel.distributed import DistributedCruncher, init_distr
 ap = argparse.ArgumentParser()
 ap.add_argument("--size", type=int, default=8192)
 ap.add_argument("--steps", type=int, default=4)
+ap.add_argument("--expect-world", type=int, default=0, help="fail unless the job has exactly this many ranks")
 a = ap.parse_args()
 ctx = init_distributed()
+if a.expect_world and ctx.world != a.expect_world:
+    raise SystemExit(f"rccl_gemm.py: expected {a.expect_world} ranks, the job has {ctx.world}")
 import torch.distributed as dist  # noqa: E402
 
 size = a.size
@@ -85,15 +88,20 @@ for r in range(ctx.world):
     if n:
         picks += [lo, lo + n - 1]
 err_gather = max(tile_err(g.C.array, t) for t in picks)
-errs = [(err_split, err_gather, ms, rec["h2d_bytes"])]
+rec6 = cr.last_record()
+mine = (err_split, err_gather, ms, rec["h2d_bytes"], rec["d2h_bytes"], rec6["h2d_bytes"], rec6["d2h_bytes"])
+errs = [mine]
 if ctx.is_distributed:
     errs = [None] * ctx.world
-    dist.all_gather_object(errs, (err_split, err_gather, ms, rec["h2d_bytes"]))
+    dist.all_gather_object(errs, mine)
 if ctx.rank == 0:
     print(json.dumps({"config": "sgemm_host_resident_rccl", "ranks": ctx.world, "size": size,
                       "split_reads_ms": max(e[2] for e in errs),
                       "split_reads_tflops": 2 * size ** 3 / (max(e[2] for e in errs) * 1e-3) / 1e12,
                       "h2d_bytes_per_rank": [e[3] for e in errs],
+                      "d2h_bytes_per_rank": [e[4] for e in errs],
+                      "gather_call_h2d_bytes_per_rank": [e[5] for e in errs],
+                      "gather_call_d2h_bytes_per_rank": [e[6] for e in errs],
                       "max_rel_err_split_reads": max(e[0] for e in errs),
                       "max_rel_err_gathered_replicas": max(e[1] for e in errs)}), flush=True)
 cr.dispose()

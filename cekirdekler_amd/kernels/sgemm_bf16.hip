@@ -25,31 +25,24 @@
 
 namespace {
 
-template <int WM, int WN, int FM, int FN, int MODE, bool SK = false, bool NOSTORE = false, int XCH = 0,
-          bool NTS = false>
+template <int WM, int WN, int FM, int FN, int MODE, bool SK = false, int XCH = 0>
 __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
                                           const uint16_t* __restrict__ A,
                                           const uint16_t* __restrict__ Bt, float* __restrict__ C,
                                           char* smem, long long off, float* __restrict__ W = nullptr,
                                           int* __restrict__ tile_cnt = nullptr) {
   constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN, BK = 64;
-  // MODE 8: two waves per output region (one per SIMD pair slot), each
-  // multiplying one 32-wide K half of every K-tile; summed through LDS at
-  // the end (an in-CU split-K: the four-wave layout's fragment traffic with
-  // two waves per SIMD to hide latency)
   constexpr int NREG = WM * WN;
-  constexpr int NWAVES = (MODE >= 8 ? 2 : 1) * NREG, NT = 64 * NWAVES;
+  constexpr int NWAVES = NREG, NT = 64 * NWAVES;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  // MODE 0: one LDS stage in flight, all waves stage; MODE 1: + register
-  // double-buffered fragments; MODE 2: ping-pong — the two halves of the
-  // work-group (waves < NWAVES/2 = G0, the rest = G1, one of each per SIMD)
-  // alternate between an LDS-read section and an MFMA section, one
-  // s_barrier apart, so each SIMD's matrix pipe always has one wave issuing;
-  // G0 also issues all LDS-DMA staging.  MODE 3: ping-pong with the DMA
-  // split — G0 stages the A tile during its read section, G1 stages the B
-  // tile of the K-tile after next at the start of its MFMA section, so each
-  // DMA has ~1.5 sections to land.
-  constexpr int STAGERS = ((MODE >= 2 && MODE < 7) || MODE == 10) ? NWAVES / 2 : NWAVES;  // MODE 7-9: every wave stages
+  // MODE 0: one LDS stage in flight, all waves stage.  MODE 2: ping-pong —
+  // the two halves of the work-group (waves < NWAVES/2 = G0, the rest = G1,
+  // one of each per SIMD) alternate between an LDS-read section and an
+  // MFMA section, one s_barrier apart, so each SIMD's matrix pipe always has
+  // one wave issuing; G0 issues all LDS-DMA staging.  MODE 4: ping-pong with
+  // balanced DMA (G0 stages A, G1 stages Bt two K-tiles ahead).  MODE 6:
+  // ping-pong with the K-tile's DMA split evenly by 1 KiB chunk, three stages.
+  constexpr int STAGERS = MODE >= 2 ? NWAVES / 2 : NWAVES;
   constexpr int A_INSTR = A_BYTES / 1024 / STAGERS;
   constexpr int B_INSTR = B_BYTES / 1024 / STAGERS;
 
@@ -84,7 +77,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
   // per-lane 32-bit byte offset + wave-uniform 64-bit base (saddr form)
   const unsigned lane_off = (unsigned)(lrow * K + lchunk * 8) * 2u;
-  const int sw = ((MODE >= 2 && MODE < 7) || MODE == 10) ? wave % (NWAVES / 2) : wave;  // staging wave index
+  const int sw = MODE >= 2 ? wave % (NWAVES / 2) : wave;  // staging wave index
   const char* a_wave = (const char*)(A + (size_t)(m0 + sw * A_INSTR * 8) * K);
   const char* b_wave = (const char*)(Bt + (size_t)(n0 + sw * B_INSTR * 8) * K);
 
@@ -130,7 +123,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 
   const int nk = K / BK / S;
   unsigned my_xcc = 0;
-  if constexpr (XCH == 2 || XCH == 5 || XCH == 6) {
+  if constexpr (XCH == 2) {
     // publish this work-group's XCD for the partner split (flags[4t + 2 + s])
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(my_xcc));
     my_xcc &= 15u;
@@ -160,192 +153,6 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  } else if constexpr (MODE == 8) {
-    const int s = wave / NREG;  // this wave's K half of every K-tile
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
-      const char* base = smem + cur * STAGE;
-      bf16x8 a[FM], b[FN];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) b[j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  } else if constexpr (MODE == 10) {
-    // MODE 2's ping-pong on the in-CU split-K: G0 (waves < NREG) multiplies
-    // K half 0 of every K-tile and G1 K half 1 of the same regions, so one
-    // group reads its half's fragments while the other multiplies; G0
-    // stages each next K-tile during its read section.  Same barrier
-    // sequence as MODE 2.
-    const bool g1 = wave >= NREG;
-    const int s = g1 ? 1 : 0;
-    bf16x8 fa[FM], fb[FN];
-    auto bar = [] {
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    if (!g1) stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    if (g1) bar();  // stagger G1 by one section
-    for (int kt = 0; kt < nk; ++kt) {
-      const char* base = smem + (kt & 1) * STAGE;
-      if (!g1 && kt + 1 < nk) stage((kt + 1) & 1, kt + 1);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) fb[j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) fa[i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      bar();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      if (!g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      bar();
-    }
-    if (!g1) bar();  // equal barrier counts for both groups
-    __syncthreads();  // both groups done with LDS before the reduction reuses it
-  } else if constexpr (MODE == 9) {
-    // MODE 8 with a three-stage LDS ring: K-tile kt + 2 is issued while kt
-    // computes, and the barrier waits only for kt + 1 (the newest stage's
-    // A_INSTR + B_INSTR loads stay in flight)
-    const int s = wave / NREG;
-    constexpr int NEWEST = A_INSTR + B_INSTR;
-    stage(0, 0);
-    if (nk > 1) stage(1, 1);
-    if (nk > 1)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NEWEST) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt % 3;
-      const bool more = kt + 2 < nk;
-      if (more) stage((kt + 2) % 3, kt + 2);
-      const char* base = smem + cur * STAGE;
-      bf16x8 a[FM], b[FN];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) b[j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      if (more)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NEWEST) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  } else if constexpr (MODE == 1) {
-    // Register double-buffered fragments: k-step 1 of the current K-tile is
-    // read from LDS while k-step 0's MFMAs run, and k-step 0 of the next
-    // K-tile is read (right after the barrier that publishes its DMA) while
-    // k-step 1's MFMAs run — LDS latency hides under MFMA issue.
-    bf16x8 xa[FM], xb[FN], ya[FM], yb[FN];
-    auto ld = [&](bf16x8(&a)[FM], bf16x8(&b)[FN], const char* base, int s) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) b[j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
-    };
-    auto mma = [&](const bf16x8(&a)[FM], const bf16x8(&b)[FN]) {
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    };
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    ld(xa, xb, smem, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      const char* base = smem + cur * STAGE;
-      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
-      ld(ya, yb, base, 1);
-      mma(xa, xb);
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (kt + 1 < nk) ld(xa, xb, smem + (cur ^ 1) * STAGE, 0);
-      mma(ya, yb);
-    }
-  } else if constexpr (MODE == 7) {
-    // Both k-steps' fragments read up front, the next K-tile's LDS-DMA
-    // pieces issued one at a time between the (k-step, row-block) MFMA
-    // groups, spread evenly, so their issue cost lands between MFMAs of
-    // this wave (the other wave on the SIMD keeps the matrix pipe busy)
-    // instead of in front of them; one vmcnt(0) + barrier per K-tile.
-    constexpr int NP = A_INSTR + B_INSTR, NG = 2 * FM;
-    bf16x8 fa[2][FM], fb[2][FN];
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      const char* base = smem + cur * STAGE;
-      const bool pre = kt + 1 < nk;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j) fb[s2][j] = *(const bf16x8*)(base + b_off[s2] + j * 2048);
-#pragma unroll
-        for (int i = 0; i < FM; ++i) fa[s2][i] = *(const bf16x8*)(base + a_off[s2] + i * 2048);
-      }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        if (pre) {
-#pragma unroll
-          for (int p = 0; p < NP; ++p) {
-            if ((p * NG) / NP != g) continue;  // piece p goes to group p·NG/NP
-            char* sb = smem + (cur ^ 1) * STAGE;
-            if (p < A_INSTR) {
-              const char* src = a_wave + ((size_t)p * 8 * K + (size_t)(ks + kt + 1) * BK) * 2;
-              __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
-                                               (lds_void*)(sb + (sw * A_INSTR + p) * 1024), 16, 0, 0);
-            } else {
-              const int q = p - A_INSTR;
-              const char* src = b_wave + ((size_t)q * 8 * K + (size_t)(ks + kt + 1) * BK) * 2;
-              __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
-                                               (lds_void*)(sb + A_BYTES + (sw * B_INSTR + q) * 1024), 16, 0, 0);
-            }
-          }
-        }
-        const int s2 = g / FM, i = g % FM;
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s2][i], fb[s2][j], acc[i][j], 0, 0, 0);
-      }
-      __builtin_amdgcn_s_setprio(0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -487,7 +294,8 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       bar();
     }
     if (!g1) bar();  // equal barrier counts for both groups
-  } else if constexpr (MODE == 4 || MODE == 5) {
+  } else {
+    static_assert(MODE == 4, "MODE is 0, 2, 4 or 6");
     // Ping-pong with balanced DMA: G0 stages the A tile of K-tile k+1 and G1
     // the Bt tile of K-tile k+2, each during its own LDS-read section, so both
     // groups' read sections carry the same DMA issue cost (~60-100 cycles per
@@ -556,13 +364,12 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     if (g1) bar();  // G1 runs one section behind
     for (int kt = 0; kt < nk; ++kt) {
       const bool b_issued = g1 && kt + 2 < nk;
-      if constexpr (MODE == 5) ldall(kt);  // reads first: their latency hides under the DMA issue
       if (!g1) {
         if (kt + 1 < nk) stage_a4(kt + 1);
       } else if (b_issued) {
         stage_b4(kt + 2);
       }
-      if constexpr (MODE == 4) ldall(kt);
+      ldall(kt);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (g1) {
         if (b_issued) {
@@ -582,57 +389,6 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       bar();
     }
     if (!g1) bar();  // equal barrier counts for both groups
-  } else {
-    // Ping-pong with split DMA (see MODE comment above).
-    const bool g1 = wave >= NWAVES / 2;
-    bf16x8 fa[2][FM], fb[2][FN];
-    auto ldall = [&](const char* base) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j) fb[s][j] = *(const bf16x8*)(base + b_off[s] + j * 2048);
-#pragma unroll
-        for (int i = 0; i < FM; ++i) fa[s][i] = *(const bf16x8*)(base + a_off[s] + i * 2048);
-      }
-    };
-    auto mmaall = [&]() {
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][i], fb[s][j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    };
-    auto bar = [] {
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    if (!g1) {
-      stage_a(0, 0);
-    } else {
-      stage_b(0, 0);
-      if (nk > 1) stage_b(1, 1);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    if (g1) bar();
-    for (int kt = 0; kt < nk; ++kt) {
-      const char* base = smem + (kt & 1) * STAGE;
-      if (!g1 && kt + 1 < nk) stage_a((kt + 1) & 1, kt + 1);
-      ldall(base);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      bar();
-      if (g1 && kt + 2 < nk) stage_b(kt & 1, kt + 2);
-      mmaall();
-      if (!g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      bar();
-    }
-    if (!g1) bar();
   }
 
   // Epilogue: acc[i][j][r] is C(row = wr·16FM + i·16 + fq·4 + r, col = wc·16FN + j·16 + fr)
@@ -646,173 +402,6 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     // (16 B per lane, 1 KiB per wave instruction).
     static_assert(WM == 2, "exchanged halves need two wave rows");
     const int s = (int)(u & 1);
-    if constexpr (XCH == 4) {
-      // probe build: no hand-over at all (wrong sums), to time the
-      // exchange's share of the epilogue
-      if (wr != s) return;
-    } else if constexpr (XCH == 5) {
-      // Hand-over by L2 atomics: split s stores its own row half of its
-      // partial straight into C, then, once the partner has stored ITS half,
-      // adds the other half into C with return-less global_atomic_add_f32.
-      // On one XCD both land in the shared L2, so nothing is read back into
-      // the CU: 128 KiB of stores + 128 KiB of atomics per work-group, one
-      // flag wait, no partial round trip.  Partners on different XCDs (not
-      // produced by the remap, kept for safety) use the fenced W exchange.
-      constexpr int HALF = BM / 2 * BN;
-      constexpr int FPT = 4;
-      int* err = &tile_cnt[(size_t)FPT * ntm * ntn];
-      auto spin = [&](int* w) -> int {
-        int v, spins = 0;
-        while ((v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++spins > (1 << 21)) {
-            __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return 0;
-          }
-        }
-        return v;
-      };
-      int* ok = reinterpret_cast<int*>(smem);
-      __syncthreads();  // every wave is past its last LDS fragment read
-      if (tid == 0) {
-        const int px = spin(&tile_cnt[4 * t + 2 + (1 - s)]);
-        tile_cnt[4 * t + 2 + (1 - s)] = 0;  // re-arm the partner's word
-        ok[0] = px != 0;
-        ok[1] = px == (int)my_xcc + 1;
-      }
-      __syncthreads();
-      const bool same = ok[1] != 0;
-      float* ct = C + (size_t)t * BM * BN;
-      f32x4* wh = reinterpret_cast<f32x4*>(W + (size_t)t * BM * BN + (size_t)wr * HALF);
-      if ((wr == s) == same) {  // one XCD: own half into C; else: the other half into W
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) {
-            if (same) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr] = acc[i][j][r];
-            } else {
-              wh[((wc * FM + i) * FN + j) * 64 + lane] = acc[i][j];
-            }
-          }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        int good = ok[0];
-        if (!same) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_store(&tile_cnt[FPT * t + (1 - s)], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (good) good = spin(&tile_cnt[FPT * t + s]) != 0;
-        tile_cnt[FPT * t + s] = 0;  // re-arm for the next call
-        ok[2] = good;
-      }
-      __syncthreads();
-      if (!ok[2]) return;  // timed out: counted in the error word
-      if (same) {
-        if (wr == s) return;  // own half already in C
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              unsafeAtomicAdd(&ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr],
-                              acc[i][j][r]);
-        return;
-      }
-      // across XCDs: the partner's half of our rows is in W; add it and fall
-      // through to the plain C store of our own half
-      if (wr != s) return;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      const f32x4* rh = reinterpret_cast<const f32x4*>(W + (size_t)t * BM * BN + (size_t)s * HALF);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] += rh[((wc * FM + i) * FN + j) * 64 + lane];
-    } else if constexpr (XCH == 6) {
-      // XCH 2's hand-over in two rounds of FM/2 row blocks (64 of the 128
-      // rows) through one 64 KiB slot per work-group, reused by round 1:
-      // the XCD's partials in flight are 2 MiB instead of its whole 4 MiB L2,
-      // so the read-back hits L2 and half as many dead partial lines are
-      // written back.  My flag word for the partner counts 1 (round-0 rows
-      // in my slot), 2 (I have read the partner's round-0 rows: its slot is
-      // free), 3 (round-1 rows in my slot); all three are monotone, so
-      // neither side can wait on the other's wait.
-      constexpr int HALF = BM / 2 * BN;
-      constexpr int FH = FM / 2;
-      constexpr int FPT = 4;
-      int* err = &tile_cnt[(size_t)FPT * ntm * ntn];
-      auto spin_ge = [&](int* w, int want) -> int {
-        int v, spins = 0;
-        while ((v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < want) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++spins > (1 << 21)) {
-            __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return 0;
-          }
-        }
-        return v;
-      };
-      int* ok = reinterpret_cast<int*>(smem);
-      __syncthreads();  // every wave is past its last LDS fragment read
-      if (tid == 0) {
-        const int px = spin_ge(&tile_cnt[4 * t + 2 + (1 - s)], 1);
-        tile_cnt[4 * t + 2 + (1 - s)] = 0;  // re-arm the partner's word
-        ok[0] = px != 0;
-        ok[1] = px == (int)my_xcc + 1;
-      }
-      __syncthreads();
-      const bool same = ok[1] != 0;
-      int* inbox = &tile_cnt[FPT * t + s];        // written by the partner
-      int* outbox = &tile_cnt[FPT * t + (1 - s)];  // read by the partner
-      f32x4* wh = reinterpret_cast<f32x4*>(W + (size_t)t * BM * BN + (size_t)(1 - s) * HALF);
-      const f32x4* rh = reinterpret_cast<const f32x4*>(W + (size_t)t * BM * BN + (size_t)s * HALF);
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        if (wr != s) {
-#pragma unroll
-          for (int i = 0; i < FH; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j) wh[((wc * FH + i) * FN + j) * 64 + lane] = acc[r * FH + i][j];
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-          int good = ok[0];
-          if (!same) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          __hip_atomic_store(outbox, 2 * r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (good) good = spin_ge(inbox, 2 * r + 1) != 0;
-          ok[0] = good;
-        }
-        __syncthreads();
-        if (wr == s && ok[0]) {
-          if (!same) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          f32x4 part[FH][FN];
-#pragma unroll
-          for (int i = 0; i < FH; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j) part[i][j] = rh[((wc * FH + i) * FN + j) * 64 + lane];
-#pragma unroll
-          for (int i = 0; i < FH; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j) acc[r * FH + i][j] += part[i][j];
-        }
-        if (r == 0) {
-          // the partner's slot is read (loads landed); wait until ours is
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __syncthreads();
-          if (tid == 0) {
-            __hip_atomic_store(outbox, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (ok[0]) ok[0] = spin_ge(inbox, 2) != 0;
-          }
-          __syncthreads();
-        }
-      }
-      if (tid == 0) *inbox = 0;  // the partner's last word (3) has arrived: re-arm
-      if (wr != s) return;
-    } else {
     constexpr int HALF = BM / 2 * BN;
     f32x4* wh = reinterpret_cast<f32x4*>(W + (size_t)t * BM * BN + (size_t)wr * HALF);
     if (wr != s) {
@@ -878,7 +467,6 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] += part[i][j];
     }
-    }  // XCH != 4
   } else if constexpr (SK) {
     if (S > 1) {
       // Every split stores its partial tile; the last of the S to arrive
@@ -920,32 +508,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       }
     }
   }
-  if constexpr (MODE >= 8) {
-    // the K-half-1 waves hand their partials to the K-half-0 waves of the
-    // same region through LDS (the loop ended on a barrier: LDS is free)
-    f32x4* red = reinterpret_cast<f32x4*>(smem);
-    const int reg = wave % NREG;
-    if (wave >= NREG) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) red[((reg * FM + i) * FN + j) * 64 + lane] = acc[i][j];
-    }
-    __syncthreads();
-    if (wave >= NREG) return;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] += red[((reg * FM + i) * FN + j) * 64 + lane];
-  }
   float* ct = C + (size_t)t * BM * BN;
-  if constexpr (NOSTORE) {  // probe build: measures the epilogue's share
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(acc[i][j]));
-    return;
-  }
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -953,10 +516,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float* dst = &ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr];
-        if constexpr (NTS)
-          __builtin_nontemporal_store(acc[i][j][r], dst);  // C is never re-read: stream it past L2
-        else
-          *dst = acc[i][j][r];
+        *dst = acc[i][j][r];
       }
 }
 
@@ -977,18 +537,10 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     gemm_tile<WM, WN, FM, FN, MODE, true>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);           \
   }
 
-// Probe-only build without the C store (tools/gemm_probe.py epilogue share).
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pp_nostore(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * 16 * 8 + 4 * 16 * 4) * 64 * 2];
-  gemm_tile<2, 4, 8, 4, 2, false, true>(dims, A, Bt, C, smem, __cek_off);
-}
-
 // Split-K ping-pong variants (dims[4] = S splits; K/64 divisible by S):
 // strongly scaled slices keep one 256-row tile per CU busy instead of
 // leaving CUs idle (8 GPUs × 1024 rows of an 8192² problem = 128 tiles).
 CEK_GEMM_SK_KERNEL(cek_sgemm_bf16_256x256pp_sk, 2, 4, 8, 4, 2)
-CEK_GEMM_SK_KERNEL(cek_sgemm_bf16_256x128pp_sk, 4, 2, 4, 4, 2)
 // balanced-DMA split-K (three Bt buffers: 160 KiB LDS)
 extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sk(
     const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
@@ -996,54 +548,13 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sk(
   gemm_tile<2, 4, 8, 4, 4, true>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
 }
 
-// balanced-DMA split-K = 2 with exchanged row halves (flags: 2 per tile + 1)
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sx(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
-  gemm_tile<2, 4, 8, 4, 4, true, false, 1>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
-}
 // same, with the hand-over through a shared L2 when both splits of a tile run
-// on one XCD (flags: 4 per tile + 1)
+// on one XCD (flags: 4 per tile + 1); the 8-GPU slice kernel (1024 rows of
+// 8192²: 128 tiles of 256² for 256 CUs)
 extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sy(
     const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
   __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
-  gemm_tile<2, 4, 8, 4, 4, true, false, 2>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
-}
-
-// Probe-only builds of the exchanged-halves kernel: no C store / no
-// hand-over (each times its share of the epilogue), and nontemporal C stores.
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sy_nostore(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
-  gemm_tile<2, 4, 8, 4, 4, true, true, 2>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
-}
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sy_noxch(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
-  gemm_tile<2, 4, 8, 4, 4, true, false, 4>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
-}
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_syn(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
-  gemm_tile<2, 4, 8, 4, 4, true, false, 2, true>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
-}
-// same split, the hand-over in two rounds through one reused 64 KiB slot
-// (flags: 4 per tile + 1)
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sz(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
-  gemm_tile<2, 4, 8, 4, 4, true, false, 6>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
-}
-// same split, the hand-over by L2 atomics into C (flags: 4 per tile + 1)
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sa(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
-  gemm_tile<2, 4, 8, 4, 4, true, false, 5>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
-}
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pbn(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
-  gemm_tile<2, 4, 8, 4, 4, false, false, 0, true>(dims, A, Bt, C, smem, __cek_off);
+  gemm_tile<2, 4, 8, 4, 4, true, 2>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
 }
 
 #define CEK_GEMM_B3_KERNEL(NAME, WM, WN, FM, FN, MODE)                                              \
@@ -1053,12 +564,10 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pbn(
     gemm_tile<WM, WN, FM, FN, MODE>(dims, A, Bt, C, smem, __cek_off);                                  \
   }
 
-// Balanced-DMA ping-pong (MODE 4; MODE 5 issues the LDS reads before the
-// DMA): 160 KiB LDS at 256², 128 KiB at 256×128.
+// Balanced-DMA ping-pong (MODE 4):
+// 160 KiB LDS at 256², 128 KiB at 256×128.
 CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x256pb, 2, 4, 8, 4, 4)
 CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x128pb, 4, 2, 4, 4, 4)
-CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x256pc, 2, 4, 8, 4, 5)
-CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x128pc, 4, 2, 4, 4, 5)
 
 // Even chunk-split DMA with three whole stages (MODE 6): 144 KiB at 256×128.
 extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x128pe(
@@ -1069,42 +578,6 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x128pe(
 
 // 256×256 tiles, 8 waves (2×4, 128×64 each), 128 KiB LDS, 1 block/CU.
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256, 2, 4, 8, 4, 0)
-// LDS-DMA pieces interleaved between MFMA groups (MODE 7)
-CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256i, 2, 4, 8, 4, 7)
-CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128i, 4, 2, 4, 4, 7)
-CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256p, 2, 4, 8, 4, 1)
 CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256pp, 2, 4, 8, 4, 2)
-CEK_GEMM_KERNEL(cek_sgemm_bf16_256x256ps, 2, 4, 8, 4, 3)
-// 256×128 tiles, 8 waves (4×2, 64×64 each), 96 KiB LDS — twice the tiles
-// for strongly scaled slices (8 GPUs × 1024 rows of an 8192² problem).
-CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128, 4, 2, 4, 4, 0)
-CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128p, 4, 2, 4, 4, 1)
-CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128pp, 4, 2, 4, 4, 2)
-CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128ps, 4, 2, 4, 4, 3)
 // 128×128 tiles, 4 waves (2×2, 64×64 each), 64 KiB LDS, 2 blocks/CU.
-// 256×128 with four waves of 128×64 (one per SIMD): 96 KiB of fragment
-// reads per K-tile against 128 KiB for eight 64×64 waves, the layout
-// hipBLASLt picks for the 1024-row slice (MT256x128x64)
-CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128w4, 2, 2, 8, 4, 0)
-CEK_GEMM_KERNEL(cek_sgemm_bf16_256x128w4p, 2, 2, 8, 4, 1)
-// the same four 128×64 regions, two waves each splitting every K-tile
-// (MODE 8, 512 threads); LDS: 96 KiB of stages, 128 KiB for the reduction
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x128k2(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * 8 * 4 * 64 * 16];
-  gemm_tile<2, 2, 8, 4, 8>(dims, A, Bt, C, smem, __cek_off);
-}
-// ping-pong on the in-CU split-K (MODE 10): 128 KiB (96 of stages)
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x128kp(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * 8 * 4 * 64 * 16];
-  gemm_tile<2, 2, 8, 4, 10>(dims, A, Bt, C, smem, __cek_off);
-}
-// same with a three-stage LDS ring (MODE 9): 144 KiB
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x128k3(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[3 * (256 + 128) * 64 * 2];
-  gemm_tile<2, 2, 8, 4, 9>(dims, A, Bt, C, smem, __cek_off);
-}
 CEK_GEMM_KERNEL(cek_sgemm_bf16_128x128, 2, 2, 4, 4, 0)
-CEK_GEMM_KERNEL(cek_sgemm_bf16_128x128p, 2, 2, 4, 4, 1)

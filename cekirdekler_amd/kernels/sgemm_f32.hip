@@ -22,7 +22,7 @@
 
 namespace {
 
-template <int WM, int WN, int FM, int FN, int PIPE, bool NTS = false>
+template <int WM, int WN, int FM, int FN, int PIPE>
 __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, const float* __restrict__ A,
                                               const float* __restrict__ Bt, float* __restrict__ C, char* smem,
                                               long long off) {
@@ -236,23 +236,8 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
       }
       __builtin_amdgcn_s_setprio(0);
     }
-  } else if constexpr (PIPE == 2) {
-    // both 16-deep k blocks' fragments are read up front: the second block's
-    // ds_reads fly under the first block's MFMAs (2 fragment sets live, no
-    // carry across the barrier, unlike PIPE == 1)
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
-      const char* base = smem + cur * STAGE;
-      f32x4 xa[FM], xb[FN], ya[FM], yb[FN];
-      ld(xa, xb, base, 0);
-      ld(ya, yb, base, 1);
-      mma(xa, xb);
-      mma(ya, yb);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  } else if constexpr (PIPE == 0) {
+  } else {
+    static_assert(PIPE == 0, "PIPE is 0, 3, 4, 5, 6, 7 or 8");
     // one barrier per K-tile; the next K-tile's DMA flies under the MFMAs
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
@@ -267,23 +252,6 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
-  } else {
-    // register double-buffered fragments: the second 16-deep k block is read
-    // while the first one's MFMAs run, and the next K-tile's first block
-    // right after the barrier that publishes it, under the second's MFMAs
-    f32x4 xa[FM], xb[FN], ya[FM], yb[FN];
-    ld(xa, xb, smem, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      const char* base = smem + cur * STAGE;
-      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
-      ld(ya, yb, base, 1);
-      mma(xa, xb);
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (kt + 1 < nk) ld(xa, xb, smem + (cur ^ 1) * STAGE, 0);
-      mma(ya, yb);
-    }
   }
 
   // acc[i][j][r] is C(row = wr·16FM + i·16 + fq·4 + r, col = wc·16FN + j·16 + fr)
@@ -295,164 +263,10 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float* dst = &ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr];
-        if constexpr (NTS)
-          __builtin_nontemporal_store(acc[i][j][r], dst);
-        else
-          *dst = acc[i][j][r];
+        *dst = acc[i][j][r];
       }
 }
 
-
-// Balanced-DMA ping-pong (the bf16 "pb" schedule, kernels/sgemm_bf16.hip
-// MODE 4, on fp32 operands): the work-group's two wave groups (waves <
-// NWAVES/2 = G0, the rest = G1, one of each per SIMD) alternate between an
-// LDS-read section and an MFMA section one s_barrier apart, so each SIMD's
-// matrix pipe always has one wave issuing.  G0 stages the A tile of K-tile
-// k+1 and G1 the Bt tile of K-tile k+2, each during its own read section.
-// A: 2 LDS buffers, Bt: 3 (160 KiB at 256², BK = 32 floats).
-//   WAR: both targets were last read in the previous read sections.
-//   RAW: G0's vmcnt(0) closes its MFMA section (A k+1 retired before G0
-//        reads it); G1 ends its read section k with only B k+2 in flight.
-template <int WM, int WN, int FM, int FN>
-__device__ __forceinline__ void gemm_f32_pb_tile(const int* __restrict__ dims, const float* __restrict__ A,
-                                                 const float* __restrict__ Bt, float* __restrict__ C, char* smem,
-                                                 long long off) {
-  constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN, BK = 32;
-  constexpr int NWAVES = WM * WN, NT = 64 * NWAVES, HALF = NWAVES / 2;
-  constexpr int A_BYTES = BM * BK * 4, B_BYTES = BN * BK * 4;
-  constexpr int A_INSTR = A_BYTES / 1024 / HALF, B_INSTR = B_BYTES / 1024 / HALF;
-  static_assert(A_INSTR * HALF * 1024 == A_BYTES && B_INSTR * HALF * 1024 == B_BYTES, "staging split");
-
-  const int M = dims[0], N = dims[1], K = dims[2], GM = dims[3] > 0 ? dims[3] : 1;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave / WN, wc = wave % WN;
-  const bool g1 = wave >= HALF;
-  const int sw = wave % HALF;  // staging wave index inside its group
-  const long long t = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
-  const int ntn = N / BN, ntm = M / BM;
-  const int per_group = GM * ntn, grp = (int)(t / per_group), first = grp * GM;
-  const int gsz = min(ntm - first, GM), in_g = (int)(t % per_group);
-  const int tm = first + in_g % gsz, tn = in_g / gsz;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);
-  const unsigned lane_off = (unsigned)(lrow * K + lchunk * 4) * 4u;
-  const char* a_wave = (const char*)(A + (size_t)(m0 + sw * A_INSTR * 8) * K);
-  const char* b_wave = (const char*)(Bt + (size_t)(n0 + sw * B_INSTR * 8) * K);
-  char* const a_base = smem;
-  char* const b_base = smem + 2 * A_BYTES;
-  auto stage_a = [&](int kt) {
-    char* base = a_base + (kt & 1) * A_BYTES;
-#pragma unroll
-    for (int j = 0; j < A_INSTR; ++j) {
-      const char* src = a_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 4;
-      __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off), (lds_void*)(base + (sw * A_INSTR + j) * 1024),
-                                       16, 0, 0);
-    }
-  };
-  auto stage_b = [&](int kt) {
-    char* base = b_base + (kt % 3) * B_BYTES;
-#pragma unroll
-    for (int j = 0; j < B_INSTR; ++j) {
-      const char* src = b_wave + ((size_t)j * 8 * K + (size_t)kt * BK) * 4;
-      __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off), (lds_void*)(base + (sw * B_INSTR + j) * 1024),
-                                       16, 0, 0);
-    }
-  };
-
-  const int fr = lane & 15, fq = lane >> 4;
-  int a_off[2], b_off[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int pc = (s * 4 + fq) ^ (lane & 7);
-    a_off[s] = (wr * 16 * FM + fr) * 128 + pc * 16;
-    b_off[s] = (wc * 16 * FN + fr) * 128 + pc * 16;
-  }
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  f32x4 fa[2][FM], fb[2][FN];
-  auto ldall = [&](int kt) {
-    const char* ab = a_base + (kt & 1) * A_BYTES;
-    const char* bb = b_base + (kt % 3) * B_BYTES;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) fb[s][j] = *(const f32x4*)(bb + b_off[s] + j * 2048);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) fa[s][i] = *(const f32x4*)(ab + a_off[s] + i * 2048);
-    }
-  };
-  auto mmaall = [&]() {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[s][i][q], fb[s][j][q], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto bar = [] {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  const int nk = K / BK;
-  if (!g1) {
-    stage_a(0);
-  } else {
-    stage_b(0);
-    if (nk > 1) stage_b(1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  bar();
-  if (g1) bar();  // G1 runs one section behind
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool b_issued = g1 && kt + 2 < nk;
-    if (!g1) {
-      if (kt + 1 < nk) stage_a(kt + 1);
-    } else if (b_issued) {
-      stage_b(kt + 2);
-    }
-    ldall(kt);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (g1) {
-      if (b_issued) {
-        static_assert(B_INSTR == 8 || B_INSTR == 4, "vmcnt immediates below");
-        if constexpr (B_INSTR == 8)
-          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    bar();
-    mmaall();
-    if (!g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-  }
-  if (!g1) bar();  // equal barrier counts for both groups
-
-  float* ct = C + (size_t)t * BM * BN;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        __builtin_nontemporal_store(acc[i][j][r],
-                                    &ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr]);
-}
 
 // The same tile with v_mfma_f32_32x32x2_f32 (64 cycles, 32×32 outputs):
 // lane l reads A[row = l%32][8·kb + 4·(l/32) .. +3] and feeds element t to
@@ -584,54 +398,16 @@ __device__ __forceinline__ void gemm_f32w_tile(const int* __restrict__ dims, con
 
 // 128×128 tiles, 4 waves (2×2, 64×64 each), 64 KiB LDS: two work-groups per CU.
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_128x128, 2, 2, 4, 4, 0)
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_128x128p, 2, 2, 4, 4, 1)
 // 256×128 tiles, 8 waves (4×2, 64×64 each), 96 KiB LDS.
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128, 4, 2, 4, 4, 0)
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128p, 4, 2, 4, 4, 1)
 // 256×256 tiles, 8 waves (2×4, 128×64 each), 128 KiB LDS.
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256, 2, 4, 8, 4, 0)
-// the same with both k blocks' fragments read before the MFMAs
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256h, 2, 4, 8, 4, 2)
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128h, 4, 2, 4, 4, 2)
-// (a register double-buffered 256×256 variant needs 256 + 57 spilled VGPRs)
-// 256×256 tiles with 4 waves of 128×128 (one wave per SIMD, 512 registers
-// per lane: the 256 accumulator registers go to AGPRs): twice the MFMAs per
-// fragment byte of the 8-wave 128×64 layout, as hipBLASLt's MT256x256x32
-// fp32 kernel (1 wave per SIMD, 98 % MFMA-busy: profiles/gemm_f32_pmc.md).
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q, 2, 2, 8, 8, 1)
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q0, 2, 2, 8, 8, 0)
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q2, 2, 2, 8, 8, 2)
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256q3, 2, 2, 8, 8, 3)
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256qr, 2, 2, 8, 8, 5)
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256qb7, 2, 2, 8, 8, 8)
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256i, 2, 4, 8, 4, 3)
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ie, 2, 4, 8, 4, 4)
+// fragment reads of k block 1 between block 0's MFMA groups (production:
+// profiles/gemm_f32_findings.md); ib7: barrier ahead of the last MFMA groups;
+// 256x128ie: every LDS-DMA piece within the first k block's MFMAs
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ir, 2, 4, 8, 4, 5)
-// "ir" with the barrier ahead of the last MFMA group(s): next K-tile's block-0
-// fragment reads under this K-tile's tail MFMAs (PIPE 6 / 7 / 8)
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ib, 2, 4, 8, 4, 6)
-CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ib6, 2, 4, 8, 4, 7)
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x256ib7, 2, 4, 8, 4, 8)
-// same with nontemporal C stores
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_f32_256x256irn(
-    const int* dims, const float* A, const float* Bt, float* C, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * (256 + 256) * 32 * 4];
-  gemm_f32_tile<2, 4, 8, 4, 5, true>(dims, A, Bt, C, smem, __cek_off);
-}
 CEK_GEMM_F32_KERNEL(cek_sgemm_f32_256x128ie, 4, 2, 4, 4, 4)
-
-// Balanced-DMA ping-pong: 256×256 (A 2 × 32 KiB + Bt 3 × 32 KiB = 160 KiB LDS)
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_f32_256x256pb(
-    const int* dims, const float* A, const float* Bt, float* C, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 32 * 4];
-  gemm_f32_pb_tile<2, 4, 8, 4>(dims, A, Bt, C, smem, __cek_off);
-}
-// 256×128 (A 2 × 32 KiB + Bt 3 × 16 KiB = 112 KiB LDS)
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_f32_256x128pb(
-    const int* dims, const float* A, const float* Bt, float* C, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 128) * 32 * 4];
-  gemm_f32_pb_tile<4, 2, 4, 4>(dims, A, Bt, C, smem, __cek_off);
-}
 
 // 32×32×2 form with register double-buffered fragments (gemm_f32w_tile).
 #define CEK_GEMM_F32W_KERNEL(NAME, WM, WN, FM, FN)                                                 \
@@ -642,5 +418,3 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_f32_256x128pb(
   }
 
 CEK_GEMM_F32W_KERNEL(cek_sgemm_f32_256x256w, 2, 4, 4, 2)  // 8 waves, 128×64 each, 128 KiB LDS
-CEK_GEMM_F32W_KERNEL(cek_sgemm_f32_256x128w, 4, 2, 2, 2)  // 8 waves, 64×64 each, 96 KiB LDS
-CEK_GEMM_F32W_KERNEL(cek_sgemm_f32_128x128w, 2, 2, 2, 2)  // 4 waves, 64×64 each, 64 KiB LDS

@@ -20,107 +20,49 @@ from ..arrays import ClArray
 from ..cruncher import ClNumberCruncher
 from .library import library
 
-# tile name -> (BM, BN, work-group size, kernel); "p" = register
-# double-buffered fragment pipeline, "pp" = ping-pong wave groups
+# tile name -> (BM, BN, work-group size, kernel).  The production tiles and
+# at most two tested alternates per dtype; every variant measured and dropped
+# in rounds 1-2 is in git history, with its numbers in profiles/gemm_*.md.
 TILES = {
-    "256x256": (256, 256, 512, "cek_sgemm_bf16_256x256"),
-    "256x256p": (256, 256, 512, "cek_sgemm_bf16_256x256p"),
-    "256x256pp": (256, 256, 512, "cek_sgemm_bf16_256x256pp"),
-    "256x256ps": (256, 256, 512, "cek_sgemm_bf16_256x256ps"),
-    "256x128": (256, 128, 512, "cek_sgemm_bf16_256x128"),
-    "256x128p": (256, 128, 512, "cek_sgemm_bf16_256x128p"),
-    "256x128pp": (256, 128, 512, "cek_sgemm_bf16_256x128pp"),
-    "256x128ps": (256, 128, 512, "cek_sgemm_bf16_256x128ps"),
-    # four waves of 128×64 (one per SIMD), fragments single / double-buffered
-    "256x128w4": (256, 128, 256, "cek_sgemm_bf16_256x128w4"),
-    "256x128w4p": (256, 128, 256, "cek_sgemm_bf16_256x128w4p"),
-    # same regions, two waves per region each taking one K half of every K-tile (LDS-summed)
-    "256x128k2": (256, 128, 512, "cek_sgemm_bf16_256x128k2"),
-    "256x128k3": (256, 128, 512, "cek_sgemm_bf16_256x128k3"),  # same, three-stage LDS ring
-    "256x128kp": (256, 128, 512, "cek_sgemm_bf16_256x128kp"),  # same split, ping-pong groups
-    "128x128": (128, 128, 256, "cek_sgemm_bf16_128x128"),
-    "128x128p": (128, 128, 256, "cek_sgemm_bf16_128x128p"),
-    # balanced-DMA ping-pong: G0 stages A, G1 stages Bt two K-tiles ahead
+    # balanced-DMA ping-pong (G0 stages A, G1 stages Bt two K-tiles ahead):
+    # the full-problem tile (1.47-1.50 PF at 8192³)
     "256x256pb": (256, 256, 512, "cek_sgemm_bf16_256x256pb"),
-    "256x128pb": (256, 128, 512, "cek_sgemm_bf16_256x128pb"),
-    "256x256pc": (256, 256, 512, "cek_sgemm_bf16_256x256pc"),  # same, LDS reads before the DMA
-    "256x128pc": (256, 128, 512, "cek_sgemm_bf16_256x128pc"),
-    "256x128pe": (256, 128, 512, "cek_sgemm_bf16_256x128pe"),  # even chunk-split DMA, 3 stages
-    # balanced-DMA, split-K = 2 with exchanged row halves (always two K-splits)
-    "256x256pbx": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sx"),
-    # same, hand-over through the shared L2 when both splits run on one XCD
+    # the same with split-K = 2, the two splits exchanging row halves through
+    # their XCD's L2: the 8-GPU slice (1024 rows of 8192², 128 tiles)
     "256x256pby": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sy"),
-    # same split, other row half added into C by L2 atomics (no partial read-back)
-    "256x256pba": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sa"),
-    # same split, the hand-over in two rounds through one reused slot (half the L2 footprint)
-    "256x256pbz": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sz"),
-    # same with nontemporal C stores; probe-only: no C store / no hand-over
-    "256x256pbyn": (256, 256, 512, "cek_sgemm_bf16_256x256pb_syn"),
-    "256x256pby_nostore": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sy_nostore"),
-    "256x256pby_noxch": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sy_noxch"),
-    # LDS-DMA pieces interleaved between MFMA groups, 2 waves per SIMD in step
-    "256x256i": (256, 256, 512, "cek_sgemm_bf16_256x256i"),
-    "256x128i": (256, 128, 512, "cek_sgemm_bf16_256x128i"),
-    # balanced-DMA ping-pong with nontemporal C stores
-    "256x256pbn": (256, 256, 512, "cek_sgemm_bf16_256x256pbn"),
-    # probe only: 256x256pp without the C store (epilogue share)
-    "256x256pp_nostore": (256, 256, 512, "cek_sgemm_bf16_256x256pp_nostore"),
-    # ping-pong with a 4-deep BK=32 LDS ring (kernels/sgemm_pp32_bf16.hip)
-    "256x256q": (256, 256, 512, "cek_sgemm_bf16_256x256q"),
-    "256x128q": (256, 128, 512, "cek_sgemm_bf16_256x128q"),
-    # 8-phase half-tile pipeline (kernels/sgemm8p_bf16.hip), ring of 8 / 10 slots
-    "256x256e8": (256, 256, 512, "cek_sgemm8p_bf16_r8"),
-    "256x256e10": (256, 256, 512, "cek_sgemm8p_bf16_r10"),
+    # 256×128 fallbacks (twice the tiles): even chunk-split DMA, three stages / balanced DMA
+    "256x128pe": (256, 128, 512, "cek_sgemm_bf16_256x128pe"),
+    "256x128pb": (256, 128, 512, "cek_sgemm_bf16_256x128pb"),
+    # reference structures: one LDS stage in flight / ping-pong wave groups
+    # (the latter with a last-arriver split-K variant)
+    "256x256": (256, 256, 512, "cek_sgemm_bf16_256x256"),
+    "256x256pp": (256, 256, 512, "cek_sgemm_bf16_256x256pp"),
+    # small problems: 2 blocks per CU
+    "128x128": (128, 128, 256, "cek_sgemm_bf16_128x128"),
 }
 
-
-GEMM_LIBS = ("sgemm_bf16", "sgemm8p_bf16", "sgemm_pp32_bf16")
+GEMM_LIBS = ("sgemm_bf16",)
 
 # fp32 tiles (kernels/sgemm_f32.hip): v_mfma_f32_16x16x4_f32, BK = 32
 F32_TILES = {
-    "128x128": (128, 128, 256, "cek_sgemm_f32_128x128"),
-    "256x128": (256, 128, 512, "cek_sgemm_f32_256x128"),
-    "256x256": (256, 256, 512, "cek_sgemm_f32_256x256"),
-    "256x256h": (256, 256, 512, "cek_sgemm_f32_256x256h"),
-    "256x128h": (256, 128, 512, "cek_sgemm_f32_256x128h"),
-    # "p": register double-buffered fragments (next k block read under the MFMAs)
-    "128x128p": (128, 128, 256, "cek_sgemm_f32_128x128p"),
-    "256x128p": (256, 128, 512, "cek_sgemm_f32_256x128p"),
-    # "w": v_mfma_f32_32x32x2_f32 with register double-buffered fragments
-    "256x256w": (256, 256, 512, "cek_sgemm_f32_256x256w"),
-    "256x128w": (256, 128, 512, "cek_sgemm_f32_256x128w"),
-    "128x128w": (128, 128, 256, "cek_sgemm_f32_128x128w"),
-    # "pb": balanced-DMA ping-pong wave groups (the bf16 pb schedule)
-    "256x256pb": (256, 256, 512, "cek_sgemm_f32_256x256pb"),
-    "256x128pb": (256, 128, 512, "cek_sgemm_f32_256x128pb"),
-    # "q": 4 waves of 128×128 (one per SIMD), register double-buffered / plain / both blocks up front
-    "256x256q": (256, 256, 256, "cek_sgemm_f32_256x256q"),
-    "256x256q0": (256, 256, 256, "cek_sgemm_f32_256x256q0"),
-    "256x256q2": (256, 256, 256, "cek_sgemm_f32_256x256q2"),
-    # fragments up front, next K-tile's LDS-DMA interleaved through the MFMAs
-    "256x256q3": (256, 256, 256, "cek_sgemm_f32_256x256q3"),
-    "256x256i": (256, 256, 512, "cek_sgemm_f32_256x256i"),
-    # same, every piece issued within the first k block's MFMAs
-    "256x256ie": (256, 256, 512, "cek_sgemm_f32_256x256ie"),
-    "256x128ie": (256, 128, 512, "cek_sgemm_f32_256x128ie"),
-    # "i" with block 1's fragment reads between block 0's MFMA groups
+    # production: k block 1's fragment reads between block 0's MFMA groups
+    # (146-147 TF at 8192³, profiles/gemm_f32_findings.md)
     "256x256ir": (256, 256, 512, "cek_sgemm_f32_256x256ir"),
-    "256x256irn": (256, 256, 512, "cek_sgemm_f32_256x256irn"),  # + nontemporal C stores
-    # "ir" with the barrier ahead of the last MFMA group (ib6: last two), so the
-    # next K-tile's first fragment reads overlap MFMAs; ib7 spreads the DMA wider
-    "256x256ib": (256, 256, 512, "cek_sgemm_f32_256x256ib"),
-    "256x256ib6": (256, 256, 512, "cek_sgemm_f32_256x256ib6"),
+    # alternates: the barrier ahead of the last MFMA groups; v_mfma_f32_32x32x2_f32
     "256x256ib7": (256, 256, 512, "cek_sgemm_f32_256x256ib7"),
-    # the 4-wave 128×128-per-wave layout (one wave per SIMD) with the ir / ib7 schedules
-    "256x256qr": (256, 256, 256, "cek_sgemm_f32_256x256qr"),
-    "256x256qb7": (256, 256, 256, "cek_sgemm_f32_256x256qb7"),
+    "256x256w": (256, 256, 512, "cek_sgemm_f32_256x256w"),
+    # 256×128: every LDS-DMA piece within the first k block's MFMAs
+    "256x128ie": (256, 128, 512, "cek_sgemm_f32_256x128ie"),
+    # plain one-stage-in-flight structures
+    "256x256": (256, 256, 512, "cek_sgemm_f32_256x256"),
+    "256x128": (256, 128, 512, "cek_sgemm_f32_256x128"),
+    "128x128": (128, 128, 256, "cek_sgemm_f32_128x128"),
 }
 
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
-SPLIT_K_TILES = {"256x256pp", "256x128pp", "256x256pb"}
+SPLIT_K_TILES = {"256x256pp", "256x256pb"}
 # tiles whose kernel always runs two K-splits that exchange row halves
-EXCHANGE_TILES = {"256x256pbx": 2, "256x256pby": 4, "256x256pba": 4, "256x256pbz": 4, "256x256pbyn": 4, "256x256pby_nostore": 4,
-                  "256x256pby_noxch": 4}  # flag words per tile
+EXCHANGE_TILES = {"256x256pby": 4}  # flag words per tile
 
 
 def to_bf16_bits(x: np.ndarray) -> np.ndarray:

@@ -54,10 +54,7 @@ def test_logical_devices_pipelines(pipeline, ptype):
     assert sum(cr.ranges(5)) == n
 
 
-@pytest.mark.parametrize("tile", ["256x256", "256x256p", "256x256pp", "256x256ps", "256x128", "256x128p", "256x128pp", "256x128ps",
-                                  "128x128", "128x128p", "256x256e8", "256x256e10", "256x256q", "256x128q",
-                                  "256x256pb", "256x128pb", "256x256pc", "256x128pc", "256x128pe",
-                                  "256x256i", "256x128i", "256x256pbn"])
+@pytest.mark.parametrize("tile", ["256x256", "256x256pp", "256x256pb", "256x128pb", "256x128pe", "128x128"])
 def test_gemm_bf16_matches_fp64(tile):
     from cekirdekler_amd.ops.gemm import GemmBf16
 
@@ -69,8 +66,7 @@ def test_gemm_bf16_matches_fp64(tile):
     assert err < 5e-3 * np.abs(ref).max(), err
 
 
-@pytest.mark.parametrize("tile", ["256x256e8", "256x256e10", "256x256q", "256x128q", "256x256pb", "256x128pb",
-                                  "256x256pc", "256x128pe"])
+@pytest.mark.parametrize("tile", ["256x256pb", "256x128pb", "256x128pe", "256x256pp"])
 @pytest.mark.parametrize("shape", [(256, 256, 64), (512, 256, 128), (256, 512, 192), (1024, 768, 320),
                                    (2048, 2048, 1024)])
 def test_gemm_8phase_pipeline_tails(tile, shape):
@@ -88,7 +84,7 @@ def test_gemm_8phase_pipeline_tails(tile, shape):
         assert err < 5e-3 * np.abs(ref).max(), (shape, err)
 
 
-@pytest.mark.parametrize("tile", ["256x256pp", "256x128pp", "256x256pb"])
+@pytest.mark.parametrize("tile", ["256x256pp", "256x256pb"])
 @pytest.mark.parametrize("split", [2, 4])
 def test_gemm_split_k(tile, split):
     """Split-K: partial tiles + last-arrival reduction, counters re-armed
@@ -112,7 +108,7 @@ def test_gemm_split_k(tile, split):
     cr.dispose()
 
 
-@pytest.mark.parametrize("tile", ["256x256pbx", "256x256pby", "256x256pba", "256x256pbz"])
+@pytest.mark.parametrize("tile", ["256x256pby"])
 def test_gemm_split_k_exchanged_halves(tile):
     """Split-K = 2 with exchanged row halves: each split finishes one half
     of the tile; flags re-armed across calls (4 calls), no spin timeouts, the
@@ -140,7 +136,7 @@ def test_gemm_two_logical_devices_balanced():
     from cekirdekler_amd.ops.gemm import GemmBf16
 
     g0 = _gpu()[0]
-    g = GemmBf16(1024, 1024, 256, devices=g0 + g0, tile="256x128")
+    g = GemmBf16(1024, 1024, 256, devices=g0 + g0, tile="256x128pe")
     for _ in range(3):
         g.run(resident=False)
     c = g.result(download=False)
@@ -242,10 +238,7 @@ def test_nbody_steps_two_logical_devices(resident):
     np.testing.assert_allclose(two.pos.array, one.pos.array, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("tile", ["128x128", "256x128", "256x256", "128x128p", "256x128p", "256x256w", "256x128w", "128x128w",
-                                  "256x256h", "256x128h", "256x256pb", "256x128pb", "256x256i", "256x256ir",
-                                  "256x256ib", "256x256ib6", "256x256ib7",
-                                  "256x256qr", "256x256qb7"])
+@pytest.mark.parametrize("tile", ["128x128", "256x128", "256x256", "256x256w", "256x256ir", "256x256ib7", "256x128ie"])
 @pytest.mark.parametrize("shape", [(512, 512, 256), (768, 512, 96), (512, 256, 32)])
 def test_gemm_f32_matches_fp64(tile, shape):
     """fp32 matrix-core GEMM (v_mfma_f32_16x16x4_f32) against a float64 host
@@ -263,7 +256,7 @@ def test_gemm_f32_matches_fp64(tile, shape):
     assert np.abs(c - ref).max() < 1e-4 * np.sqrt(K) * max(1.0, np.abs(ref).max())
 
 
-@pytest.mark.parametrize("tile,rows", [("256x256pb", 8192), ("256x256pby", 1024), ("256x256pba", 1024), ("256x256pbz", 1024)])
+@pytest.mark.parametrize("tile,rows", [("256x256pb", 8192), ("256x256pby", 1024)])
 def test_gemm_benchmarked_size_verify(tile, rows):
     """The headline kernels at the benchmarked size: the full 8192³ problem
     (N = 1) and the 1024-row slice one GPU of eight computes, device-resident
