@@ -1,15 +1,32 @@
-"""BASELINE config 5: a task pool of 256 mixed non-separable kernels,
-greedy asynchronous schedule over a device pool (all GPUs; with one GPU the
-same GPU is added several times, as the reference allows).  Reports makespan
-against the ideal Σ(task time)/GPUs, where a task's time is its kernel's
-device time (hipEvent span from ``record_timeline``, one task at a time on
-one GPU) — host launch and sync overheads are not in the ideal, and the
-excess is the scheduler's overhead plus imbalance (BASELINE target ≤ 1.15).
-The ideal is not a strict floor: with several tasks in flight on one GPU
-(3 queues per device) one kernel's tail work-groups run beside the next
-kernel's, which the serial spans cannot do, so a well-packed pool can land
-slightly under 1 (0.99 measured on one MI355X)."""
+"""BASELINE config 5: a task pool of 256 mixed non-separable kernels, greedy
+asynchronous schedule over a device pool (every GPU of the job; with one GPU
+the same GPU is added several times, as the reference allows:
+ClPipeline.cs:4337).
+
+The tasks differ in cost and in shape (reference pool: ClPipeline.cs:4132-4312,
+:4841-5047):
+
+* ``gemm``      library bf16 MFMA GEMM tile kernel, 2048×2048×1024 (64 work-groups)
+* ``reduce``    library wave-reduction over 4M floats (HBM-bound)
+* ``nbody``     library all-pairs force step, 16384 bodies (32 work-groups, compute-bound)
+* ``mandel``    library Mandelbrot band kernel, 1024² image (divergent VALU)
+* ``saxpy``     library streaming kernel over 4M floats
+* ``vecadd``    library streaming kernel over 4M floats
+* ``spin``      JIT-compiled user kernel string, iteration count per task
+
+plus a serial group (eight ``add`` tasks on one array, in order on one
+device: TASK_MESSAGE_SERIAL_MODE_BEGIN/END) and a global barrier task
+(TASK_MESSAGE_GLOBAL_SYNCHRONIZATION_FIRST) in the middle of the pool.
+
+Makespan is compared with the ideal Σ(task time) / physical GPUs, where a
+task's time is its kernel's hipEvent device time run alone on one GPU.  The
+ideal is not a strict floor: tasks that occupy a fraction of the CUs (gemm,
+nbody) run beside each other on one GPU when several are in flight.  The
+outputs of the serial group, of a GEMM task and of a reduction task are
+checked against numpy.  The same script runs unchanged at N GPUs.
+"""
 import argparse
+import collections
 import time
 
 import numpy as np
@@ -17,7 +34,11 @@ import numpy as np
 from common import emit, sync
 
 import cekirdekler_amd as ck
-from cekirdekler_amd.parallel.pool import ClDevicePool, ClDevicePoolType, ClTaskPool
+from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
+from cekirdekler_amd.models.nbody import NBodySimulation
+from cekirdekler_amd.ops.gemm import from_bf16_bits, to_bf16_bits, untile
+from cekirdekler_amd.ops.library import library
+from cekirdekler_amd.parallel.pool import ClDevicePool, ClDevicePoolType, ClTask, ClTaskPool, ClTaskType
 
 SRC = r"""
 __global__ void spin(float* x, const int* it) {
@@ -27,14 +48,16 @@ __global__ void spin(float* x, const int* it) {
   for (int k = 0; k < n; ++k) v = v * 0.9999f + 0.5f;
   x[i] = v;
 }
-__global__ void saxpy(float* x, const int* it) {
+__global__ void add(float* x, const float* v) {
   long long i = get_global_id(0);
-  x[i] = 2.0f * x[i] + (float)it[0];
+  x[i] = x[i] * 2.0f + v[0];
 }
 """
+LIBS = ("sgemm_bf16", "reduce", "nbody", "mandelbrot", "stream")
+MIX = {"gemm": 32, "reduce": 40, "nbody": 16, "mandel": 32, "saxpy": 48, "vecadd": 40, "spin": 39}
+SERIAL = 8  # + the serial group; + 1 barrier task = 256
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--tasks", type=int, default=256)
 ap.add_argument("--gpus", type=int, default=0)
 ap.add_argument("--logical", type=int, default=2, help="logical devices per GPU when only one GPU")
 ap.add_argument("--queues", type=int, default=3)
@@ -46,47 +69,181 @@ if ng == 1 and a.logical > 1:
     for _ in range(a.logical - 1):
         devs = devs + g[0]
 rng = np.random.default_rng(3)
-N = 1 << 22
-tasks = []
-for t in range(a.tasks):
-    kind = "spin" if t % 4 else "saxpy"
-    iters = int(rng.choice([256, 512, 1024, 2048]))
-    x = ck.ClArray(np.ones(N, np.float32))
-    x.read = x.write = False
-    it = ck.ClArray(np.array([iters], np.int32))
-    it.write = False
-    tasks.append((kind, x, it))
+prebuilt = library(*LIBS)
+ref_cr = ck.ClNumberCruncher(g[0], SRC, prebuilt=prebuilt)
+NS = 1 << 22  # streaming / reduction elements
 
-# per-task device times, serially on one device (hipEvent-timed kernel spans)
-ref_cr = ck.ClNumberCruncher(g[0], SRC)
-for kind, x, it in tasks:
-    x.next_param(it).compute(ref_cr, 1, kind, N, 256)
+
+def dev_only(*arrs):
+    for x in arrs:
+        x.read = x.write = False
+
+
+def make_gemm():
+    M, N, K = 2048, 2048, 1024
+    dims = ck.ClArray(np.array([M, N, K, 4, 1, 0, 0, 0], np.int32))
+    A = ck.ClArray(to_bf16_bits(rng.uniform(-1, 1, M * K).astype(np.float32)), "bfloat16")
+    B = ck.ClArray(to_bf16_bits(rng.uniform(-1, 1, N * K).astype(np.float32)), "bfloat16")
+    C = ck.ClArray(np.zeros(M * N, np.float32))
+    dims.write = A.write = B.write = False
+    C.read = False
+    C.elements_per_work_item = 256 * 256 // 512
+    return dims.next_param(A, B, C), "cek_sgemm_bf16_256x256pb", (M // 256) * (N // 256) * 512, 512, (A, B, C, M, N, K)
+
+
+def make_reduce():
+    x = ck.ClArray(rng.standard_normal(NS).astype(np.float32))
+    p = ck.ClArray(np.zeros(NS // (256 * 8), np.float32))
+    x.write = False
+    p.read = False
+    p.elements_per_group = 1
+    return x.next_param(p), "cek_reduce_sum_f32", NS // 8, 256, (x, p)
+
+
+def make_nbody():
+    sim = NBodySimulation(16384, cruncher=ref_cr, bodies_per_item=2, seed=int(rng.integers(1 << 30)))
+    return sim.pos.next_param(sim.vel, sim.acc, sim.params), sim.k_force, sim.n // sim.bpw, 256, sim
+
+
+def make_mandel():
+    x0 = float(rng.uniform(-2.0, -0.5))
+    m = MandelbrotRenderer(1024, 1024, max_iter=256, view=(x0, -1.0, 1.5, 2.0), cruncher=ref_cr, kernel="blk8h")
+    return m.view.next_param(m.size, m.out), m.kernel, m.global_range, m.local, m
+
+
+def make_saxpy():
+    s = ck.ClArray(np.array([1.5], np.float32))
+    x = ck.ClArray(rng.standard_normal(NS).astype(np.float32))
+    y = ck.ClArray(np.zeros(NS, np.float32))
+    s.write = x.write = False
+    y.read = False
+    for arr in (x, y):
+        arr.elements_per_work_item = 4
+    return s.next_param(x, y), "cek_saxpy_f32", NS // 4, 256, None
+
+
+def make_vecadd():
+    x = ck.ClArray(rng.standard_normal(NS).astype(np.float32))
+    y = ck.ClArray(rng.standard_normal(NS).astype(np.float32))
+    z = ck.ClArray(np.zeros(NS, np.float32))
+    for arr in (x, y, z):
+        arr.elements_per_work_item = 4
+    x.write = y.write = False
+    z.read = False
+    return x.next_param(y, z), "cek_vec_add_f32", NS // 4, 256, None
+
+
+def make_spin():
+    x = ck.ClArray(np.ones(NS // 4, np.float32))
+    it = ck.ClArray(np.array([int(rng.choice([256, 512, 1024]))], np.int32))
+    x.write = False
+    it.write = False
+    return x.next_param(it), "spin", NS // 4, 256, None
+
+
+MAKERS = {"gemm": make_gemm, "reduce": make_reduce, "nbody": make_nbody, "mandel": make_mandel,
+          "saxpy": make_saxpy, "vecadd": make_vecadd, "spin": make_spin}
+kinds = [k for k, n in MIX.items() for _ in range(n)]
+rng.shuffle(kinds)
+work = [(k,) + MAKERS[k]() for k in kinds]  # (kind, group, kernel, G, L, extra)
+
+# every array goes up to GPU 0 once, then each task's kernel is timed alone,
+# device-resident (hipEvent span)
+for _, grp, kern, G, L, _ in work:
+    grp.compute(ref_cr, 1, kern, G, L)
 sync()
 ref_cr.record_timeline = True
-for kind, x, it in tasks:
-    x.next_param(it).compute(ref_cr, 1, kind, N, 256)
+for _, grp, kern, G, L, _ in work:
+    flags = [(x.read, x.write, x.partial_read) for x in grp.arrays]
+    dev_only(*grp.arrays)
+    grp.compute(ref_cr, 1, kern, G, L)
+    for x, (r, w, p) in zip(grp.arrays, flags):
+        x.read, x.write, x.partial_read = r, w, p
 single = [sp["end_ms"] - sp["begin_ms"] for sp in ref_cr.timeline()]
-assert len(single) == len(tasks), (len(single), len(tasks))
-ref_cr.dispose()
+assert len(single) == len(work), (len(single), len(work))
+per_kind = collections.defaultdict(list)
+for (kind, *_), ms in zip(work, single):
+    per_kind[kind].append(ms)
 
-pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, True, a.queues)
+serial_x = ck.ClArray(np.zeros(256 * 64, np.float32))
+serial_v = ck.ClArray(np.array([1.0], np.float32))
+serial_v.write = False
+
+
+CHECKED = {next(i for i, w in enumerate(work) if w[0] == k) for k in ("gemm", "reduce")}
+
+
+def build_pool() -> ClTaskPool:
+    """The 256 tasks, device-resident (every array was uploaded to every pool
+    device beforehand); the checked GEMM and reduction outputs and the serial
+    group's array come back to the host."""
+    tp = ClTaskPool()
+    half = len(work) // 2
+    for i, (kind, grp, kern, G, L, extra) in enumerate(work):
+        if i == half:
+            bar = ClTask(None)
+            bar.type = ClTaskType.TASK_MESSAGE_GLOBAL_SYNCHRONIZATION_FIRST
+            tp.feed(bar)
+        flags = [(x.read, x.write, x.partial_read) for x in grp.arrays]
+        for x in grp.arrays:
+            x.read = x.partial_read = False
+            x.write = x.write and i in CHECKED
+        tp.feed(grp.task(1, kern, G, L))
+        for x, (r, w, p) in zip(grp.arrays, flags):
+            x.read, x.write, x.partial_read = r, w, p
+    serial_x.array[:] = 0
+    for k in range(SERIAL):
+        serial_x.read = k == 0
+        serial_x.write = k == SERIAL - 1
+        t = serial_x.next_param(serial_v).task(2, "add", serial_x.N, 64)
+        if k == 0:
+            t.type = ClTaskType.TASK_MESSAGE_SERIAL_MODE_BEGIN
+        if k == SERIAL - 1:
+            t.type = ClTaskType.TASK_MESSAGE_SERIAL_MODE_END
+        tp.feed(t)
+    return tp
+
+
+pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, True, a.queues, prebuilt=prebuilt)
 pool.add_device(devs)
-tp = ClTaskPool()
-for kind, x, it in tasks:
-    tp.feed(x.next_param(it).task(1, kind, N, 256))
-# warm the pool's crunchers/buffers once
+for cr in pool.crunchers:  # every input on every device: a task may land anywhere
+    for _, grp, *_ in work:
+        for x in grp.arrays:
+            cr.upload(x)
+    cr.upload(serial_v)
+pool.enqueue_task_pool(build_pool())  # warm-up pass: untimed
+pool.finish()
+tp = build_pool()
+ntasks = len(tp.tasks)
+sync()
+t0 = time.perf_counter()
 pool.enqueue_task_pool(tp)
 pool.finish()
-for kind, x, it in tasks:
-    tp.feed(x.next_param(it).task(1, kind, N, 256))
 sync()
-t = time.perf_counter()
-pool.enqueue_task_pool(tp)
-pool.finish()
-sync()
-makespan = (time.perf_counter() - t) * 1e3
+makespan = (time.perf_counter() - t0) * 1e3
 ideal = sum(single) / max(1, ng)
-emit({"config": "task_pool_256", "tasks": a.tasks, "gpus": ng, "logical_devices": len(devs),
-      "makespan_ms": makespan, "ideal_ms_sum_over_gpus": ideal, "ideal_basis": "hipEvent device time per task", "makespan_over_ideal": makespan / ideal,
-      "tasks_per_s": a.tasks / (makespan * 1e-3), "per_device_tasks": pool.device_task_counts()})
+
+# checks: serial group order (x ← 2x + 1, eight times from 0 = 255), one GEMM, one reduction
+serial_ok = bool(np.all(serial_x.array == 255.0))
+gi = next(i for i, w in enumerate(work) if w[0] == "gemm")
+A, B, C, M, N, K = work[gi][5]
+Af = from_bf16_bits(A.array).reshape(M, K).astype(np.float64)
+Bf = from_bf16_bits(B.array).reshape(N, K).astype(np.float64)
+ref = Af[:256] @ Bf.T
+got = untile(C.array, M, N, 256, 256, 4)[:256]
+gemm_err = float(np.abs(got - ref).max() / np.abs(ref).max())
+ri = next(i for i, w in enumerate(work) if w[0] == "reduce")
+x, p = work[ri][5]
+red_err = float(abs(p.array.astype(np.float64).sum() - x.array.astype(np.float64).sum()) / np.abs(x.array).sum())
+emit({"config": "task_pool_256", "tasks": ntasks, "gpus": ng, "logical_devices": len(devs),
+      "kernel_mix": {k: len(v) for k, v in per_kind.items()} | {"add(serial group)": SERIAL, "barrier": 1},
+      "task_device_ms": {k: {"median": float(np.median(v)), "min": float(np.min(v)), "max": float(np.max(v))}
+                         for k, v in per_kind.items()},
+      "makespan_ms": makespan, "ideal_ms_sum_over_gpus": ideal, "ideal_basis": "hipEvent device time per task, alone",
+      "makespan_over_ideal": makespan / ideal, "tasks_per_s": ntasks / (makespan * 1e-3),
+      "per_device_tasks": pool.device_task_counts(), "serial_group_in_order": serial_ok,
+      "gemm_task_max_rel_err": gemm_err, "reduce_task_rel_err": red_err})
 pool.dispose()
+ref_cr.dispose()
+if not (serial_ok and gemm_err < 5e-3 and red_err < 1e-4):
+    raise SystemExit("task pool output check failed")

@@ -637,3 +637,108 @@ extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8h_f32(const 
   out[((long long)row * W + col) >> 1] =
       make_int2(min(ex + (int)(cnt.x + 0.5f), max_iter), min(ey + (int)(cnt.y + 0.5f), max_iter));
 }
+
+// blk8h with fewer instructions per useful iteration ("blk8k"):
+//  * the iteration is 4 packed instructions instead of 5 —
+//      t = zr·zi;  a = fma(zr, zr, cr);  zr' = fma(−zi, zi, a);  zi' = fma(t, 2, ci)
+//    (blk8h computed zi² separately because blk8 shared it with |z|²; the
+//    8-iteration blocks need |z|² only at the block's end);
+//  * the first block counts every iteration (blk8's exact count), so a wave
+//    whose pixels all escape within 8 iterations — most of the exterior —
+//    stores its counts and ends without the counting pass;
+//  * a wave none of whose pixels escaped (set interior) skips the counting
+//    pass (wave-uniform branch).
+// Same 8×16 block per one-wave work-group and block-end bookkeeping as blk8h.
+extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8k_f32(const float* view, const int* size,
+                                                                        int2* out, CEK_HIDDEN) {
+  const long long w = cek_global_id();
+  const int W = size[0], max_iter = size[2];
+  const long long band_items = 4LL * W;
+  const long long band = w / band_items;
+  const int q = (int)(w - band * band_items);
+  const int blk = q >> 6, l = q & 63;
+  const int row = (int)band * 8 + (l >> 3), col = blk * 16 + (l & 7) * 2;
+  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
+  const float ci = y0 + row * dy;
+  const f32x2 cr = {x0 + col * dx, x0 + (col + 1) * dx}, civ = {ci, ci};
+  const f32x2 two = {2.f, 2.f};
+  const f32x2 nbig = {-1048576.f, -1048576.f}, cbig = {4194304.f, 4194304.f};
+  const long long o = ((long long)row * W + col) >> 1;
+  f32x2 zr = {0.f, 0.f}, zi = {0.f, 0.f};
+  // block 1, counted exactly (blk8's iteration)
+  f32x2 cnt = {0.f, 0.f}, tc = {1.f, 1.f};
+  const int first = min(8, max_iter);
+  for (int u = 0; u < first; ++u) {
+    const f32x2 zi2 = zi * zi;
+    const f32x2 m = __builtin_elementwise_fma(zr, zr, zi2);
+    tc = pk_fma_clamp(m, nbig, cbig);
+    cnt += tc;
+    const f32x2 tz = zr * zi;
+    zr = __builtin_elementwise_fma(zr, zr, -zi2) + cr;
+    zi = __builtin_elementwise_fma(tz, two, civ);
+  }
+  // escaped within block 1 ⇔ the last counted step was already escaped
+  const bool dx1 = tc.x < 0.5f, dy1 = tc.y < 0.5f;
+  const bool wave_done = __all(dx1 && dy1) || first >= max_iter;
+  if (wave_done) {
+    out[o] = make_int2(min((int)(cnt.x + 0.5f), max_iter), min((int)(cnt.y + 0.5f), max_iter));
+    return;
+  }
+  // blk8h's bookkeeping from iteration 8 on: the last z with |z|² <= 4 at a
+  // block end, and its iteration; a pixel escaped in block 1 keeps (0, z=0)
+  // and is recounted from the start by the counting pass
+  f32x2 fr = {0.f, 0.f}, fi = {0.f, 0.f};
+  int ex = 0, ey = 0;
+  if (!dx1) {
+    fr.x = zr.x;
+    fi.x = zi.x;
+    ex = 8;
+  }
+  if (!dy1) {
+    fr.y = zr.y;
+    fi.y = zi.y;
+    ey = 8;
+  }
+  bool kx = !dx1, ky = !dy1;
+  for (int it = 16; it <= max_iter && (kx || ky); it += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const f32x2 tz = zr * zi;
+      const f32x2 a = __builtin_elementwise_fma(zr, zr, cr);
+      zr = __builtin_elementwise_fma(-zi, zi, a);
+      zi = __builtin_elementwise_fma(tz, two, civ);
+    }
+    const f32x2 m = __builtin_elementwise_fma(zr, zr, zi * zi);
+    kx = m.x <= 4.f;
+    ky = m.y <= 4.f;
+    if (kx) {
+      fr.x = zr.x;
+      fi.x = zi.x;
+      ex = it;
+    }
+    if (ky) {
+      fr.y = zr.y;
+      fi.y = zi.y;
+      ey = it;
+    }
+  }
+  // counting pass over the escape block, skipped when no pixel of the wave
+  // escaped (every lane reached max_iter)
+  cnt = f32x2{0.f, 0.f};
+  if (!__all(ex >= max_iter && ey >= max_iter)) {
+    zr = fr;
+    zi = fi;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const f32x2 zi2 = zi * zi;
+      const f32x2 m = __builtin_elementwise_fma(zr, zr, zi2);
+      cnt += pk_fma_clamp(m, nbig, cbig);
+      const f32x2 tz = zr * zi;
+      const f32x2 a = __builtin_elementwise_fma(zr, zr, cr);
+      zr = a - zi2;
+      zi = __builtin_elementwise_fma(tz, two, civ);
+    }
+  }
+  out[o] = make_int2(min(ex + (int)(cnt.x + 0.5f), max_iter), min(ey + (int)(cnt.y + 0.5f), max_iter));
+}
+

@@ -20,7 +20,7 @@ FLOP_PER_ITER = 8
 
 # kernel variants; the band kernels additionally need device and pipeline
 # chunk ranges made of whole 16-row bands (see kernels/mandelbrot.hip)
-BAND_ROWS = {"blk16": 16, "blk16w4": 16, "blk64": 16, "blk8": 8, "blk8f": 8, "blk8g": 8, "blk16g": 16, "blk8h": 8}  # rows per band
+BAND_ROWS = {"blk16": 16, "blk16w4": 16, "blk64": 16, "blk8": 8, "blk8f": 8, "blk8g": 8, "blk16g": 16, "blk8h": 8, "blk8k": 8}  # rows per band
 BAND_KERNELS = set(BAND_ROWS)
 KERNELS = {
     # name: (library kernel, pixels per work item, work-group size)
@@ -42,6 +42,9 @@ KERNELS = {
     "blk8g": ("cek_mandelbrot_blk8g_f32", 2, 64),     # blk8f, zr chain reassociated (2 deep)
     "blk16g": ("cek_mandelbrot_blk16g_f32", 4, 64),   # blk8g, two pairs per lane (16×16 block)
     "blk8h": ("cek_mandelbrot_blk8h_f32", 2, 64),     # blk8g, last non-escaped z recorded per block
+    # blk8h with a 4-instruction iteration, an exactly counted first block
+    # (all-exterior waves end there) and no counting pass for interior waves
+    "blk8k": ("cek_mandelbrot_blk8k_f32", 2, 64),
 }
 
 
