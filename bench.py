@@ -187,11 +187,11 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
         # one GPU holds the whole problem: the square-shell stream
         # (Cores::gemm_host_shells), whose first kernels need two panels
         # instead of all of B; reported when it is the faster path
+        # (a GEMM-specific entry point outside compute(): reported on its own,
+        # never as the host-resident number)
         ms_shells = timed(ctx, lambda: g.run_host_shells(panels), host_steps, 2)
         err_shells = g.verify_shells(panels)
         err_host = max(err_host, err_shells)
-        if ms_shells < ms_host:
-            ms_host, mode = ms_shells, f"square shells, {panels} panels"
     cr.dispose()
     for a in (g.A, g.B, g.C, g.dims):
         a.dispose()  # release 0.5 GB of pinned host memory before the next config

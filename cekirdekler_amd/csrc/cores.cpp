@@ -244,6 +244,7 @@ Cores::~Cores() {
       workers_[w]->set_device();
       (void)hipFree(shell_dims_[w]);
     }
+  for (void* p : shell_dims_pin_) host_free(p);
   for (size_t w = 0; w < peer_ev_.size() && w < workers_.size(); ++w) {
     if (!peer_ev_[w].up) continue;
     workers_[w]->set_device();

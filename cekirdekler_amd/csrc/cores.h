@@ -424,6 +424,8 @@ class Cores {
   bool capturing_ = false;
   std::vector<void*> shell_dims_;         // gemm_host_shells: per-kernel dims, per worker
   std::vector<size_t> shell_dims_cap_;
+  std::vector<std::vector<int>> shell_dims_host_;  // what shell_dims_ holds (re-uploaded only on change)
+  std::vector<void*> shell_dims_pin_;               // pinned staging for that upload
   void restore_capture_state();  // the modes capture_begin saved
   struct CaptureSaved {
     bool device_spans, peer_reads, async_enqueue, fine_grained, enqueue_mode, record_timeline;

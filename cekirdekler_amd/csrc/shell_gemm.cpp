@@ -19,10 +19,12 @@
 // Host C layout: shell by shell, R_s then C_s, each tile-major in the
 // kernel's grouped tile order (ops/gemm.py untiles it).
 #include <algorithm>
+#include <cstring>
 #include <string>
 #include <vector>
 
 #include "cores.h"
+#include "memory.h"
 
 namespace cek {
 
@@ -57,19 +59,33 @@ void Cores::gemm_host_shells(int local_dev, const std::string& kernel, const Arr
     c[0] = s * PM, c[1] = PN, c[2] = K, c[3] = group_m, c[4] = 1;
   }
   const size_t dims_bytes = dims.size() * sizeof(int);
-  if (shell_dims_cap_[local_dev] < dims_bytes) {
-    if (shell_dims_[local_dev]) (void)hipFree(shell_dims_[local_dev]);
-    shell_dims_[local_dev] = nullptr;
-    CEK_HIP(hipMalloc(&shell_dims_[local_dev], dims_bytes));
-    shell_dims_cap_[local_dev] = dims_bytes;
+  if (shell_dims_host_.size() < workers_.size()) shell_dims_host_.resize(workers_.size());
+  hipStream_t up = w.main_stream();
+  if (shell_dims_host_[local_dev] != dims) {
+    // the dims change only with the shape: uploaded (asynchronously, ahead of
+    // the first panel on the upload stream the kernels wait on) when they do
+    if (shell_dims_cap_[local_dev] < dims_bytes) {
+      if (shell_dims_[local_dev]) {
+        CEK_HIP(hipStreamSynchronize(up));  // a previous call's kernels may still read the old block
+        (void)hipFree(shell_dims_[local_dev]);
+      }
+      shell_dims_[local_dev] = nullptr;
+      CEK_HIP(hipMalloc(&shell_dims_[local_dev], dims_bytes));
+      shell_dims_cap_[local_dev] = dims_bytes;
+      if (shell_dims_pin_.size() < workers_.size()) shell_dims_pin_.resize(workers_.size(), nullptr);
+      if (shell_dims_pin_[local_dev]) host_free(shell_dims_pin_[local_dev]);
+      shell_dims_pin_[local_dev] = host_alloc(dims_bytes, 4096, nullptr);
+    }
+    CEK_HIP(hipStreamSynchronize(up));  // the staging buffer may still feed an earlier copy
+    std::memcpy(shell_dims_pin_[local_dev], dims.data(), dims_bytes);
+    CEK_HIP(hipMemcpyAsync(shell_dims_[local_dev], shell_dims_pin_[local_dev], dims_bytes, hipMemcpyHostToDevice, up));
+    shell_dims_host_[local_dev] = dims;
   }
-  CEK_HIP(hipMemcpy(shell_dims_[local_dev], dims.data(), dims_bytes, hipMemcpyHostToDevice));
   char* dA = static_cast<char*>(w.buffer(A));
   char* dB = static_cast<char*>(w.buffer(B));
   char* dC = static_cast<char*>(w.buffer(C));
   int* dd = static_cast<int*>(shell_dims_[local_dev]);
 
-  hipStream_t up = w.main_stream();
   const uint64_t a_panel = static_cast<uint64_t>(PM) * K, b_panel = static_cast<uint64_t>(PN) * K;  // elements
   uint64_t c_off = 0;  // elements of C before shell s
   int slot = 0;
