@@ -69,7 +69,7 @@ def tile_err(c, t):
     r, col = tile_coords(np.array([t]), size, size, g.BM, g.BN, g.group_m)
     r, col = int(r[0]), int(col[0])
     ref = A[r * g.BM:(r + 1) * g.BM].astype(np.float64) @ B[col * g.BN:(col + 1) * g.BN].astype(np.float64).T
-    got = c[t * tile:(t + 1) * tile].reshape(g.BM, g.BN)
+    got = g.tile_block(c[t * tile:(t + 1) * tile])
     return float(np.abs(got - ref).max() / np.abs(ref).max())
 
 

@@ -36,7 +36,7 @@ from common import emit, sync
 import cekirdekler_amd as ck
 from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
 from cekirdekler_amd.models.nbody import NBodySimulation
-from cekirdekler_amd.ops.gemm import from_bf16_bits, to_bf16_bits, untile
+from cekirdekler_amd.ops.gemm import TILE_WAVES, from_bf16_bits, to_bf16_bits, untile
 from cekirdekler_amd.ops.library import library
 from cekirdekler_amd.parallel.pool import ClDevicePool, ClDevicePoolType, ClTask, ClTaskPool, ClTaskType
 
@@ -230,7 +230,7 @@ A, B, C, M, N, K = work[gi][5]
 Af = from_bf16_bits(A.array).reshape(M, K).astype(np.float64)
 Bf = from_bf16_bits(B.array).reshape(N, K).astype(np.float64)
 ref = Af[:256] @ Bf.T
-got = untile(C.array, M, N, 256, 256, 4)[:256]
+got = untile(C.array, M, N, 256, 256, 4, TILE_WAVES["256x256pb"])[:256]
 gemm_err = float(np.abs(got - ref).max() / np.abs(ref).max())
 ri = next(i for i, w in enumerate(work) if w[0] == "reduce")
 x, p = work[ri][5]

@@ -3,7 +3,8 @@
 //
 //   C = A · Bᵀ      A: [M][K] bf16 row-major, Bt: [N][K] bf16 row-major
 //   C is written TILE-MAJOR: tile t = (tm, tn) (tn fastest) occupies
-//   C[t·BM·BN ...] row-major inside the tile, so any contiguous range of
+//   C[t·BM·BN ...] in MFMA-fragment order inside the tile (epilogue; the
+//   host's ops/gemm.py tile_to_rows restores rows), so any contiguous range of
 //   tiles — the slice a device gets from the load balancer — is one
 //   contiguous byte range (the reference's partial write of
 //   [ref·e, (ref+r)·e), Worker.cs:1349-1352, with e = BM·BN / local).
@@ -508,16 +509,17 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       }
     }
   }
-  float* ct = C + (size_t)t * BM * BN;
+  // C tile in fragment order: wave (wr, wc)'s fragment (i, j) is 64 lanes ×
+  // 16 B = 1 KiB contiguous, so every store is one dwordx4 per lane (a
+  // row-major tile takes four dword stores per fragment, and with one
+  // work-group per CU the store tail is exposed).  Host side: ops/gemm.py
+  // tile_to_rows.  Element (row, col) of the tile lives at
+  // ((((wr·WN + wc)·FM + i)·FN + j)·64 + fq·16 + fr)·4 + r.
+  f32x4* ct = reinterpret_cast<f32x4*>(C + (size_t)t * BM * BN);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float* dst = &ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr];
-        *dst = acc[i][j][r];
-      }
+    for (int j = 0; j < FN; ++j) ct[(((wr * WN + wc) * FM + i) * FN + j) * 64 + lane] = acc[i][j];
 }
 
 }  // namespace

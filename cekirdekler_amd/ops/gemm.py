@@ -43,6 +43,36 @@ TILES = {
 
 GEMM_LIBS = ("sgemm_bf16",)
 
+# Wave geometry of every bf16 tile (WM × WN waves, FM × FN 16×16 fragments
+# each): the kernels store a C tile in fragment order (one dwordx4 per lane
+# per fragment), which tile_to_rows / rows_to_tile convert.
+TILE_WAVES = {
+    "256x256pb": (2, 4, 8, 4), "256x256pby": (2, 4, 8, 4), "256x256": (2, 4, 8, 4), "256x256pp": (2, 4, 8, 4),
+    "256x128pe": (4, 2, 4, 4), "256x128pb": (4, 2, 4, 4), "128x128": (2, 2, 4, 4),
+}
+
+
+def tile_to_rows(t: np.ndarray, geom) -> np.ndarray:
+    """Fragment-ordered C tiles (``[..., BM·BN]``) → row-major ``[..., BM, BN]``.
+    In-tile offset of (row, col) = ((((wr·WN + wc)·FM + i)·FN + j)·64 + fq·16 + fr)·4 + r
+    with row = wr·16FM + i·16 + fq·4 + r and col = wc·16FN + j·16 + fr."""
+    WM, WN, FM, FN = geom
+    lead = t.shape[:-1]
+    x = t.reshape(lead + (WM, WN, FM, FN, 4, 16, 4))
+    n = len(lead)
+    perm = list(range(n)) + [n + 0, n + 2, n + 4, n + 6, n + 1, n + 3, n + 5]
+    return x.transpose(perm).reshape(lead + (WM * FM * 16, WN * FN * 16))
+
+
+def rows_to_tile(b: np.ndarray, geom) -> np.ndarray:
+    """Inverse of :func:`tile_to_rows`: row-major ``[..., BM, BN]`` → fragment order."""
+    WM, WN, FM, FN = geom
+    lead = b.shape[:-2]
+    x = b.reshape(lead + (WM, FM, 4, 4, WN, FN, 16))  # wr i fq r wc j fr
+    n = len(lead)
+    perm = list(range(n)) + [n + 0, n + 4, n + 1, n + 5, n + 2, n + 6, n + 3]
+    return np.ascontiguousarray(x.transpose(perm)).reshape(lead + (-1,))
+
 # fp32 tiles (kernels/sgemm_f32.hip): v_mfma_f32_16x16x4_f32, BK = 32
 F32_TILES = {
     # production: k block 1's fragment reads between block 0's MFMA groups
@@ -87,10 +117,12 @@ def tile_coords(t: np.ndarray, M: int, N: int, BM: int, BN: int, group_m: int):
     return first + in_g % gsz, in_g // gsz
 
 
-def untile(c: np.ndarray, M: int, N: int, BM: int, BN: int, group_m: int = 1) -> np.ndarray:
-    """Tile-major C (grouped tile order) → row-major [M][N]."""
+def untile(c: np.ndarray, M: int, N: int, BM: int, BN: int, group_m: int = 1, geom=None) -> np.ndarray:
+    """Tile-major C (grouped tile order) → row-major [M][N]; ``geom``: the
+    tile's wave geometry when its elements are in fragment order (bf16
+    kernels), None for row-major tiles."""
     ntm, ntn = M // BM, N // BN
-    tiles = c.reshape(ntm * ntn, BM, BN)
+    tiles = c.reshape(ntm * ntn, BM, BN) if geom is None else tile_to_rows(c.reshape(ntm * ntn, BM * BN), geom)
     tm, tn = tile_coords(np.arange(ntm * ntn), M, N, BM, BN, group_m)
     out = np.empty((ntm, ntn, BM, BN), c.dtype)
     out[tm, tn] = tiles
@@ -116,6 +148,7 @@ class GemmBf16:
                 raise ValueError(f"K/64 ({K // 64}) must be even for tile {tile}")
             split_k = 2
         self.M, self.N, self.K, self.BM, self.BN, self.L, self.kernel = M, N, K, BM, BN, L, kname
+        self.geom = TILE_WAVES[tile]  # C tiles in fragment order
         self.split_k = max(1, int(split_k))
         self.tiles = (M // BM) * (N // BN)
         self.global_range = self.tiles * self.split_k * L
@@ -248,11 +281,11 @@ class GemmBf16:
         c, off = self.C.array, 0
         for s in range(panels):
             m, n = pm, (s + 1) * pn
-            out[s * pm:(s + 1) * pm, :n] = untile(c[off:off + m * n], m, n, self.BM, self.BN, self.group_m)
+            out[s * pm:(s + 1) * pm, :n] = untile(c[off:off + m * n], m, n, self.BM, self.BN, self.group_m, self.geom)
             off += m * n
             if s:
                 m, n = s * pm, pn
-                out[:s * pm, s * pn:(s + 1) * pn] = untile(c[off:off + m * n], m, n, self.BM, self.BN, self.group_m)
+                out[:s * pm, s * pn:(s + 1) * pn] = untile(c[off:off + m * n], m, n, self.BM, self.BN, self.group_m, self.geom)
                 off += m * n
         return out
 
@@ -282,7 +315,11 @@ class GemmBf16:
                 g = self.cr._cores.global_base + dev
                 lo, n = refs[g] * e, rng[g] * e
                 self._download_slice(dev, lo, n)
-        return untile(self.C.array, self.M, self.N, self.BM, self.BN, self.group_m)
+        return untile(self.C.array, self.M, self.N, self.BM, self.BN, self.group_m, self.geom)
+
+    def tile_block(self, flat: np.ndarray) -> np.ndarray:
+        """One C tile as stored (``BM·BN`` floats) → row-major ``[BM][BN]``."""
+        return flat.reshape(self.BM, self.BN) if self.geom is None else tile_to_rows(flat, self.geom)
 
     def spin_timeouts(self) -> int:
         """Exchange tiles only: how many work-groups gave up waiting for their
@@ -327,7 +364,7 @@ class GemmBf16:
             picks = np.array(sorted(picks))
             tm, tn = tile_coords(picks, self.M, self.N, self.BM, self.BN, self.group_m)
             for t, r, c in zip(picks, tm, tn):
-                got = self.C.array[t * tile:(t + 1) * tile].reshape(self.BM, self.BN).astype(np.float64)
+                got = self.tile_block(self.C.array[t * tile:(t + 1) * tile]).astype(np.float64)
                 ref = (a[r * self.BM:(r + 1) * self.BM].astype(np.float64)
                        @ b[c * self.BN:(c + 1) * self.BN].astype(np.float64).T)
                 worst = max(worst, float(np.max(np.abs(got - ref)) / max(float(np.max(np.abs(ref))), 1e-30)))
@@ -364,6 +401,7 @@ class GemmF32(GemmBf16):
         if M % BM or N % BN or K % 32:
             raise ValueError(f"M%{BM}, N%{BN} and K%32 must be 0 (got {M},{N},{K})")
         self.M, self.N, self.K, self.BM, self.BN, self.L, self.kernel = M, N, K, BM, BN, L, kname
+        self.geom = None  # the fp32 kernels store C tiles row-major
         self.split_k = 1
         self.tiles = (M // BM) * (N // BN)
         self.global_range = self.tiles * L

@@ -98,17 +98,41 @@ def test_library_arity_covers_every_kernel():
             assert k in ARITY, k
 
 
-def _tile_major(c, M, N, BM, BN, gm):
-    """Row-major [M][N] → tile-major in the kernels' grouped tile order."""
-    from cekirdekler_amd.ops.gemm import tile_coords
+def _tile_major(c, M, N, BM, BN, gm, geom=None):
+    """Row-major [M][N] → tile-major in the kernels' grouped tile order (each
+    tile in fragment order when ``geom`` is given, as the bf16 kernels store it)."""
+    from cekirdekler_amd.ops.gemm import rows_to_tile, tile_coords
 
     ntiles = (M // BM) * (N // BN)
     tm, tn = tile_coords(np.arange(ntiles), M, N, BM, BN, gm)
-    return np.concatenate([c[r * BM:(r + 1) * BM, q * BN:(q + 1) * BN].ravel() for r, q in zip(tm, tn)])
+    blocks = [c[r * BM:(r + 1) * BM, q * BN:(q + 1) * BN] for r, q in zip(tm, tn)]
+    return np.concatenate([(b if geom is None else rows_to_tile(b, geom)).ravel() for b in blocks])
 
 
+@pytest.mark.parametrize("tile", ["256x256pb", "256x128pe", "128x128"])
+def test_fragment_order_round_trip(tile):
+    """tile_to_rows / rows_to_tile are inverse, and the element the kernel
+    epilogue stores at ((((wr·WN + wc)·FM + i)·FN + j)·64 + fq·16 + fr)·4 + r
+    comes back at (wr·16FM + i·16 + fq·4 + r, wc·16FN + j·16 + fr)."""
+    from cekirdekler_amd.ops.gemm import TILE_WAVES, TILES, rows_to_tile, tile_to_rows
+
+    BM, BN = TILES[tile][:2]
+    WM, WN, FM, FN = geom = TILE_WAVES[tile]
+    assert (WM * FM * 16, WN * FN * 16) == (BM, BN)
+    rows = np.arange(BM * BN, dtype=np.float32).reshape(BM, BN)
+    flat = rows_to_tile(rows, geom)
+    np.testing.assert_array_equal(tile_to_rows(flat, geom), rows)
+    rng = np.random.default_rng(0)
+    for _ in range(64):
+        wr, wc, i, j = (int(rng.integers(n)) for n in (WM, WN, FM, FN))
+        fq, fr, r = int(rng.integers(4)), int(rng.integers(16)), int(rng.integers(4))
+        off = ((((wr * WN + wc) * FM + i) * FN + j) * 64 + fq * 16 + fr) * 4 + r
+        assert flat[off] == rows[wr * 16 * FM + i * 16 + fq * 4 + r, wc * 16 * FN + j * 16 + fr]
+
+
+@pytest.mark.parametrize("geom", [None, (2, 2, 4, 4)])
 @pytest.mark.parametrize("panels,gm", [(1, 2), (2, 2), (4, 1), (4, 3)])
-def test_shell_layout_round_trip(panels, gm):
+def test_shell_layout_round_trip(panels, gm, geom):
     """The host C layout of the square-shell stream (Cores::gemm_host_shells:
     shell by shell, R_s = rows of panel s × columns of panels 0..s, then
     C_s = rows of panels 0..s-1 × columns of panel s, each tile-major) is
@@ -117,15 +141,15 @@ def test_shell_layout_round_trip(panels, gm):
 
     from cekirdekler_amd.ops.gemm import GemmBf16
 
-    M, N, BM, BN = 512, 1024, 64, 128
+    M, N, BM, BN = 512, 1024, 128, 128
     full = np.random.default_rng(0).standard_normal((M, N)).astype(np.float32)
     pm, pn = M // panels, N // panels
     parts = []
     for s in range(panels):
-        parts.append(_tile_major(full[s * pm:(s + 1) * pm, :(s + 1) * pn], pm, (s + 1) * pn, BM, BN, gm))
+        parts.append(_tile_major(full[s * pm:(s + 1) * pm, :(s + 1) * pn], pm, (s + 1) * pn, BM, BN, gm, geom))
         if s:
-            parts.append(_tile_major(full[:s * pm, s * pn:(s + 1) * pn], s * pm, pn, BM, BN, gm))
+            parts.append(_tile_major(full[:s * pm, s * pn:(s + 1) * pn], s * pm, pn, BM, BN, gm, geom))
     host = np.concatenate(parts)
     assert host.size == M * N
-    g = SimpleNamespace(M=M, N=N, BM=BM, BN=BN, group_m=gm, C=SimpleNamespace(array=host))
+    g = SimpleNamespace(M=M, N=N, BM=BM, BN=BN, group_m=gm, geom=geom, C=SimpleNamespace(array=host))
     np.testing.assert_array_equal(GemmBf16.shells_result(g, panels), full)

@@ -80,7 +80,7 @@ for cid, blobs in enumerate(blob_list, start=10):
     tm, tn = tile_coords(picks, size, size, g.BM, g.BN, g.group_m)
     err = 0.0
     for t, r, c in zip(picks, tm, tn):
-        got = g.C.array[t * g.BM * g.BN:(t + 1) * g.BM * g.BN].reshape(g.BM, g.BN)
+        got = g.tile_block(g.C.array[t * g.BM * g.BN:(t + 1) * g.BM * g.BN])
         ref = a[r * g.BM:(r + 1) * g.BM].astype(np.float64) @ b[c * g.BN:(c + 1) * g.BN].astype(np.float64).T
         err = max(err, float(np.abs(got - ref).max() / np.abs(ref).max()))
     rec = cr.last_record()

@@ -69,7 +69,7 @@ picks = rng.choice(g2.tiles, 4, replace=False)
 tm, tn = tile_coords(picks, size, size, g2.BM, g2.BN, g2.group_m)
 err = 0.0
 for t, r, c in zip(picks, tm, tn):
-    got = g2.C.array[t * g2.BM * g2.BN:(t + 1) * g2.BM * g2.BN].reshape(g2.BM, g2.BN)
+    got = g2.tile_block(g2.C.array[t * g2.BM * g2.BN:(t + 1) * g2.BM * g2.BN])
     ref = a[r * g2.BM:(r + 1) * g2.BM].astype(np.float64) @ b[c * g2.BN:(c + 1) * g2.BN].astype(np.float64).T
     err = max(err, float(np.abs(got - ref).max() / np.abs(ref).max()))
 out["max_rel_err"] = err
