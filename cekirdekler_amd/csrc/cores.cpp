@@ -1505,16 +1505,22 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
   stage_peer_reads(c, st.ranges, h2d);
   DeviceFailure failure;
   int participants = 0;
+  std::vector<char> part(nloc, 0);
   for (int w = 0; w < nloc; ++w)
-    if (st.ranges[global_base_ + w] > 0 || (comm_ && (dist_gather_writes || dist_broadcast_reads || dist_split_reads)))
+    if (st.ranges[global_base_ + w] > 0 || (comm_ && (dist_gather_writes || dist_broadcast_reads || dist_split_reads))) {
+      part[w] = 1;
       ++participants;
+    }
   PhaseBarrier phase(participants);
   if (hazard && !enqueue_mode_ && participants > 1) phase_ = &phase;
   struct ResetPhase {
     PhaseBarrier*& p;
     ~ResetPhase() { p = nullptr; }
   } reset_phase{phase_};
-  if (nloc == 1 || (serial && !phase_)) {
+  // A device with an empty range does no device work; with at most one
+  // participant there is nothing to overlap, so no worker-thread hand-off
+  // (a device the overhead-aware balancer left out costs nothing per call).
+  if (nloc == 1 || (serial && !phase_) || participants <= 1) {
     for (int w = 0; w < nloc; ++w) {
       int g = global_base_ + w;
       try {
@@ -1525,6 +1531,7 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
     }
   } else {
     for (int w = 0; w < nloc; ++w) {
+      if (!part[w]) continue;
       int g = global_base_ + w;
       long long ref = st.references[g], rng = st.ranges[g];
       workers_[w]->post([=, &c, &ms, &h2d, &d2h] {
@@ -1532,6 +1539,15 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
       });
     }
     for (int w = 0; w < nloc; ++w) {
+      if (part[w]) continue;
+      try {
+        run_device(w, c, st.references[global_base_ + w], 0, pipelined, &ms[w], &h2d[w], &d2h[w]);
+      } catch (const std::exception& e) {
+        failure.add(w, e.what());
+      }
+    }
+    for (int w = 0; w < nloc; ++w) {
+      if (!part[w]) continue;
       try {
         workers_[w]->wait();
       } catch (const std::exception& e) {

@@ -742,3 +742,159 @@ extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8k_f32(const 
   out[o] = make_int2(min(ex + (int)(cnt.x + 0.5f), max_iter), min(ey + (int)(cnt.y + 0.5f), max_iter));
 }
 
+
+// blk8k with fewer instructions per wave ("blk8m": 16-iteration blocks from
+// iteration 16; "blk8n": 32-iteration blocks from iteration 32; "blk8p":
+// blk8n over NB = 4 consecutive 8×16 blocks per wave, one after the other):
+//  * wave-uniform prologue: the wave's band and block come from one scalar
+//    32-bit division of the work-group index (one-wave work-groups; the
+//    range offset is a multiple of 64), not a per-lane 64-bit division;
+//  * block 1 counted exactly, with a wave exit after 4 iterations as well as
+//    after 8 (half the exterior waves are done by then);
+//  * from iteration S the blocks are BIG iterations long: the block-end
+//    bookkeeping (|z|², 2 compares, 6 selects) is paid per BIG iterations;
+//  * the loop runs wave-uniformly (exit when no lane is still bounded at a
+//    block end), so its counter stays scalar;
+//  * the counting pass runs in chunks of 8 counted iterations from the last
+//    bounded block end and stops as soon as every lane has escaped, is
+//    interior, or has reached max_iter;
+//  * NB > 1: the kernel-argument and view loads and the wave launch are paid
+//    once per NB blocks (an exterior block is only ~40 instructions).
+// A lane escaped in block 1 keeps (0, z = 0) and is recounted from the start.
+// wave-uniform votes combined from the compare masks on the scalar unit
+// (a vote on a combined bool costs a VALU select and compare)
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ bool all_lanes(unsigned long long m) { return m == __builtin_amdgcn_read_exec(); }
+
+template <int BIG, int S>
+__device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ, const int max_iter) {
+  static_assert(BIG % 8 == 0 && S % 8 == 0 && S >= 8, "block lengths are multiples of 8");
+  const f32x2 two = {2.f, 2.f};
+  const f32x2 nbig = {-1048576.f, -1048576.f}, cbig = {4194304.f, 4194304.f};
+  f32x2 zr = {0.f, 0.f}, zi = {0.f, 0.f}, cnt = {0.f, 0.f}, tc = {1.f, 1.f};
+  auto counted = [&]() {
+    const f32x2 zi2 = zi * zi;
+    const f32x2 m = __builtin_elementwise_fma(zr, zr, zi2);
+    tc = pk_fma_clamp(m, nbig, cbig);
+    cnt += tc;
+    const f32x2 tz = zr * zi;
+    zr = __builtin_elementwise_fma(zr, zr, cr) - zi2;
+    zi = __builtin_elementwise_fma(tz, two, civ);
+  };
+  if (max_iter <= 8) {  // uniform: the whole range is one counted block
+    for (int u = 0; u < max_iter; ++u) counted();
+    return make_int2((int)(cnt.x + 0.5f), (int)(cnt.y + 0.5f));
+  }
+  // z0 = 0 is always bounded and z1 = c: start counted from there
+  zr = cr;
+  zi = civ;
+  cnt = f32x2{1.f, 1.f};
+#pragma unroll
+  for (int u = 1; u < 4; ++u) counted();
+  if (all_lanes(ballot(tc.x < 0.5f) & ballot(tc.y < 0.5f))) return make_int2((int)(cnt.x + 0.5f), (int)(cnt.y + 0.5f));
+#pragma unroll
+  for (int u = 0; u < 4; ++u) counted();
+  const bool dx1 = tc.x < 0.5f, dy1 = tc.y < 0.5f;
+  if (all_lanes(ballot(dx1) & ballot(dy1))) return make_int2((int)(cnt.x + 0.5f), (int)(cnt.y + 0.5f));
+  f32x2 fr = {0.f, 0.f}, fi = {0.f, 0.f};
+  int ex = 0, ey = 0;
+  if (!dx1) {
+    fr.x = zr.x;
+    fi.x = zi.x;
+    ex = 8;
+  }
+  if (!dy1) {
+    fr.y = zr.y;
+    fi.y = zi.y;
+    ey = 8;
+  }
+  auto block_end = [&](int it) -> bool {  // true while some lane is still bounded
+    const f32x2 m = __builtin_elementwise_fma(zr, zr, zi * zi);
+    const bool kx = m.x <= 4.f, ky = m.y <= 4.f;
+    if (kx) {
+      fr.x = zr.x;
+      fi.x = zi.x;
+      ex = it;
+    }
+    if (ky) {
+      fr.y = zr.y;
+      fi.y = zi.y;
+      ey = it;
+    }
+    return (ballot(kx) | ballot(ky)) != 0;
+  };
+  auto step = [&]() {
+    const f32x2 tz = zr * zi;
+    const f32x2 a = __builtin_elementwise_fma(zr, zr, cr);
+    zr = __builtin_elementwise_fma(-zi, zi, a);
+    zi = __builtin_elementwise_fma(tz, two, civ);
+  };
+  int it = 8;
+  bool live = true;
+  for (; live && it < S && it + 8 <= max_iter; it += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) step();
+    live = block_end(it + 8);
+  }
+  for (; live && it + BIG <= max_iter; it += BIG) {
+#pragma unroll
+    for (int u = 0; u < BIG; ++u) step();
+    live = block_end(it + BIG);
+  }
+  // counting pass from the last bounded block end; the remainder after the
+  // loop is shorter than BIG, so BIG counted iterations always suffice
+  cnt = f32x2{0.f, 0.f};
+  if (!all_lanes(ballot(ex >= max_iter) & ballot(ey >= max_iter))) {
+    zr = fr;
+    zi = fi;
+    for (int k = 0; k < BIG; k += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) counted();
+      const unsigned long long doneX = ballot(tc.x < 0.5f) | ballot(ex + k + 8 >= max_iter);
+      const unsigned long long doneY = ballot(tc.y < 0.5f) | ballot(ey + k + 8 >= max_iter);
+      if (all_lanes(doneX & doneY)) break;
+    }
+  }
+  return make_int2(min(ex + (int)(cnt.x + 0.5f), max_iter), min(ey + (int)(cnt.y + 0.5f), max_iter));
+}
+
+// NB consecutive 8×16 blocks of one 8-row band per wave (an 8 × 16·NB strip)
+template <int BIG, int S, int NB>
+__device__ __forceinline__ void mandel_blk8m(const float* view, const int* size, int2* out, long long off) {
+  const int W = size[0], max_iter = size[2];
+  const int wv = __builtin_amdgcn_readfirstlane((int)(((long long)blockIdx.x * 64 + off) >> 6));
+  const int spb = W / (16 * NB);  // strips per 8-row band
+  const int band = wv / spb, strip = wv - band * spb;
+  const int l = threadIdx.x;
+  const int r = l >> 3, c2 = (l & 7) * 2;
+  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
+  const float ci = y0 + (float)(band * 8 + r) * dy;
+  const f32x2 civ = {ci, ci};
+  int2* po = out + ((long long)band * 4 * W + strip * 8 * NB) + r * (W >> 1) + (l & 7);
+#pragma unroll 1
+  for (int b = 0; b < NB; ++b) {
+    const float crx = x0 + (float)((strip * NB + b) * 16 + c2) * dx;
+    const f32x2 cr = {crx, crx + dx};
+    po[b * 8] = mandel_blk8_core<BIG, S>(cr, civ, max_iter);
+  }
+}
+
+extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8m_f32(const float* view, const int* size,
+                                                                        int2* out, CEK_HIDDEN) {
+  mandel_blk8m<16, 16, 1>(view, size, out, __cek_off);
+}
+
+extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8n_f32(const float* view, const int* size,
+                                                                        int2* out, CEK_HIDDEN) {
+  mandel_blk8m<32, 32, 1>(view, size, out, __cek_off);
+}
+
+extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8p_f32(const float* view, const int* size,
+                                                                        int2* out, CEK_HIDDEN) {
+  mandel_blk8m<32, 32, 4>(view, size, out, __cek_off);
+}
+
+extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8q_f32(const float* view, const int* size,
+                                                                        int2* out, CEK_HIDDEN) {
+  mandel_blk8m<32, 32, 2>(view, size, out, __cek_off);
+}

@@ -20,7 +20,7 @@ FLOP_PER_ITER = 8
 
 # kernel variants; the band kernels additionally need device and pipeline
 # chunk ranges made of whole 16-row bands (see kernels/mandelbrot.hip)
-BAND_ROWS = {"blk16": 16, "blk16w4": 16, "blk64": 16, "blk8": 8, "blk8f": 8, "blk8g": 8, "blk16g": 16, "blk8h": 8, "blk8k": 8}  # rows per band
+BAND_ROWS = {"blk16": 16, "blk16w4": 16, "blk64": 16, "blk8": 8, "blk8f": 8, "blk8g": 8, "blk16g": 16, "blk8h": 8, "blk8k": 8, "blk8m": 8, "blk8n": 8, "blk8p": 8, "blk8q": 8}  # rows per band
 BAND_KERNELS = set(BAND_ROWS)
 KERNELS = {
     # name: (library kernel, pixels per work item, work-group size)
@@ -45,6 +45,15 @@ KERNELS = {
     # blk8h with a 4-instruction iteration, an exactly counted first block
     # (all-exterior waves end there) and no counting pass for interior waves
     "blk8k": ("cek_mandelbrot_blk8k_f32", 2, 64),
+    # blk8k with a scalar prologue, a wave exit after 4 counted iterations,
+    # 16- (blk8m) or 32-iteration (blk8n) blocks later on, a uniform loop and
+    # a chunked counting pass
+    "blk8m": ("cek_mandelbrot_blk8m_f32", 2, 64),
+    "blk8n": ("cek_mandelbrot_blk8n_f32", 2, 64),
+    # blk8n over 4 (blk8p) or 2 (blk8q) consecutive blocks per wave, one
+    # after the other: the wave launch and argument loads are paid per strip
+    "blk8p": ("cek_mandelbrot_blk8p_f32", 8, 64),
+    "blk8q": ("cek_mandelbrot_blk8q_f32", 4, 64),
 }
 
 
