@@ -107,7 +107,7 @@ def make_nbody():
 
 def make_mandel():
     x0 = float(rng.uniform(-2.0, -0.5))
-    m = MandelbrotRenderer(1024, 1024, max_iter=256, view=(x0, -1.0, 1.5, 2.0), cruncher=ref_cr, kernel="blk8h")
+    m = MandelbrotRenderer(1024, 1024, max_iter=256, view=(x0, -1.0, 1.5, 2.0), cruncher=ref_cr, kernel="blk8t")
     return m.view.next_param(m.size, m.out), m.kernel, m.global_range, m.local, m
 
 

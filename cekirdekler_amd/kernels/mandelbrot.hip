@@ -766,7 +766,67 @@ extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8k_f32(const 
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ bool all_lanes(unsigned long long m) { return m == __builtin_amdgcn_read_exec(); }
 
-template <int BIG, int S>
+// N iterations of the 4-instruction step in one hand-ordered stream:
+//   a = zr·zr + cr;  t = zr·zi;  zr' = −zi·zi + a;  zi' = 2t + ci
+// Every result is read two instructions after it is written, so the packed
+// FP32 read-after-write wait state is filled by the other chain; the
+// compiler's order (t, a, zr', zi') puts two s_nop per iteration in a
+// wave's stream.  One s_nop pads each end against the surrounding code.
+#define CEK_MANDEL_STEP                                                    \
+  "v_pk_fma_f32 %2, %0, %0, %4\n\t"                                       \
+  "v_pk_mul_f32 %3, %0, %1\n\t"                                           \
+  "v_pk_fma_f32 %0, %1, %1, %2 neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"         \
+  "v_pk_fma_f32 %1, %3, 2.0, %5 op_sel_hi:[1,0,1]\n\t"
+#define CEK_MANDEL_STEP4 CEK_MANDEL_STEP CEK_MANDEL_STEP CEK_MANDEL_STEP CEK_MANDEL_STEP
+template <int N>
+__device__ __forceinline__ void mandel_steps_asm(f32x2& zr, f32x2& zi, const f32x2 cr, const f32x2 civ) {
+  static_assert(N == 8 || N == 16 || N == 32, "8, 16 or 32 steps");
+  f32x2 a, t;
+  if constexpr (N == 8)
+    asm volatile("s_nop 0\n\t" CEK_MANDEL_STEP4 CEK_MANDEL_STEP4 "s_nop 0"
+                 : "+v"(zr), "+v"(zi), "=&v"(a), "=&v"(t) : "v"(cr), "v"(civ));
+  else if constexpr (N == 16)
+    asm volatile("s_nop 0\n\t" CEK_MANDEL_STEP4 CEK_MANDEL_STEP4 CEK_MANDEL_STEP4 CEK_MANDEL_STEP4 "s_nop 0"
+                 : "+v"(zr), "+v"(zi), "=&v"(a), "=&v"(t) : "v"(cr), "v"(civ));
+  else
+    asm volatile("s_nop 0\n\t" CEK_MANDEL_STEP4 CEK_MANDEL_STEP4 CEK_MANDEL_STEP4 CEK_MANDEL_STEP4
+                 CEK_MANDEL_STEP4 CEK_MANDEL_STEP4 CEK_MANDEL_STEP4 CEK_MANDEL_STEP4 "s_nop 0"
+                 : "+v"(zr), "+v"(zi), "=&v"(a), "=&v"(t) : "v"(cr), "v"(civ));
+}
+
+// N counted iterations (|z|² checked and counted every step), ordered so
+// that every result is read at least two instructions after it is written:
+//   q = zi·zi; t = zr·zi; m = zr·zr + q; a = zr·zr + cr; tc = clamp(m·nbig + cbig);
+//   zr = a − q; zi = 2t + ci; cnt += tc
+#define CEK_MANDEL_COUNT                                                   \
+  "v_pk_mul_f32 %4, %1, %1\n\t"                                           \
+  "v_pk_mul_f32 %5, %0, %1\n\t"                                           \
+  "v_pk_fma_f32 %6, %0, %0, %4\n\t"                                       \
+  "v_pk_fma_f32 %7, %0, %0, %8\n\t"                                       \
+  "v_pk_fma_f32 %3, %6, %10, %11 clamp\n\t"                               \
+  "v_pk_add_f32 %0, %7, %4 neg_lo:[0,1] neg_hi:[0,1]\n\t"                 \
+  "v_pk_fma_f32 %1, %5, 2.0, %9 op_sel_hi:[1,0,1]\n\t"                    \
+  "v_pk_add_f32 %2, %2, %3\n\t"
+template <int N>
+__device__ __forceinline__ void mandel_counted_asm(f32x2& zr, f32x2& zi, f32x2& cnt, f32x2& tc, const f32x2 cr,
+                                                   const f32x2 civ, const f32x2 nbig, const f32x2 cbig) {
+  static_assert(N == 3 || N == 4 || N == 8, "3, 4 or 8 counted steps");
+  f32x2 q, t, m, a;
+#define CEK_MANDEL_COUNT_ARGS                                              \
+  : "+v"(zr), "+v"(zi), "+v"(cnt), "=&v"(tc), "=&v"(q), "=&v"(t), "=&v"(m), "=&v"(a) \
+  : "v"(cr), "v"(civ), "v"(nbig), "v"(cbig)
+  if constexpr (N == 3)
+    asm volatile("s_nop 0\n\t" CEK_MANDEL_COUNT CEK_MANDEL_COUNT CEK_MANDEL_COUNT "s_nop 0" CEK_MANDEL_COUNT_ARGS);
+  else if constexpr (N == 4)
+    asm volatile("s_nop 0\n\t" CEK_MANDEL_COUNT CEK_MANDEL_COUNT CEK_MANDEL_COUNT CEK_MANDEL_COUNT
+                 "s_nop 0" CEK_MANDEL_COUNT_ARGS);
+  else
+    asm volatile("s_nop 0\n\t" CEK_MANDEL_COUNT CEK_MANDEL_COUNT CEK_MANDEL_COUNT CEK_MANDEL_COUNT
+                 CEK_MANDEL_COUNT CEK_MANDEL_COUNT CEK_MANDEL_COUNT CEK_MANDEL_COUNT "s_nop 0" CEK_MANDEL_COUNT_ARGS);
+#undef CEK_MANDEL_COUNT_ARGS
+}
+
+template <int BIG, int S, bool ASM = false>
 __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ, const int max_iter) {
   static_assert(BIG % 8 == 0 && S % 8 == 0 && S >= 8, "block lengths are multiples of 8");
   const f32x2 two = {2.f, 2.f};
@@ -789,11 +849,19 @@ __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ
   zr = cr;
   zi = civ;
   cnt = f32x2{1.f, 1.f};
+  if constexpr (ASM) {
+    mandel_counted_asm<3>(zr, zi, cnt, tc, cr, civ, nbig, cbig);
+  } else {
 #pragma unroll
-  for (int u = 1; u < 4; ++u) counted();
+    for (int u = 1; u < 4; ++u) counted();
+  }
   if (all_lanes(ballot(tc.x < 0.5f) & ballot(tc.y < 0.5f))) return make_int2((int)(cnt.x + 0.5f), (int)(cnt.y + 0.5f));
+  if constexpr (ASM) {
+    mandel_counted_asm<4>(zr, zi, cnt, tc, cr, civ, nbig, cbig);
+  } else {
 #pragma unroll
-  for (int u = 0; u < 4; ++u) counted();
+    for (int u = 0; u < 4; ++u) counted();
+  }
   const bool dx1 = tc.x < 0.5f, dy1 = tc.y < 0.5f;
   if (all_lanes(ballot(dx1) & ballot(dy1))) return make_int2((int)(cnt.x + 0.5f), (int)(cnt.y + 0.5f));
   f32x2 fr = {0.f, 0.f}, fi = {0.f, 0.f};
@@ -832,13 +900,21 @@ __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ
   int it = 8;
   bool live = true;
   for (; live && it < S && it + 8 <= max_iter; it += 8) {
+    if constexpr (ASM) {
+      mandel_steps_asm<8>(zr, zi, cr, civ);
+    } else {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) step();
+      for (int u = 0; u < 8; ++u) step();
+    }
     live = block_end(it + 8);
   }
   for (; live && it + BIG <= max_iter; it += BIG) {
+    if constexpr (ASM) {
+      mandel_steps_asm<BIG>(zr, zi, cr, civ);
+    } else {
 #pragma unroll
-    for (int u = 0; u < BIG; ++u) step();
+      for (int u = 0; u < BIG; ++u) step();
+    }
     live = block_end(it + BIG);
   }
   // counting pass from the last bounded block end; the remainder after the
@@ -848,8 +924,12 @@ __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ
     zr = fr;
     zi = fi;
     for (int k = 0; k < BIG; k += 8) {
+      if constexpr (ASM) {
+        mandel_counted_asm<8>(zr, zi, cnt, tc, cr, civ, nbig, cbig);
+      } else {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) counted();
+        for (int u = 0; u < 8; ++u) counted();
+      }
       const unsigned long long doneX = ballot(tc.x < 0.5f) | ballot(ex + k + 8 >= max_iter);
       const unsigned long long doneY = ballot(tc.y < 0.5f) | ballot(ey + k + 8 >= max_iter);
       if (all_lanes(doneX & doneY)) break;
@@ -859,7 +939,7 @@ __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ
 }
 
 // NB consecutive 8×16 blocks of one 8-row band per wave (an 8 × 16·NB strip)
-template <int BIG, int S, int NB>
+template <int BIG, int S, int NB, bool ASM = false>
 __device__ __forceinline__ void mandel_blk8m(const float* view, const int* size, int2* out, long long off) {
   const int W = size[0], max_iter = size[2];
   const int wv = __builtin_amdgcn_readfirstlane((int)(((long long)blockIdx.x * 64 + off) >> 6));
@@ -875,7 +955,7 @@ __device__ __forceinline__ void mandel_blk8m(const float* view, const int* size,
   for (int b = 0; b < NB; ++b) {
     const float crx = x0 + (float)((strip * NB + b) * 16 + c2) * dx;
     const f32x2 cr = {crx, crx + dx};
-    po[b * 8] = mandel_blk8_core<BIG, S>(cr, civ, max_iter);
+    po[b * 8] = mandel_blk8_core<BIG, S, ASM>(cr, civ, max_iter);
   }
 }
 
@@ -897,4 +977,15 @@ extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8p_f32(const 
 extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8q_f32(const float* view, const int* size,
                                                                         int2* out, CEK_HIDDEN) {
   mandel_blk8m<32, 32, 2>(view, size, out, __cek_off);
+}
+
+// blk8m / blk8n with the hand-ordered step stream (no s_nop in the loop)
+extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8s_f32(const float* view, const int* size,
+                                                                        int2* out, CEK_HIDDEN) {
+  mandel_blk8m<16, 16, 1, true>(view, size, out, __cek_off);
+}
+
+extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8t_f32(const float* view, const int* size,
+                                                                        int2* out, CEK_HIDDEN) {
+  mandel_blk8m<32, 32, 1, true>(view, size, out, __cek_off);
 }

@@ -20,7 +20,7 @@ FLOP_PER_ITER = 8
 
 # kernel variants; the band kernels additionally need device and pipeline
 # chunk ranges made of whole 16-row bands (see kernels/mandelbrot.hip)
-BAND_ROWS = {"blk16": 16, "blk16w4": 16, "blk64": 16, "blk8": 8, "blk8f": 8, "blk8g": 8, "blk16g": 16, "blk8h": 8, "blk8k": 8, "blk8m": 8, "blk8n": 8, "blk8p": 8, "blk8q": 8}  # rows per band
+BAND_ROWS = {"blk16": 16, "blk16w4": 16, "blk64": 16, "blk8": 8, "blk8f": 8, "blk8g": 8, "blk16g": 16, "blk8h": 8, "blk8k": 8, "blk8m": 8, "blk8n": 8, "blk8p": 8, "blk8q": 8, "blk8s": 8, "blk8t": 8}  # rows per band
 BAND_KERNELS = set(BAND_ROWS)
 KERNELS = {
     # name: (library kernel, pixels per work item, work-group size)
@@ -54,6 +54,9 @@ KERNELS = {
     # after the other: the wave launch and argument loads are paid per strip
     "blk8p": ("cek_mandelbrot_blk8p_f32", 8, 64),
     "blk8q": ("cek_mandelbrot_blk8q_f32", 4, 64),
+    # blk8m / blk8n with the iteration stream ordered by hand (inline asm)
+    "blk8s": ("cek_mandelbrot_blk8s_f32", 2, 64),
+    "blk8t": ("cek_mandelbrot_blk8t_f32", 2, 64),
 }
 
 

@@ -1,6 +1,9 @@
 """GPU probe: Mandelbrot 4096² kernel-only time (image left in device
 memory), variants interleaved over rounds in one process, median and min
-per variant; FLOPs from the escape counts (8 per iteration).
+per variant; FLOPs from the escape counts (8 per iteration).  The timed
+calls run in enqueue mode (back to back, no host sync per call), as in
+bench.py's kernel-only number; ``sync_ms_median`` is the same with a host
+sync per call.
 
     python tools/mandel_kernel_ab.py blk8,blk8g,blk8h [rounds] [reps]
 """
@@ -28,6 +31,7 @@ for k in kernels:
     m.out.write = False
     rs[k] = m
 ts = {k: [] for k in kernels}
+sync_ts = {k: [] for k in kernels}
 for r in range(rounds):
     for k, m in rs.items():
         for _ in range(3):
@@ -37,11 +41,19 @@ for r in range(rounds):
         for _ in range(reps):
             m.render(1, pipeline=False)
         torch.cuda.synchronize()
+        sync_ts[k].append((time.perf_counter() - t0) * 1e3 / reps)
+        t0 = time.perf_counter()
+        m.cr.enqueue_mode = True
+        for _ in range(reps):
+            m.render(1, pipeline=False)
+        m.cr.enqueue_mode = False
+        torch.cuda.synchronize()
         ts[k].append((time.perf_counter() - t0) * 1e3 / reps)
 out = {}
 for k in kernels:
     med = statistics.median(ts[k])
     out[k] = {"ms_median": round(med, 4), "ms_min": round(min(ts[k]), 4),
               "tflops_median": round(flops[k] / med / 1e9, 2),
-              "pct_fp32_peak_median": round(flops[k] / med / 1e9 / 157.3 * 100, 1)}
+              "pct_fp32_peak_median": round(flops[k] / med / 1e9 / 157.3 * 100, 1),
+              "sync_ms_median": round(statistics.median(sync_ts[k]), 4)}
 print(json.dumps(out), flush=True)
