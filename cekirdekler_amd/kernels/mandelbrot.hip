@@ -49,290 +49,19 @@ extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_f32(const float
 }
 
 // ---------------------------------------------------------------------------
-// Pool-scheduled variant.  A wave owns a pool of 64·PPW consecutive pixels
-// (PPW pixels per work item) and keeps two pixels in flight per lane; every
-// 8 iterations the lanes whose pixel escaped (or reached max_iter) retire it
-// into LDS and take the next pool pixel (ballot + mbcnt prefix, no atomics),
-// so a wave's lanes stay busy until the whole pool is drained instead of
-// idling behind the slowest of their own fixed pixels (≈73 % → ≈97 % lane
-// utilisation on the 4096² view).  The finished pool leaves LDS as coalesced
-// 16-byte stores.  Per pixel-iteration: 8 VALU ops (mul, fma, cmp, addc,
-// mul, fma, fma, add) with the escape count exact per iteration.
-template <int PPW>
-__device__ __forceinline__ void mandel_pool(const float* view, const int* size, int4* out,
-                                            long long off) {
-  constexpr int P = 64 * PPW;
-  __shared__ int res[4][P];
-  if (blockDim.x != 256) return;  // LDS pools are sized for 4 waves
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const long long wi0 = (long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63) + off;
-  const int pbase = (int)(wi0 * PPW);  // first pixel of the pool (W·H < 2^31)
-  const int W = size[0], max_iter = size[2];
-  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
-  const float invW = 1.0f / (float)W;
-  auto coords = [&](int p, float& cr, float& ci) {
-    const int g = pbase + p;
-    int y = (int)((float)g * invW);
-    int x = g - y * W;
-    if (x < 0) { --y; x += W; }
-    if (x >= W) { ++y; x -= W; }
-    cr = x0 + x * dx;
-    ci = y0 + y * dy;
-  };
-  int p0 = lane, p1 = lane + 64, next = 128;
-  float zr0 = 0.f, zi0 = 0.f, zr1 = 0.f, zi1 = 0.f, cr0, ci0, cr1, ci1, m0 = 0.f, m1 = 0.f;
-  int n0 = 0, n1 = 0;
-  coords(p0, cr0, ci0);
-  coords(p1, cr1, ci1);
-  // every pixel retires after at most ceil(max_iter/8) chunks, so the pool
-  // drains within this many chunks (a hard bound: the loop always exits)
-  const int chunk_cap = (P / 128 + 2) * ((max_iter + 7) / 8 + 1);
-  for (int chunk = 0; chunk < chunk_cap; ++chunk) {
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float zi20 = zi0 * zi0, zi21 = zi1 * zi1;
-      m0 = fmaf(zr0, zr0, zi20);
-      m1 = fmaf(zr1, zr1, zi21);
-      n0 += m0 <= 4.f;
-      n1 += m1 <= 4.f;
-      const float t0 = zr0 * zi0, t1 = zr1 * zi1;
-      zr0 = fmaf(zr0, zr0, -zi20) + cr0;
-      zr1 = fmaf(zr1, zr1, -zi21) + cr1;
-      zi0 = fmaf(t0, 2.f, ci0);
-      zi1 = fmaf(t1, 2.f, ci1);
-    }
-    const bool d0 = p0 < P && (!(m0 <= 4.f) || n0 >= max_iter);
-    const bool d1 = p1 < P && (!(m1 <= 4.f) || n1 >= max_iter);
-    const unsigned long long b0 = __ballot(d0), b1 = __ballot(d1);
-    if ((b0 | b1) != 0ull) {
-      if (d0) {
-        res[wv][p0] = min(n0, max_iter);
-        p0 = next + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(b0 >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo((unsigned)b0, 0u));
-        zr0 = zi0 = 0.f;
-        n0 = 0;
-        if (p0 < P) coords(p0, cr0, ci0);
-      }
-      next += __popcll(b0);
-      if (d1) {
-        res[wv][p1] = min(n1, max_iter);
-        p1 = next + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(b1 >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo((unsigned)b1, 0u));
-        zr1 = zi1 = 0.f;
-        n1 = 0;
-        if (p1 < P) coords(p1, cr1, ci1);
-      }
-      next += __popcll(b1);
-    }
-    if (__ballot(p0 < P || p1 < P) == 0ull) break;
-  }
-  __syncthreads();
-  const int4* r4 = reinterpret_cast<const int4*>(res[wv]);
-  int4* o = out + pbase / 4;
-#pragma unroll
-  for (int k = 0; k < PPW / 4; ++k) o[k * 64 + lane] = r4[k * 64 + lane];
-}
-
-extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_pool16_f32(const float* view, const int* size,
-                                                                          int4* out, CEK_HIDDEN) {
-  mandel_pool<16>(view, size, out, __cek_off);
-}
-
-extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_pool8_f32(const float* view, const int* size,
-                                                                         int4* out, CEK_HIDDEN) {
-  mandel_pool<8>(view, size, out, __cek_off);
-}
-
-// ---------------------------------------------------------------------------
-// Packed pool variant.  Same pool scheduling as above, but every operation of
-// the iteration is a packed-f32 instruction over a PAIR of pixels (on MI355X a
-// wave64 VALU instruction costs ~4 issue cycles packed or not, so packing
-// halves the cost per pixel), including the escape count: instead of a
-// per-pixel compare + carry-add, each iteration adds
+// Packed escape count: every operation of the iteration is a packed-f32
+// instruction over a PAIR of pixels (a wave64 VALU instruction costs ~4
+// issue cycles packed or not), including the count: each counted iteration
+// adds
 //     t = clamp(2^20 · (4 − |z|²), 0, 1)        (one v_pk_fma_f32 … clamp)
 // which is 1 while |z|² ≤ 4 − 2^-20 and 0 once the pixel escaped (±inf and NaN
 // clamp to 0), so the float sum is the escape iteration.  Only pixels whose
 // |z|² lands within 2^-20 of 4 can differ by one iteration from a strict
-// "|z|² > 4" test.  Per pixel-iteration: 4 packed instructions.
-// Two pairs (four pixels) in flight per lane.
+// "|z|² > 4" test.
 __device__ __forceinline__ f32x2 pk_fma_clamp(f32x2 a, f32x2 b, f32x2 c) {
   f32x2 r;
   asm("v_pk_fma_f32 %0, %1, %2, %3 clamp" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
-}
-
-template <int PPW>
-__device__ __forceinline__ void mandel_pool_pk(const float* view, const int* size, int4* out,
-                                               long long off) {
-  constexpr int P = 64 * PPW, NS = 4;  // pool pixels per wave, slots per lane
-  __shared__ int res[4][P];
-  if (blockDim.x != 256) return;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const long long wi0 = (long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63) + off;
-  const int pbase = (int)(wi0 * PPW);
-  const int W = size[0], max_iter = size[2];
-  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
-  const float invW = 1.0f / (float)W;
-  const float iter_cap = (float)max_iter - 0.5f;
-  auto coords = [&](int p, float& cr, float& ci) {
-    const int g = pbase + p;
-    int y = (int)((float)g * invW);
-    int x = g - y * W;
-    if (x < 0) { --y; x += W; }
-    if (x >= W) { ++y; x -= W; }
-    cr = x0 + x * dx;
-    ci = y0 + y * dy;
-  };
-  // slot s of this lane: pair s/2, element s%2
-  f32x2 zr[2], zi[2], cr[2], ci[2], cnt[2], t[2];
-  int pix[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) pix[s] = lane + 64 * s;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    float a, b, c, d;
-    coords(pix[2 * q], a, b);
-    coords(pix[2 * q + 1], c, d);
-    cr[q] = f32x2{a, c};
-    ci[q] = f32x2{b, d};
-    zr[q] = zi[q] = cnt[q] = t[q] = f32x2{0.f, 0.f};
-  }
-  int next = 64 * NS;
-  const f32x2 nbig = {-1048576.f, -1048576.f}, cbig = {4194304.f, 4194304.f}, two = {2.f, 2.f};
-  const int chunk_cap = (P / (64 * NS) + 2) * ((max_iter + 7) / 8 + 1);
-  for (int chunk = 0; chunk < chunk_cap; ++chunk) {
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const f32x2 zi2 = zi[q] * zi[q];
-        const f32x2 m = __builtin_elementwise_fma(zr[q], zr[q], zi2);
-        t[q] = pk_fma_clamp(m, nbig, cbig);
-        cnt[q] += t[q];
-        const f32x2 tz = zr[q] * zi[q];
-        zr[q] = __builtin_elementwise_fma(zr[q], zr[q], -zi2) + cr[q];
-        zi[q] = __builtin_elementwise_fma(tz, two, ci[q]);
-      }
-    }
-    bool d[NS];
-    unsigned long long b[NS], any = 0ull;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const float ts = (s & 1) ? t[s >> 1].y : t[s >> 1].x;
-      const float cs = (s & 1) ? cnt[s >> 1].y : cnt[s >> 1].x;
-      d[s] = pix[s] < P && (ts < 0.5f || cs >= iter_cap);
-      b[s] = __ballot(d[s]);
-      any |= b[s];
-    }
-    if (any != 0ull) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        if (d[s]) {
-          const int q = s >> 1;
-          const float cs = (s & 1) ? cnt[q].y : cnt[q].x;
-          res[wv][pix[s]] = min((int)(cs + 0.5f), max_iter);
-          pix[s] = next + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(b[s] >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((unsigned)b[s], 0u));
-          float a = 0.f, c = 0.f;
-          if (pix[s] < P) coords(pix[s], a, c);
-          if (s & 1) {
-            zr[q].y = zi[q].y = cnt[q].y = 0.f;
-            t[q].y = 1.f;
-            cr[q].y = a;
-            ci[q].y = c;
-          } else {
-            zr[q].x = zi[q].x = cnt[q].x = 0.f;
-            t[q].x = 1.f;
-            cr[q].x = a;
-            ci[q].x = c;
-          }
-        }
-        next += __popcll(b[s]);
-      }
-    }
-    bool live = false;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) live |= pix[s] < P;
-    if (__ballot(live) == 0ull) break;
-  }
-  __syncthreads();
-  const int4* r4 = reinterpret_cast<const int4*>(res[wv]);
-  int4* o = out + pbase / 4;
-#pragma unroll
-  for (int k = 0; k < PPW / 4; ++k) o[k * 64 + lane] = r4[k * 64 + lane];
-}
-
-extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_pk16_f32(const float* view, const int* size,
-                                                                        int4* out, CEK_HIDDEN) {
-  mandel_pool_pk<16>(view, size, out, __cek_off);
-}
-
-extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_pk32_f32(const float* view, const int* size,
-                                                                        int4* out, CEK_HIDDEN) {
-  mandel_pool_pk<32>(view, size, out, __cek_off);
-}
-
-// ---------------------------------------------------------------------------
-// 2-D block variant.  Pixel coherence, not pooling: the range is cut into
-// bands of 16 image rows (4·W work items; compute() keeps device and
-// pipeline-chunk ranges whole bands via its granularity), and each wave of
-// a band computes one 16×16 pixel block — lane l owns row l/4, columns
-// 4·(l%4) … +3 as two packed pairs.  Neighbouring pixels escape at similar
-// iterations, so a wave's lanes stay busy (85 % on the 4096² view vs 73 % for
-// 256×1 strips) without any refill bookkeeping; the count uses the packed
-// clamp of the pooled variant (4 packed instructions per pixel-iteration).
-// NB blocks per wave, processed one after another (NB·4 pixels per work
-// item): longer-lived waves amortise workgroup dispatch, which capped the
-// one-block version at ~3.4 resident waves per SIMD (PMC).
-template <int NB>
-__device__ __forceinline__ void mandel_blk(const float* view, const int* size, int4* out, long long off) {
-  const long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x + off;
-  const int W = size[0], max_iter = size[2];
-  const long long band_items = 4LL * W / NB;  // 16 rows × W px / (4·NB px per work item)
-  const long long band = w / band_items;
-  const int q = (int)(w - band * band_items);
-  const int wave_in_band = q >> 6, l = q & 63;
-  const int row = (int)band * 16 + (l >> 2);
-  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
-  const float ci = y0 + row * dy;
-  const f32x2 civ = {ci, ci};
-  const f32x2 nbig = {-1048576.f, -1048576.f}, cbig = {4194304.f, 4194304.f}, two = {2.f, 2.f};
-  for (int b = 0; b < NB; ++b) {
-    const int col = (wave_in_band * NB + b) * 16 + (l & 3) * 4;
-    f32x2 cr[2] = {{x0 + col * dx, x0 + (col + 1) * dx}, {x0 + (col + 2) * dx, x0 + (col + 3) * dx}};
-    f32x2 zr[2] = {{0.f, 0.f}, {0.f, 0.f}}, zi[2] = {{0.f, 0.f}, {0.f, 0.f}};
-    f32x2 cnt[2] = {{0.f, 0.f}, {0.f, 0.f}}, t[2] = {{1.f, 1.f}, {1.f, 1.f}};
-    for (int it = 0; it < max_iter; it += 8) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const f32x2 zi2 = zi[p] * zi[p];
-          const f32x2 m = __builtin_elementwise_fma(zr[p], zr[p], zi2);
-          t[p] = pk_fma_clamp(m, nbig, cbig);
-          cnt[p] += t[p];
-          const f32x2 tz = zr[p] * zi[p];
-          zr[p] = __builtin_elementwise_fma(zr[p], zr[p], -zi2) + cr[p];
-          zi[p] = __builtin_elementwise_fma(tz, two, civ);
-        }
-      }
-      // a lane is done with this block once all four of its pixels escaped
-      const f32x2 tm = __builtin_elementwise_max(t[0], t[1]);
-      if (tm.x < 0.5f && tm.y < 0.5f) break;
-    }
-    auto fin = [&](float c) { return min((int)(c + 0.5f), max_iter); };
-    out[((long long)row * W + col) >> 2] = make_int4(fin(cnt[0].x), fin(cnt[0].y), fin(cnt[1].x), fin(cnt[1].y));
-  }
-}
-
-extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_blk16_f32(const float* view, const int* size,
-                                                                         int4* out, CEK_HIDDEN) {
-  mandel_blk<1>(view, size, out, __cek_off);
-}
-
-extern "C" __global__ __launch_bounds__(256) void cek_mandelbrot_blk64_f32(const float* view, const int* size,
-                                                                         int4* out, CEK_HIDDEN) {
-  mandel_blk<4>(view, size, out, __cek_off);
 }
 
 // 8×16 pixel block per wave, one packed pair (2 horizontally adjacent
@@ -369,214 +98,8 @@ extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8_f32(const f
   out[((long long)row * W + col) >> 1] = make_int2(min((int)(cnt.x + 0.5f), max_iter), min((int)(cnt.y + 0.5f), max_iter));
 }
 
-// blk8 with deferred escape counting ("blk8f"): the same 8×16 block per
-// one-wave work-group and the same packed z update, but the 8-iteration
-// blocks run without the per-iteration escape count (5 packed instructions
-// per pair-iteration instead of 8).  At each block's end |z|² decides which
-// pixels escaped somewhere in it; such a pixel freezes the z it had at that
-// block's start, and ONE counting pass over 8 iterations from the frozen z
-// (the blk8 arithmetic, bit for bit) after the loop gives the exact escape
-// iteration.  Escape is monotone once |z|² > 4 (|z| keeps growing), and a z
-// that overflowed to inf/NaN fails `m <= 4` as well, so the block-end test
-// cannot miss an escape inside the block.  Output identical to blk8.
-extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8f_f32(const float* view, const int* size,
-                                                                        int2* out, CEK_HIDDEN) {
-  const long long w = cek_global_id();
-  const int W = size[0], max_iter = size[2];
-  const long long band_items = 4LL * W;
-  const long long band = w / band_items;
-  const int q = (int)(w - band * band_items);
-  const int blk = q >> 6, l = q & 63;
-  const int row = (int)band * 8 + (l >> 3), col = blk * 16 + (l & 7) * 2;
-  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
-  const float ci = y0 + row * dy;
-  const f32x2 cr = {x0 + col * dx, x0 + (col + 1) * dx}, civ = {ci, ci};
-  const f32x2 two = {2.f, 2.f};
-  f32x2 zr = {0.f, 0.f}, zi = {0.f, 0.f};
-  f32x2 fr = {0.f, 0.f}, fi = {0.f, 0.f};  // z at the start of the escape block
-  int ex = -1, ey = -1;                    // escape block's first iteration
-  for (int it = 0; it < max_iter; it += 8) {
-    const f32x2 sr = zr, si = zi;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const f32x2 zi2 = zi * zi;
-      const f32x2 tz = zr * zi;
-      zr = __builtin_elementwise_fma(zr, zr, -zi2) + cr;
-      zi = __builtin_elementwise_fma(tz, two, civ);
-    }
-    const f32x2 m = __builtin_elementwise_fma(zr, zr, zi * zi);
-    if (ex < 0 && !(m.x <= 4.f)) {
-      ex = it;
-      fr.x = sr.x;
-      fi.x = si.x;
-    }
-    if (ey < 0 && !(m.y <= 4.f)) {
-      ey = it;
-      fr.y = sr.y;
-      fi.y = si.y;
-    }
-    if (ex >= 0 && ey >= 0) break;
-  }
-  // exact count inside the escape block: blk8's counting iteration from the
-  // frozen z (the m <= 4 iterations before the first escape)
-  const f32x2 nbig = {-1048576.f, -1048576.f}, cbig = {4194304.f, 4194304.f};
-  f32x2 cnt = {0.f, 0.f};
-  zr = fr;
-  zi = fi;
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const f32x2 zi2 = zi * zi;
-    const f32x2 m = __builtin_elementwise_fma(zr, zr, zi2);
-    cnt += pk_fma_clamp(m, nbig, cbig);
-    const f32x2 tz = zr * zi;
-    zr = __builtin_elementwise_fma(zr, zr, -zi2) + cr;
-    zi = __builtin_elementwise_fma(tz, two, civ);
-  }
-  const int nx = ex < 0 ? max_iter : min(ex + (int)(cnt.x + 0.5f), max_iter);
-  const int ny = ey < 0 ? max_iter : min(ey + (int)(cnt.y + 0.5f), max_iter);
-  out[((long long)row * W + col) >> 1] = make_int2(nx, ny);
-}
-
-// blk8f with zr' = fma(zr, zr, cr) − zi² instead of fma(zr, zr, −zi²) + cr:
-// the fma no longer waits for zi², so the zr chain is two dependent ops per
-// iteration instead of three (different rounding from blk8, same count of
-// instructions).
-extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8g_f32(const float* view, const int* size,
-                                                                        int2* out, CEK_HIDDEN) {
-  const long long w = cek_global_id();
-  const int W = size[0], max_iter = size[2];
-  const long long band_items = 4LL * W;
-  const long long band = w / band_items;
-  const int q = (int)(w - band * band_items);
-  const int blk = q >> 6, l = q & 63;
-  const int row = (int)band * 8 + (l >> 3), col = blk * 16 + (l & 7) * 2;
-  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
-  const float ci = y0 + row * dy;
-  const f32x2 cr = {x0 + col * dx, x0 + (col + 1) * dx}, civ = {ci, ci};
-  const f32x2 two = {2.f, 2.f};
-  f32x2 zr = {0.f, 0.f}, zi = {0.f, 0.f};
-  f32x2 fr = {0.f, 0.f}, fi = {0.f, 0.f};  // z at the start of the escape block
-  int ex = -1, ey = -1;                    // escape block's first iteration
-  for (int it = 0; it < max_iter; it += 8) {
-    const f32x2 sr = zr, si = zi;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const f32x2 zi2 = zi * zi;
-      const f32x2 tz = zr * zi;
-      zr = __builtin_elementwise_fma(zr, zr, cr) - zi2;
-      zi = __builtin_elementwise_fma(tz, two, civ);
-    }
-    const f32x2 m = __builtin_elementwise_fma(zr, zr, zi * zi);
-    if (ex < 0 && !(m.x <= 4.f)) {
-      ex = it;
-      fr.x = sr.x;
-      fi.x = si.x;
-    }
-    if (ey < 0 && !(m.y <= 4.f)) {
-      ey = it;
-      fr.y = sr.y;
-      fi.y = si.y;
-    }
-    if (ex >= 0 && ey >= 0) break;
-  }
-  // exact count inside the escape block: blk8's counting iteration from the
-  // frozen z (the m <= 4 iterations before the first escape)
-  const f32x2 nbig = {-1048576.f, -1048576.f}, cbig = {4194304.f, 4194304.f};
-  f32x2 cnt = {0.f, 0.f};
-  zr = fr;
-  zi = fi;
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const f32x2 zi2 = zi * zi;
-    const f32x2 m = __builtin_elementwise_fma(zr, zr, zi2);
-    cnt += pk_fma_clamp(m, nbig, cbig);
-    const f32x2 tz = zr * zi;
-    zr = __builtin_elementwise_fma(zr, zr, cr) - zi2;
-    zi = __builtin_elementwise_fma(tz, two, civ);
-  }
-  const int nx = ex < 0 ? max_iter : min(ex + (int)(cnt.x + 0.5f), max_iter);
-  const int ny = ey < 0 ? max_iter : min(ey + (int)(cnt.y + 0.5f), max_iter);
-  out[((long long)row * W + col) >> 1] = make_int2(nx, ny);
-}
-
-// blk8g with two packed pairs per lane: a 16×16 block per one-wave
-// work-group (rows r and r + 8 of a 16-row band), twice the independent
-// work per wave for the same deferred-count iteration ("blk16g").
-extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk16g_f32(const float* view, const int* size,
-                                                                         int2* out, CEK_HIDDEN) {
-  const long long w = cek_global_id();
-  const int W = size[0], max_iter = size[2];
-  const long long band_items = 4LL * W;  // 16 rows × W px / 4 px per work item
-  const long long band = w / band_items;
-  const int q = (int)(w - band * band_items);
-  const int blk = q >> 6, l = q & 63;
-  const int row0 = (int)band * 16 + (l >> 3), col = blk * 16 + (l & 7) * 2;
-  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
-  const f32x2 cr = {x0 + col * dx, x0 + (col + 1) * dx};
-  const f32x2 two = {2.f, 2.f};
-  f32x2 civ[2], zr[2], zi[2], fr[2], fi[2];
-  int e[2][2];
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const float ci = y0 + (row0 + 8 * p) * dy;
-    civ[p] = f32x2{ci, ci};
-    zr[p] = zi[p] = fr[p] = fi[p] = f32x2{0.f, 0.f};
-    e[p][0] = e[p][1] = -1;
-  }
-  for (int it = 0; it < max_iter; it += 8) {
-    f32x2 sr[2], si[2];
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      sr[p] = zr[p];
-      si[p] = zi[p];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const f32x2 zi2 = zi[p] * zi[p];
-        const f32x2 tz = zr[p] * zi[p];
-        zr[p] = __builtin_elementwise_fma(zr[p], zr[p], cr) - zi2;
-        zi[p] = __builtin_elementwise_fma(tz, two, civ[p]);
-      }
-    bool all = true;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const f32x2 m = __builtin_elementwise_fma(zr[p], zr[p], zi[p] * zi[p]);
-      if (e[p][0] < 0 && !(m.x <= 4.f)) {
-        e[p][0] = it;
-        fr[p].x = sr[p].x;
-        fi[p].x = si[p].x;
-      }
-      if (e[p][1] < 0 && !(m.y <= 4.f)) {
-        e[p][1] = it;
-        fr[p].y = sr[p].y;
-        fi[p].y = si[p].y;
-      }
-      all = all && e[p][0] >= 0 && e[p][1] >= 0;
-    }
-    if (all) break;
-  }
-  const f32x2 nbig = {-1048576.f, -1048576.f}, cbig = {4194304.f, 4194304.f};
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    f32x2 cnt = {0.f, 0.f}, ar = fr[p], ai = fi[p];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const f32x2 zi2 = ai * ai;
-      const f32x2 m = __builtin_elementwise_fma(ar, ar, zi2);
-      cnt += pk_fma_clamp(m, nbig, cbig);
-      const f32x2 tz = ar * ai;
-      ar = __builtin_elementwise_fma(ar, ar, cr) - zi2;
-      ai = __builtin_elementwise_fma(tz, two, civ[p]);
-    }
-    const int nx = e[p][0] < 0 ? max_iter : min(e[p][0] + (int)(cnt.x + 0.5f), max_iter);
-    const int ny = e[p][1] < 0 ? max_iter : min(e[p][1] + (int)(cnt.y + 0.5f), max_iter);
-    out[((long long)(row0 + 8 * p) * W + col) >> 1] = make_int2(nx, ny);
-  }
-}
-
-// blk8g with cheaper bookkeeping ("blk8h"): at each block's end a pixel
+// Deferred escape counting with cheap bookkeeping ("blk8h"): the 8-iteration
+// blocks run without the per-iteration escape count; at each block's end a pixel
 // whose |z|² is still <= 4 records that z and the iteration (it + 8) as its
 // last known non-escaped point; an escaped pixel stops recording (escape is
 // monotone, inf/NaN fail `m <= 4`).  No start-of-block copies and no "already
@@ -742,25 +265,24 @@ extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8k_f32(const 
   out[o] = make_int2(min(ex + (int)(cnt.x + 0.5f), max_iter), min(ey + (int)(cnt.y + 0.5f), max_iter));
 }
 
-
 // blk8k with fewer instructions per wave ("blk8m": 16-iteration blocks from
-// iteration 16; "blk8n": 32-iteration blocks from iteration 32; "blk8p":
-// blk8n over NB = 4 consecutive 8×16 blocks per wave, one after the other):
+// iteration 16; "blk8t": 32-iteration blocks from iteration 32, with the
+// iteration and counting streams ordered by hand):
 //  * wave-uniform prologue: the wave's band and block come from one scalar
 //    32-bit division of the work-group index (one-wave work-groups; the
 //    range offset is a multiple of 64), not a per-lane 64-bit division;
-//  * block 1 counted exactly, with a wave exit after 4 iterations as well as
-//    after 8 (half the exterior waves are done by then);
+//  * block 1 counted exactly from z1 = c, with a wave exit after 4 iterations
+//    as well as after 8 (half the exterior waves are done by then);
 //  * from iteration S the blocks are BIG iterations long: the block-end
 //    bookkeeping (|z|², 2 compares, 6 selects) is paid per BIG iterations;
 //  * the loop runs wave-uniformly (exit when no lane is still bounded at a
 //    block end), so its counter stays scalar;
 //  * the counting pass runs in chunks of 8 counted iterations from the last
 //    bounded block end and stops as soon as every lane has escaped, is
-//    interior, or has reached max_iter;
-//  * NB > 1: the kernel-argument and view loads and the wave launch are paid
-//    once per NB blocks (an exterior block is only ~40 instructions).
+//    interior, or has reached max_iter.
 // A lane escaped in block 1 keeps (0, z = 0) and is recounted from the start.
+// Measured: profiles/mandelbrot_r3.md.
+
 // wave-uniform votes combined from the compare masks on the scalar unit
 // (a vote on a combined bool costs a VALU select and compare)
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
@@ -826,7 +348,7 @@ __device__ __forceinline__ void mandel_counted_asm(f32x2& zr, f32x2& zi, f32x2& 
 #undef CEK_MANDEL_COUNT_ARGS
 }
 
-template <int BIG, int S, bool ASM = false>
+template <int BIG, int S, bool ASM>
 __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ, const int max_iter) {
   static_assert(BIG % 8 == 0 && S % 8 == 0 && S >= 8, "block lengths are multiples of 8");
   const f32x2 two = {2.f, 2.f};
@@ -938,54 +460,28 @@ __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ
   return make_int2(min(ex + (int)(cnt.x + 0.5f), max_iter), min(ey + (int)(cnt.y + 0.5f), max_iter));
 }
 
-// NB consecutive 8×16 blocks of one 8-row band per wave (an 8 × 16·NB strip)
-template <int BIG, int S, int NB, bool ASM = false>
+// one 8×16 block of an 8-row band per one-wave work-group
+template <int BIG, int S, bool ASM>
 __device__ __forceinline__ void mandel_blk8m(const float* view, const int* size, int2* out, long long off) {
   const int W = size[0], max_iter = size[2];
   const int wv = __builtin_amdgcn_readfirstlane((int)(((long long)blockIdx.x * 64 + off) >> 6));
-  const int spb = W / (16 * NB);  // strips per 8-row band
-  const int band = wv / spb, strip = wv - band * spb;
+  const int bpb = W >> 4;  // blocks per band
+  const int band = wv / bpb, blk = wv - band * bpb;
   const int l = threadIdx.x;
   const int r = l >> 3, c2 = (l & 7) * 2;
   const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
   const float ci = y0 + (float)(band * 8 + r) * dy;
-  const f32x2 civ = {ci, ci};
-  int2* po = out + ((long long)band * 4 * W + strip * 8 * NB) + r * (W >> 1) + (l & 7);
-#pragma unroll 1
-  for (int b = 0; b < NB; ++b) {
-    const float crx = x0 + (float)((strip * NB + b) * 16 + c2) * dx;
-    const f32x2 cr = {crx, crx + dx};
-    po[b * 8] = mandel_blk8_core<BIG, S, ASM>(cr, civ, max_iter);
-  }
+  const float crx = x0 + (float)(blk * 16 + c2) * dx;
+  const f32x2 cr = {crx, crx + dx}, civ = {ci, ci};
+  out[((long long)band * 4 * W + blk * 8) + r * (W >> 1) + (l & 7)] = mandel_blk8_core<BIG, S, ASM>(cr, civ, max_iter);
 }
 
 extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8m_f32(const float* view, const int* size,
                                                                         int2* out, CEK_HIDDEN) {
-  mandel_blk8m<16, 16, 1>(view, size, out, __cek_off);
-}
-
-extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8n_f32(const float* view, const int* size,
-                                                                        int2* out, CEK_HIDDEN) {
-  mandel_blk8m<32, 32, 1>(view, size, out, __cek_off);
-}
-
-extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8p_f32(const float* view, const int* size,
-                                                                        int2* out, CEK_HIDDEN) {
-  mandel_blk8m<32, 32, 4>(view, size, out, __cek_off);
-}
-
-extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8q_f32(const float* view, const int* size,
-                                                                        int2* out, CEK_HIDDEN) {
-  mandel_blk8m<32, 32, 2>(view, size, out, __cek_off);
-}
-
-// blk8m / blk8n with the hand-ordered step stream (no s_nop in the loop)
-extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8s_f32(const float* view, const int* size,
-                                                                        int2* out, CEK_HIDDEN) {
-  mandel_blk8m<16, 16, 1, true>(view, size, out, __cek_off);
+  mandel_blk8m<16, 16, false>(view, size, out, __cek_off);
 }
 
 extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8t_f32(const float* view, const int* size,
                                                                         int2* out, CEK_HIDDEN) {
-  mandel_blk8m<32, 32, 1, true>(view, size, out, __cek_off);
+  mandel_blk8m<32, 32, true>(view, size, out, __cek_off);
 }

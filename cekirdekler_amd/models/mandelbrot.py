@@ -20,42 +20,26 @@ FLOP_PER_ITER = 8
 
 # kernel variants; the band kernels additionally need device and pipeline
 # chunk ranges made of whole 16-row bands (see kernels/mandelbrot.hip)
-BAND_ROWS = {"blk16": 16, "blk16w4": 16, "blk64": 16, "blk8": 8, "blk8f": 8, "blk8g": 8, "blk16g": 16, "blk8h": 8, "blk8k": 8, "blk8m": 8, "blk8n": 8, "blk8p": 8, "blk8q": 8, "blk8s": 8, "blk8t": 8}  # rows per band
+BAND_ROWS = {"blk8": 8, "blk8h": 8, "blk8k": 8, "blk8m": 8, "blk8t": 8}  # rows per band
 BAND_KERNELS = set(BAND_ROWS)
 KERNELS = {
     # name: (library kernel, pixels per work item, work-group size)
     "quad": ("cek_mandelbrot_f32", 4, 256),           # 4 fixed pixels per work item
-    "pool8": ("cek_mandelbrot_pool8_f32", 8, 256),     # wave-pooled, 512-pixel pools
-    "pool16": ("cek_mandelbrot_pool16_f32", 16, 256),  # wave-pooled, 1024-pixel pools
-    "pk16": ("cek_mandelbrot_pk16_f32", 16, 256),      # pooled, packed pairs + clamp count
-    "pk32": ("cek_mandelbrot_pk32_f32", 32, 256),      # same, 2048-pixel pools
-    # 16×16 pixel block per wave, packed; one-wave work-groups so a finished
-    # wave's slot is refilled at once (a 4-wave group holds all four SIMD
-    # slots until its slowest block is done)
-    "blk16": ("cek_mandelbrot_blk16_f32", 4, 64),
-    "blk16w4": ("cek_mandelbrot_blk16_f32", 4, 256),
-    "blk64": ("cek_mandelbrot_blk64_f32", 16, 64),     # four 16×16 blocks per wave
-    "blk8": ("cek_mandelbrot_blk8_f32", 2, 64),        # 8×16 block per wave, one pair per lane
-    # same block, escape counted once after the loop from the z frozen at the
-    # escape block's start (5 instead of 8 packed instructions per iteration)
-    "blk8f": ("cek_mandelbrot_blk8f_f32", 2, 64),
-    "blk8g": ("cek_mandelbrot_blk8g_f32", 2, 64),     # blk8f, zr chain reassociated (2 deep)
-    "blk16g": ("cek_mandelbrot_blk16g_f32", 4, 64),   # blk8g, two pairs per lane (16×16 block)
-    "blk8h": ("cek_mandelbrot_blk8h_f32", 2, 64),     # blk8g, last non-escaped z recorded per block
+    # 8×16 pixel block per one-wave work-group (one packed pair per lane):
+    # neighbouring pixels escape at similar iterations, and a finished wave's
+    # slot is refilled at once
+    "blk8": ("cek_mandelbrot_blk8_f32", 2, 64),        # escape counted every iteration
+    # escape checked once per 8 iterations, counted after the loop from the
+    # last bounded z (5 packed instructions per iteration instead of 8)
+    "blk8h": ("cek_mandelbrot_blk8h_f32", 2, 64),
     # blk8h with a 4-instruction iteration, an exactly counted first block
     # (all-exterior waves end there) and no counting pass for interior waves
     "blk8k": ("cek_mandelbrot_blk8k_f32", 2, 64),
     # blk8k with a scalar prologue, a wave exit after 4 counted iterations,
-    # 16- (blk8m) or 32-iteration (blk8n) blocks later on, a uniform loop and
-    # a chunked counting pass
+    # 16-iteration blocks later on, a uniform loop and a chunked counting pass
     "blk8m": ("cek_mandelbrot_blk8m_f32", 2, 64),
-    "blk8n": ("cek_mandelbrot_blk8n_f32", 2, 64),
-    # blk8n over 4 (blk8p) or 2 (blk8q) consecutive blocks per wave, one
-    # after the other: the wave launch and argument loads are paid per strip
-    "blk8p": ("cek_mandelbrot_blk8p_f32", 8, 64),
-    "blk8q": ("cek_mandelbrot_blk8q_f32", 4, 64),
-    # blk8m / blk8n with the iteration stream ordered by hand (inline asm)
-    "blk8s": ("cek_mandelbrot_blk8s_f32", 2, 64),
+    # blk8m with 32-iteration blocks and hand-ordered instruction streams
+    # (the fastest; bench.py's kernel-only number)
     "blk8t": ("cek_mandelbrot_blk8t_f32", 2, 64),
 }
 

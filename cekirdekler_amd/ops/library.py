@@ -22,9 +22,8 @@ LIBRARY = {
     "sgemm_f32": ["cek_sgemm_f32_128x128", "cek_sgemm_f32_256x128", "cek_sgemm_f32_256x256",
                   "cek_sgemm_f32_256x256ir", "cek_sgemm_f32_256x256ib7", "cek_sgemm_f32_256x128ie",
                   "cek_sgemm_f32_256x256w"],
-    "mandelbrot": ["cek_mandelbrot_f32", "cek_mandelbrot_pool16_f32", "cek_mandelbrot_pool8_f32",
-                   "cek_mandelbrot_pk16_f32", "cek_mandelbrot_pk32_f32", "cek_mandelbrot_blk16_f32",
-                   "cek_mandelbrot_blk64_f32", "cek_mandelbrot_blk8_f32", "cek_mandelbrot_blk8f_f32", "cek_mandelbrot_blk8g_f32", "cek_mandelbrot_blk16g_f32", "cek_mandelbrot_blk8h_f32", "cek_mandelbrot_blk8k_f32", "cek_mandelbrot_blk8m_f32", "cek_mandelbrot_blk8n_f32", "cek_mandelbrot_blk8p_f32", "cek_mandelbrot_blk8q_f32", "cek_mandelbrot_blk8s_f32", "cek_mandelbrot_blk8t_f32"],
+    "mandelbrot": ["cek_mandelbrot_f32", "cek_mandelbrot_blk8_f32", "cek_mandelbrot_blk8h_f32",
+                   "cek_mandelbrot_blk8k_f32", "cek_mandelbrot_blk8m_f32", "cek_mandelbrot_blk8t_f32"],
     "nbody": ["cek_nbody_f32_b2", "cek_nbody_integrate_f32_b2", "cek_nbody_energy_f32_b2",
               "cek_nbody_f32_b4", "cek_nbody_integrate_f32_b4", "cek_nbody_energy_f32_b4"],
     "reduce": ["cek_reduce_sum_f32", "cek_reduce_sum_f32_x32", "cek_reduce_sum_f32_final"],

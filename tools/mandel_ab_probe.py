@@ -3,7 +3,7 @@ pipeline (8 blobs), interleaved over rounds on one box (median ms), plus
 each variant's pixel mismatch against the float32 numpy reference on the
 first 1024 rows.
 
-    python tools/mandel_ab_probe.py blk8,blk8f,blk8g [rounds] [blobs,...]
+    python tools/mandel_ab_probe.py blk8,blk8h,blk8t [rounds] [blobs,...]
 """
 import json
 import os

@@ -5,7 +5,7 @@ calls run in enqueue mode (back to back, no host sync per call), as in
 bench.py's kernel-only number; ``sync_ms_median`` is the same with a host
 sync per call.
 
-    python tools/mandel_kernel_ab.py blk8,blk8g,blk8h [rounds] [reps]
+    python tools/mandel_kernel_ab.py blk8h,blk8k,blk8t [rounds] [reps]
 """
 import json
 import os

@@ -1,4 +1,4 @@
-"""Few dispatches of the VALU-bound kernels (Mandelbrot pool16, N-body b2/b4)
+"""Few dispatches of the VALU-bound kernels (Mandelbrot $MANDEL_KERNELS, N-body b2/b4)
 for counter collection under rocprofv3 --pmc."""
 import sys
 
@@ -11,7 +11,7 @@ from cekirdekler_amd.models.nbody import NBodySimulation  # noqa: E402
 
 g0 = ck.ClPlatforms.all().gpus()[0]
 import os
-for kern in os.environ.get("MANDEL_KERNELS", "pool16,blk16").split(","):
+for kern in os.environ.get("MANDEL_KERNELS", "blk8k,blk8t").split(","):
     m = MandelbrotRenderer(4096, 4096, 256, devices=g0, kernel=kern)
     m.out.write = False
     for _ in range(3):
