@@ -95,6 +95,10 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
   //    (a repeated range refreshes its time: an EWMA, so old noise fades)
   int active = 0, alone = -1;
   double tmax = 0;
+  std::vector<char> mask(n, 0);
+  for (size_t i = 0; i < n; ++i) mask[i] = ranges[i] > 0;
+  if (fs.last_active.size() == n && fs.last_active != mask) warm = false;  // a switch call
+  fs.last_active = mask;
   for (size_t i = 0; i < n; ++i) {
     if (ranges[i] <= 0 || i >= bench.size() || bench[i] <= 0) continue;
     ++active;
@@ -117,11 +121,19 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
     if (active >= 2) {
       const double ov = std::max(0.0, wall_ms - tmax);
       fs.o_multi = fs.o_multi < 0 ? ov : 0.7 * fs.o_multi + 0.3 * ov;
+    } else if (fs.recording_probe && alone == fs.probe_dev) {
+      fs.probe_walls.push_back(wall_ms);
     } else {
       double& w = fs.single_wall[alone];
       w = w < 0 ? wall_ms : 0.5 * w + 0.5 * wall_ms;
     }
   }
+  if (fs.probe_left == 0 && !fs.probe_walls.empty() && fs.probe_dev >= 0) {  // probe over
+    const auto& v = fs.probe_walls;
+    fs.single_wall[fs.probe_dev] = *std::min_element(v.begin(), v.end());
+    fs.probe_walls.clear();
+  }
+  fs.recording_probe = false;
   // 2) fits t = a + b·r (least squares over distinct ranges)
   fs.a.assign(n, 0.0);
   fs.b.assign(n, 0.0);
@@ -207,7 +219,10 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
   if (single) {
     target[best] = static_cast<double>(total);
     fs.decision = fs.probe_left > 0 ? "probe" : "single";
-    if (fs.probe_left > 0) --fs.probe_left;
+    if (fs.probe_left > 0) {
+      --fs.probe_left;
+      fs.recording_probe = true;
+    }
   } else {
     for (size_t i = 0; i < n; ++i)
       if (keep[i]) target[i] = (T - fs.a[i]) / fs.b[i];

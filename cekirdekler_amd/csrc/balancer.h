@@ -32,12 +32,20 @@ struct FitState {
   std::vector<double> single_wall;     // per device: EWMA wall ms of calls it ran alone (−1: never)
   std::vector<char> probed;
   int probe_left = 0, probe_dev = -1;
+  bool recording_probe = false;        // the call being recorded ran as a probe
+  std::vector<char> last_active;       // devices with a share in the last recorded call
+  std::vector<double> probe_walls;     // the probe calls' wall ms, in order
   std::string decision = "law";        // law | multi | single | probe
   std::vector<double> a, b;            // last fits (ms, ms per work item)
   double predicted_multi_ms = 0;
 };
 
 constexpr int kFitSamples = 8;
+// The first compute after the set of devices with a share changed is not
+// recorded: it pays the move (slices going up to their new device), a cost
+// of the switch, not of the split.  A probe runs the best single device
+// alone for kProbeCalls computes; its wall time is the minimum over the
+// recorded ones.
 constexpr int kProbeCalls = 3;
 
 // Records the last compute of this id (its ranges, per-device ms and wall ms;

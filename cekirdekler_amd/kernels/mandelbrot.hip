@@ -460,13 +460,31 @@ __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ
   return make_int2(min(ex + (int)(cnt.x + 0.5f), max_iter), min(ey + (int)(cnt.y + 0.5f), max_iter));
 }
 
-// one 8×16 block of an 8-row band per one-wave work-group
-template <int BIG, int S, bool ASM>
+// one 8×16 block of an 8-row band per one-wave work-group.  CENTER: the
+// launch's bands run from its middle band outwards (middle, middle − 1,
+// middle + 1, …), a longest-first order for views centred on the set: the
+// set-interior waves (~20× an exterior wave's work) start early and the
+// cheap exterior bands fill the end of the launch instead of a tail of
+// interior waves sharing a few SIMDs.  The order stays inside the launch's
+// own bands (device ranges and pipeline chunks are whole bands), so every
+// write stays in the launch's range.
+template <int BIG, int S, bool ASM, bool CENTER = false>
 __device__ __forceinline__ void mandel_blk8m(const float* view, const int* size, int2* out, long long off) {
   const int W = size[0], max_iter = size[2];
-  const int wv = __builtin_amdgcn_readfirstlane((int)(((long long)blockIdx.x * 64 + off) >> 6));
   const int bpb = W >> 4;  // blocks per band
-  const int band = wv / bpb, blk = wv - band * bpb;
+  int band, blk;
+  if constexpr (CENTER) {
+    const int b0 = __builtin_amdgcn_readfirstlane((int)((off >> 6) / bpb));
+    const int nbl = (int)gridDim.x / bpb;  // bands in this launch
+    const int kb = (int)blockIdx.x / bpb;
+    blk = (int)blockIdx.x - kb * bpb;
+    const int c = nbl >> 1;
+    band = b0 + ((kb & 1) ? c - ((kb + 1) >> 1) : c + (kb >> 1));
+  } else {
+    const int wv = __builtin_amdgcn_readfirstlane((int)(((long long)blockIdx.x * 64 + off) >> 6));
+    band = wv / bpb;
+    blk = wv - band * bpb;
+  }
   const int l = threadIdx.x;
   const int r = l >> 3, c2 = (l & 7) * 2;
   const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
@@ -484,4 +502,10 @@ extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8m_f32(const 
 extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8t_f32(const float* view, const int* size,
                                                                         int2* out, CEK_HIDDEN) {
   mandel_blk8m<32, 32, true>(view, size, out, __cek_off);
+}
+
+// blk8t with the launch's bands in centre-out order
+extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8u_f32(const float* view, const int* size,
+                                                                        int2* out, CEK_HIDDEN) {
+  mandel_blk8m<32, 32, true, true>(view, size, out, __cek_off);
 }

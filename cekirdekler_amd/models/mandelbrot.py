@@ -20,7 +20,7 @@ FLOP_PER_ITER = 8
 
 # kernel variants; the band kernels additionally need device and pipeline
 # chunk ranges made of whole 16-row bands (see kernels/mandelbrot.hip)
-BAND_ROWS = {"blk8": 8, "blk8h": 8, "blk8k": 8, "blk8m": 8, "blk8t": 8}  # rows per band
+BAND_ROWS = {"blk8": 8, "blk8h": 8, "blk8k": 8, "blk8m": 8, "blk8t": 8, "blk8u": 8}  # rows per band
 BAND_KERNELS = set(BAND_ROWS)
 KERNELS = {
     # name: (library kernel, pixels per work item, work-group size)
@@ -41,6 +41,9 @@ KERNELS = {
     # blk8m with 32-iteration blocks and hand-ordered instruction streams
     # (the fastest; bench.py's kernel-only number)
     "blk8t": ("cek_mandelbrot_blk8t_f32", 2, 64),
+    # blk8t with each launch's bands in centre-out order (longest first for
+    # views centred on the set)
+    "blk8u": ("cek_mandelbrot_blk8u_f32", 2, 64),
 }
 
 

@@ -12,7 +12,7 @@ from cekirdekler_amd._native import cek
 
 
 def _simulate(a, b, o_multi, o_single, G=102_400, step=256, calls=40, predictor=True, noise=0.0, seed=0,
-              cold_ms=0.0):
+              cold_ms=0.0, switch_ms=0.0):
     """Run the balancer against devices whose time is a_i + b_i·r_i (ms) and a
     compute whose wall time adds o_multi (≥ 2 devices) or o_single (1)."""
     rng = np.random.default_rng(seed)
@@ -21,10 +21,15 @@ def _simulate(a, b, o_multi, o_single, G=102_400, step=256, calls=40, predictor=
     ranges, hist = cek.initial_split(n, True, hist, G, step)
     fs = cek.FitState()
     walls, decisions = [], []
+    prev_active = None
     for call in range(calls):
         t = [(a[i] + b[i] * r) * (1 + noise * rng.standard_normal()) if r > 0 else 0.0 for i, r in enumerate(ranges)]
         if call < 2:  # the first computes of an id allocate and upload
             t = [x + cold_ms if x else 0.0 for x in t]
+        active = tuple(r > 0 for r in ranges)
+        if call and active != prev_active:  # a device set change moves slices
+            t = [x + switch_ms if x else 0.0 for x in t]
+        prev_active = active
         k = sum(1 for r in ranges if r > 0)
         wall = max(t) + (o_multi if k >= 2 else o_single)
         walls.append(wall)
@@ -118,3 +123,14 @@ def test_cores_drops_a_device_with_an_injected_fixed_cost():
     assert r_fit == [n, 0], (r_fit, info)
     assert info["decision"] in ("single", "probe")
     assert np.median(w_fit[-5:]) < np.median(w_law[-5:]) - 10.0, (w_fit[-5:], w_law[-5:])
+
+
+def test_probe_ignores_the_switch_call():
+    """The first compute after the balancer moves everything to one device
+    pays the move (the other device's slices go up to it).  The probe's wall
+    time leaves that call out, so a 1 ms switch does not make the GPU alone
+    look slower than the split (bench wave_cpu_gpu on a loaded host)."""
+    a, b = [0.05, 0.004], [5e-8, 2.1e-6]
+    ranges, walls, dec, fs = _simulate(a, b, o_multi=0.035, o_single=0.005, G=57_344, step=64, switch_ms=1.0)
+    assert ranges == [57_344, 0] and dec[-1] == "single", (ranges, dec[-6:])
+    assert fs.single_wall[0] == pytest.approx(0.05 + 5e-8 * 57_344 + 0.005, rel=1e-6)
