@@ -57,7 +57,10 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   const long long u = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
   const int S = SK ? max(dims[4], 1) : 1;
   const long long t = u / S;
-  const int ks = SK ? (int)(u % S) * (dims[2] / 64 / S) : 0;
+  // XCH 3: uneven split — the helper (u odd) takes K/64/2 − dims[5] K-tiles
+  // from the start, the owner (u even) the rest
+  const int kt_all = dims[2] / 64, shift = XCH == 3 ? dims[5] : 0;
+  const int ks = XCH == 3 ? ((u & 1) ? 0 : kt_all / 2 - shift) : SK ? (int)(u % S) * (kt_all / S) : 0;
   // Grouped tile order (dims[3] = GM row panels per group, tiles walk down
   // the group's rows first): the 32 work-groups an XCD runs at once cover a
   // GM × (32/GM) block of C, so A and B K-slices are shared through that
@@ -122,9 +125,9 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / BK / S;
+  const int nk = XCH == 3 ? ((u & 1) ? kt_all / 2 - shift : kt_all / 2 + shift) : K / BK / S;
   unsigned my_xcc = 0;
-  if constexpr (XCH == 2) {
+  if constexpr (XCH == 2 || XCH == 3) {
     // publish this work-group's XCD for the partner split (flags[4t + 2 + s])
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(my_xcc));
     my_xcc &= 15u;
@@ -393,7 +396,68 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   }
 
   // Epilogue: acc[i][j][r] is C(row = wr·16FM + i·16 + fq·4 + r, col = wc·16FN + j·16 + fr)
-  if constexpr (XCH > 0) {
+  if constexpr (XCH == 3) {
+    // Uneven split-K = 2, one-way hand-over: the helper ran `shift` K-tiles
+    // fewer than half, so it stores its whole partial tile (fragment order,
+    // 1 KiB per wave instruction) while the owner still multiplies; the owner
+    // then finds the partial ready, adds it and stores the whole C tile.  The
+    // end of the launch carries one read-back (no write) and the C stores of
+    // half the CUs; the other half's partial stores overlapped the main loop.
+    // Flags per tile: [4t] ready, [4t + 2] owner's XCD, [4t + 3] helper's XCD.
+    int* err = &tile_cnt[(size_t)4 * ntm * ntn];
+    auto spin = [&](int* w) -> int {
+      int v, spins = 0;
+      while ((v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1 << 21)) {
+          __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return 0;
+        }
+      }
+      return v;
+    };
+    f32x4* wt = reinterpret_cast<f32x4*>(W + (size_t)t * BM * BN);
+    if (u & 1) {  // helper: publish the partial and leave
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) wt[(((wr * WN + wc) * FM + i) * FN + j) * 64 + lane] = acc[i][j];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        // the owner published its XCD when it started (it is dispatched first)
+        const int px = spin(&tile_cnt[4 * t + 2]);
+        tile_cnt[4 * t + 2] = 0;  // re-arm
+        if (px != (int)my_xcc + 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(&tile_cnt[4 * t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    __syncthreads();  // every wave is done with LDS before it holds the flags
+    int* ok = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      const int hx = spin(&tile_cnt[4 * t + 3]);
+      tile_cnt[4 * t + 3] = 0;
+      int good = hx != 0;
+      if (good) good = spin(&tile_cnt[4 * t]) != 0;
+      tile_cnt[4 * t] = 0;
+      ok[0] = good;
+      ok[1] = hx == (int)my_xcc + 1;
+    }
+    __syncthreads();
+    if (!ok[1]) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (ok[0]) {
+      f32x4 part[FM][FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) part[i][j] = wt[(((wr * WN + wc) * FM + i) * FN + j) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] += part[i][j];
+    }
+  } else if constexpr (XCH > 0) {
     // Split-K = 2 with exchanged halves (WM = 2): split s finishes row half
     // s of the tile (waves wr == s) and hands its partial of the other half
     // to the partner split.  Both work-groups of a tile end at about the
@@ -557,6 +621,15 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sy(
     const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
   __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
   gemm_tile<2, 4, 8, 4, 4, true, 2>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
+}
+
+// uneven split-K = 2 with a one-way hand-over (dims[5] = the helper's
+// K-tile deficit): the helper's partial stores overlap the owner's last
+// K-tiles instead of both sides' exchange landing at the end of the launch
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sw(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
+  gemm_tile<2, 4, 8, 4, 4, true, 3>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
 }
 
 #define CEK_GEMM_B3_KERNEL(NAME, WM, WN, FM, FN, MODE)                                              \

@@ -30,6 +30,9 @@ TILES = {
     # the same with split-K = 2, the two splits exchanging row halves through
     # their XCD's L2: the 8-GPU slice (1024 rows of 8192², 128 tiles)
     "256x256pby": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sy"),
+    # uneven split-K = 2 (the helper runs `exchange_shift` K-tiles fewer and
+    # hands its whole partial to the owner while the owner still multiplies)
+    "256x256pbw": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sw"),
     # 256×128 fallbacks (twice the tiles): even chunk-split DMA, three stages / balanced DMA
     "256x128pe": (256, 128, 512, "cek_sgemm_bf16_256x128pe"),
     "256x128pb": (256, 128, 512, "cek_sgemm_bf16_256x128pb"),
@@ -47,7 +50,7 @@ GEMM_LIBS = ("sgemm_bf16",)
 # each): the kernels store a C tile in fragment order (one dwordx4 per lane
 # per fragment), which tile_to_rows / rows_to_tile convert.
 TILE_WAVES = {
-    "256x256pb": (2, 4, 8, 4), "256x256pby": (2, 4, 8, 4), "256x256": (2, 4, 8, 4), "256x256pp": (2, 4, 8, 4),
+    "256x256pb": (2, 4, 8, 4), "256x256pby": (2, 4, 8, 4), "256x256pbw": (2, 4, 8, 4), "256x256": (2, 4, 8, 4), "256x256pp": (2, 4, 8, 4),
     "256x128pe": (4, 2, 4, 4), "256x128pb": (4, 2, 4, 4), "128x128": (2, 2, 4, 4),
 }
 
@@ -92,7 +95,9 @@ F32_TILES = {
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
 SPLIT_K_TILES = {"256x256pp", "256x256pb"}
 # tiles whose kernel always runs two K-splits that exchange row halves
-EXCHANGE_TILES = {"256x256pby": 4}  # flag words per tile
+EXCHANGE_TILES = {"256x256pby": 4, "256x256pbw": 4}  # flag words per tile
+# uneven-split tiles: default K-tile deficit of the helper split (dims[5])
+EXCHANGE_SHIFT = {"256x256pbw": 4}
 
 
 def to_bf16_bits(x: np.ndarray) -> np.ndarray:
@@ -132,7 +137,8 @@ def untile(c: np.ndarray, M: int, N: int, BM: int, BN: int, group_m: int = 1, ge
 class GemmBf16:
     def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256",
                  cruncher: ClNumberCruncher | None = None, fill: str = "random", seed: int = 0,
-                 group_m: int = 4, split_k: int = 1, wave_granularity: bool | None = None):
+                 group_m: int = 4, split_k: int = 1, wave_granularity: bool | None = None,
+                 exchange_shift: int | None = None):
         BM, BN, L, kname = TILES[tile]
         if M % BM or N % BN or K % 64:
             raise ValueError(f"M%{BM}, N%{BN} and K%64 must be 0 (got {M},{N},{K})")
@@ -143,10 +149,15 @@ class GemmBf16:
                 raise ValueError(f"K/64 ({K // 64}) must be divisible by split_k ({split_k})")
             kname = kname + "_sk"
         self.exchange = tile in EXCHANGE_TILES
+        shift = 0
         if self.exchange:
             if (K // 64) % 2:
                 raise ValueError(f"K/64 ({K // 64}) must be even for tile {tile}")
             split_k = 2
+            if tile in EXCHANGE_SHIFT:
+                shift = EXCHANGE_SHIFT[tile] if exchange_shift is None else int(exchange_shift)
+                shift = max(0, min(shift, K // 128 - 1))  # the helper keeps >= 1 K-tile
+        self.exchange_shift = shift
         self.M, self.N, self.K, self.BM, self.BN, self.L, self.kernel = M, N, K, BM, BN, L, kname
         self.geom = TILE_WAVES[tile]  # C tiles in fragment order
         self.split_k = max(1, int(split_k))
@@ -154,7 +165,7 @@ class GemmBf16:
         self.global_range = self.tiles * self.split_k * L
         self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library(*GEMM_LIBS))
         self.group_m = group_m
-        self.dims = ClArray(np.array([M, N, K, group_m, self.split_k, 0, 0, 0], np.int32))
+        self.dims = ClArray(np.array([M, N, K, group_m, self.split_k, shift, 0, 0], np.int32))
         self.dims.write = False
         self.A = ClArray(M * K, "bfloat16")
         self.B = ClArray(N * K, "bfloat16")

@@ -108,7 +108,7 @@ def test_gemm_split_k(tile, split):
     cr.dispose()
 
 
-@pytest.mark.parametrize("tile", ["256x256pby"])
+@pytest.mark.parametrize("tile", ["256x256pby", "256x256pbw"])
 def test_gemm_split_k_exchanged_halves(tile):
     """Split-K = 2 with exchanged row halves: each split finishes one half
     of the tile; flags re-armed across calls (4 calls), no spin timeouts, the
@@ -256,7 +256,7 @@ def test_gemm_f32_matches_fp64(tile, shape):
     assert np.abs(c - ref).max() < 1e-4 * np.sqrt(K) * max(1.0, np.abs(ref).max())
 
 
-@pytest.mark.parametrize("tile,rows", [("256x256pb", 8192), ("256x256pby", 1024)])
+@pytest.mark.parametrize("tile,rows", [("256x256pb", 8192), ("256x256pby", 1024), ("256x256pbw", 1024)])
 def test_gemm_benchmarked_size_verify(tile, rows):
     """The headline kernels at the benchmarked size: the full 8192³ problem
     (N = 1) and the 1024-row slice one GPU of eight computes, device-resident

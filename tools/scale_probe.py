@@ -6,7 +6,9 @@ times that slice as a standalone ``rows × 8192 × 8192`` GEMM through
 tile kernels, interleaving the variants over rounds (one process, one device)
 and reporting median / min TF/s.
 
-    python tools/scale_probe.py [rows,...] [tile[:sS],...] [rounds] [steps]
+    python tools/scale_probe.py [rows,...] [tile[:sS][:wD],...] [rounds] [steps]
+
+(``:sS`` split-K S, ``:wD`` the helper's K-tile deficit of an uneven-split tile)
 """
 import json
 import os
@@ -32,9 +34,11 @@ dev = ck.ClPlatforms.all().gpus()[0]
 runs = {}
 for m in rows:
     for t in tiles:
-        name, _, sk = t.partition(":s")
+        name, *opts = t.split(":")
+        sk = next((int(o[1:]) for o in opts if o.startswith("s")), 1)
+        wd = next((int(o[1:]) for o in opts if o.startswith("w")), None)
         try:
-            g = GemmBf16(m, n, k, devices=dev, tile=name, group_m=gm, split_k=int(sk or 1))
+            g = GemmBf16(m, n, k, devices=dev, tile=name, group_m=gm, split_k=sk, exchange_shift=wd)
         except ValueError as e:
             print(f"skip {m}/{t}: {e}", flush=True)
             continue
