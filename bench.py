@@ -129,12 +129,13 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     if tile is None:
         # 256² tiles while every CU still gets one (balanced-DMA ping-pong,
         # ~1.45 PF at 8192³).  Once a GPU's slice has fewer 256² tiles than
-        # CUs (8 GPUs × 1024 rows: 128 tiles), the split-K = 2 kernel whose
-        # two K-splits exchange row halves through their XCD's L2 keeps every
-        # CU busy: 1.22 PF at 1024 rows vs 1.08 for the 256×128 tile on the
-        # same box (profiles/gemm_scaling_slices.md)
+        # CUs (8 GPUs × 1024 rows: 128 tiles), the uneven split-K = 2 kernel
+        # keeps every CU busy: its helper split runs 4 K-tiles fewer and hands
+        # its whole partial over while the owner still multiplies, 1.22 PF at
+        # 1024 rows vs 1.18 for the exchanged-halves split and 1.07 for
+        # hipBLASLt (fp32 out) on the same box (profiles/gemm_exchange_splitk.md)
         tile = "256x256pb" if (size // 256) ** 2 // ctx.world >= 256 else (
-            "256x256pby" if (size // 64) % 2 == 0 else "256x128pe")
+            "256x256pbw" if (size // 64) % 2 == 0 else "256x128pe")
     from cekirdekler_amd.ops.gemm import GEMM_LIBS
 
     cr = DistributedCruncher("", ctx=ctx, prebuilt=library(*GEMM_LIBS))

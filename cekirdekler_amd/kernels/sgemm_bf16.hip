@@ -57,10 +57,10 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   const long long u = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
   const int S = SK ? max(dims[4], 1) : 1;
   const long long t = u / S;
-  // XCH 3: uneven split — the helper (u odd) takes K/64/2 − dims[5] K-tiles
-  // from the start, the owner (u even) the rest
-  const int kt_all = dims[2] / 64, shift = XCH == 3 ? dims[5] : 0;
-  const int ks = XCH == 3 ? ((u & 1) ? 0 : kt_all / 2 - shift) : SK ? (int)(u % S) * (kt_all / S) : 0;
+  // XCH 2 / 3: the K-split of u odd (the helper) takes K/64/2 − dims[5]
+  // K-tiles from the start, u even (the owner) the rest (dims[5] = 0: halves)
+  const int kt_all = dims[2] / 64, shift = XCH >= 2 ? dims[5] : 0;
+  const int ks = XCH >= 2 ? ((u & 1) ? 0 : kt_all / 2 - shift) : SK ? (int)(u % S) * (kt_all / S) : 0;
   // Grouped tile order (dims[3] = GM row panels per group, tiles walk down
   // the group's rows first): the 32 work-groups an XCD runs at once cover a
   // GM × (32/GM) block of C, so A and B K-slices are shared through that
@@ -125,7 +125,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = XCH == 3 ? ((u & 1) ? kt_all / 2 - shift : kt_all / 2 + shift) : K / BK / S;
+  const int nk = XCH >= 2 ? ((u & 1) ? kt_all / 2 - shift : kt_all / 2 + shift) : K / BK / S;
   unsigned my_xcc = 0;
   if constexpr (XCH == 2 || XCH == 3) {
     // publish this work-group's XCD for the partner split (flags[4t + 2 + s])

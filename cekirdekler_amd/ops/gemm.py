@@ -96,8 +96,10 @@ F32_TILES = {
 SPLIT_K_TILES = {"256x256pp", "256x256pb"}
 # tiles whose kernel always runs two K-splits that exchange row halves
 EXCHANGE_TILES = {"256x256pby": 4, "256x256pbw": 4}  # flag words per tile
-# uneven-split tiles: default K-tile deficit of the helper split (dims[5])
-EXCHANGE_SHIFT = {"256x256pbw": 4}
+# K-tile deficit of the split that finishes first (dims[5]; exchange tiles):
+# pby hands its give-half over early and waits for the partner's, pbw hands
+# its whole partial over and leaves
+EXCHANGE_SHIFT = {"256x256pby": 0, "256x256pbw": 4}
 
 
 def to_bf16_bits(x: np.ndarray) -> np.ndarray:
