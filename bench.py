@@ -307,10 +307,10 @@ def _mandelbrot_kernel_only(kernel: str = "blk8u", reps: int = 20) -> dict:
     m.render(1, pipeline=False)  # image downloaded once: its counts give the FLOPs
     flops = m.flops()
     m.out.write = False
-    for _ in range(100):  # ~15 ms: the clock settles (the first runs read 10 % slower)
+    for _ in range(200):  # ~20 ms: the clock settles (the first runs read 10 % slower)
         m.render(1, pipeline=False)
     runs = []
-    for _ in range(5):  # median of 5 runs of `reps` calls (clock settling)
+    for _ in range(9):  # median of 9 runs of `reps` calls (clock settling)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         m.cr.enqueue_mode = True  # back-to-back kernels, no host sync per call

@@ -28,7 +28,7 @@ hipEvent_t CopyEngine::timing_event(int ordinal) {
       return e;
     }
   hipEvent_t e;
-  CEK_HIP(hipEventCreate(&e));
+  CEK_HIP(hipEventCreateWithFlags(&e, kTimingEventFlags));
   return e;
 }
 

@@ -748,8 +748,8 @@ void Cores::launch_kernels(Worker& wk, hipStream_t s, const ComputeCall& c, long
   while (dev < num_devices() && workers_[dev].get() != &wk) ++dev;
   PendingSpan sp{dev, c.compute_id, nullptr, nullptr, 0, 0};
   if (wk.gpu()) {
-    CEK_HIP(hipEventCreate(&sp.begin));
-    CEK_HIP(hipEventCreate(&sp.end));
+    CEK_HIP(hipEventCreateWithFlags(&sp.begin, kTimingEventFlags));
+    CEK_HIP(hipEventCreateWithFlags(&sp.end, kTimingEventFlags));
     CEK_HIP(hipEventRecord(sp.begin, s));
     launch_kernels_body(wk, s, c, ref, range);
     CEK_HIP(hipEventRecord(sp.end, s));
@@ -841,8 +841,8 @@ void Cores::span_begin(Worker& wk, hipStream_t s) {
   const int i = enqueue_mode_ ? d.used++ : 0;
   while (static_cast<int>(d.pool.size()) <= i) {
     hipEvent_t a, b;
-    CEK_HIP(hipEventCreate(&a));
-    CEK_HIP(hipEventCreate(&b));
+    CEK_HIP(hipEventCreateWithFlags(&a, kTimingEventFlags));
+    CEK_HIP(hipEventCreateWithFlags(&b, kTimingEventFlags));
     d.pool.emplace_back(a, b);
   }
   d.gap = false;
@@ -1108,8 +1108,8 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
     DevSpans* ds = wk.gpu() ? &spans_[worker_index(wk)] : nullptr;
     if (ds) {
       if (!ds->gap_a) {
-        CEK_HIP(hipEventCreate(&ds->gap_a));
-        CEK_HIP(hipEventCreate(&ds->gap_b));
+        CEK_HIP(hipEventCreateWithFlags(&ds->gap_a, kTimingEventFlags));
+        CEK_HIP(hipEventCreateWithFlags(&ds->gap_b, kTimingEventFlags));
       }
       CEK_HIP(hipEventRecord(ds->gap_a, s));
     }
