@@ -307,7 +307,7 @@ def _mandelbrot_kernel_only(kernel: str = "blk8u", reps: int = 20) -> dict:
     m.render(1, pipeline=False)  # image downloaded once: its counts give the FLOPs
     flops = m.flops()
     m.out.write = False
-    for _ in range(200):  # ~20 ms: the clock settles (the first runs read 10 % slower)
+    for _ in range(500):  # ~45 ms: the clock settles (the first runs read up to 10 % slower)
         m.render(1, pipeline=False)
     runs = []
     for _ in range(9):  # median of 9 runs of `reps` calls (clock settling)

@@ -830,8 +830,13 @@ void Cores::launch_kernels_body(Worker& wk, hipStream_t s, const ComputeCall& c,
   wk.launch_graph(s, key, body);
 }
 
+// Enqueue mode with one device in the whole job: nothing to balance, so no
+// span events between the back-to-back computes (the host clock times the
+// enqueued batch when the mode is left).
+bool Cores::spans_on() const { return device_spans && !(enqueue_mode_ && global_devices_ == 1); }
+
 void Cores::span_begin(Worker& wk, hipStream_t s) {
-  if (!wk.gpu() || !device_spans) return;
+  if (!wk.gpu() || !spans_on()) return;
   const int w = worker_index(wk);
   DevSpans& d = spans_[w];
   // enqueue mode keeps up to kMaxSpans pairs; past that the last pair's end
@@ -850,7 +855,7 @@ void Cores::span_begin(Worker& wk, hipStream_t s) {
 }
 
 void Cores::span_end(Worker& wk, hipStream_t s) {
-  if (!wk.gpu() || !device_spans) return;
+  if (!wk.gpu() || !spans_on()) return;
   DevSpans& d = spans_[worker_index(wk)];
   const int i = enqueue_mode_ ? d.used - 1 : 0;
   if (i < 0) return;

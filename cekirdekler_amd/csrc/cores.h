@@ -458,6 +458,7 @@ class Cores {
  public:
   bool device_spans = true;  // CEK_DEVICE_SPANS=0: host wall clock instead
  private:
+  bool spans_on() const;
   void span_begin(Worker& wk, hipStream_t s);
   void span_end(Worker& wk, hipStream_t s);
   double span_ms(int w);              // sync mode: the last span (stream drained)
