@@ -369,6 +369,7 @@ void Cores::set_enqueue_mode(bool on) {
   if (on && !enqueue_mode_) {
     enqueue_t0_ = now_ms();
   } else if (!on && enqueue_mode_) {
+    close_batch_spans();
     finish();
     double el = now_ms() - enqueue_t0_;
     auto it = state_.find(last_id_);
@@ -839,6 +840,25 @@ void Cores::span_begin(Worker& wk, hipStream_t s) {
   if (!wk.gpu() || !spans_on()) return;
   const int w = worker_index(wk);
   DevSpans& d = spans_[w];
+  if (enqueue_mode_ && !async_enqueue && num_devices() == 1) {
+    // one local device on one stream (a rank of a distributed job): one span
+    // for the whole enqueued batch, opened by its first compute and closed
+    // when the mode is left (close_batch_spans), so no event marker sits
+    // between two back-to-back computes; several local devices keep a span
+    // per compute (their batches overlap on shared hardware)
+    if (d.used > 0) return;
+    if (d.pool.empty()) {
+      hipEvent_t a, b;
+      CEK_HIP(hipEventCreateWithFlags(&a, kTimingEventFlags));
+      CEK_HIP(hipEventCreateWithFlags(&b, kTimingEventFlags));
+      d.pool.emplace_back(a, b);
+    }
+    d.used = 1;
+    d.batch = s;
+    d.gap = false;
+    CEK_HIP(hipEventRecord(d.pool[0].first, s));
+    return;
+  }
   // enqueue mode keeps up to kMaxSpans pairs; past that the last pair's end
   // is re-recorded, so its span stretches over the remaining computes
   constexpr int kMaxSpans = 1024;
@@ -857,6 +877,7 @@ void Cores::span_begin(Worker& wk, hipStream_t s) {
 void Cores::span_end(Worker& wk, hipStream_t s) {
   if (!wk.gpu() || !spans_on()) return;
   DevSpans& d = spans_[worker_index(wk)];
+  if (enqueue_mode_ && !async_enqueue && num_devices() == 1) return;  // closed at the mode's end
   const int i = enqueue_mode_ ? d.used - 1 : 0;
   if (i < 0) return;
   CEK_HIP(hipEventRecord(d.pool[i].second, s));
@@ -879,6 +900,16 @@ double Cores::span_ms(int w) {
       (void)hipGetLastError();
   }
   return out;
+}
+
+void Cores::close_batch_spans() {
+  for (int w = 0; w < num_devices(); ++w) {
+    DevSpans& d = spans_[w];
+    if (!d.batch || d.used <= 0) continue;
+    workers_[w]->set_device();
+    CEK_HIP(hipEventRecord(d.pool[0].second, d.batch));
+    d.batch = nullptr;
+  }
 }
 
 double Cores::enqueue_spans_ms(int w) {

@@ -453,12 +453,14 @@ class Cores {
     int used = 0;
     hipEvent_t gap_a = nullptr, gap_b = nullptr;  // phase-barrier idle gap
     bool gap = false;
+    hipStream_t batch = nullptr;  // enqueue mode: stream of the open batch span
   };
   std::vector<DevSpans> spans_;
  public:
   bool device_spans = true;  // CEK_DEVICE_SPANS=0: host wall clock instead
  private:
   bool spans_on() const;
+  void close_batch_spans();
   void span_begin(Worker& wk, hipStream_t s);
   void span_end(Worker& wk, hipStream_t s);
   double span_ms(int w);              // sync mode: the last span (stream drained)
