@@ -478,3 +478,33 @@ __global__ void oob(float* x) { x[get_global_id(0) + 1] = 7.0f; }
     with pytest.raises(Exception, match=r"oob.*wrote past the end of array #0"):
         x.compute(c, 2, "oob", 1024, 256)
     c.dispose()
+
+
+def test_enqueue_batch_span_single_device(gpu):
+    """One local device in enqueue mode: one device-time span covers the
+    whole enqueued batch (no event marker between the computes); leaving the
+    mode credits the device with that span, and the results are complete."""
+    cr1 = ck.ClNumberCruncher(gpu[0], SRC)
+    n = 1 << 20
+    x = ck.ClArray(np.zeros(n, np.float32))
+    x.compute(cr1, 21, "inc", n, 256)  # sync: uploads, first split
+    x.read = False
+    cr1.enqueue_mode = True
+    import time
+
+    t0 = time.perf_counter()
+    for _ in range(50):
+        x.compute(cr1, 21, "inc", n, 256)
+    cr1.enqueue_mode = False  # drains; closes the batch span
+    wall_ms = (time.perf_counter() - t0) * 1e3
+    b = cr1.benchmarks(21)
+    assert len(b) == 1 and 0 < b[0] <= wall_ms * 1.05, (b, wall_ms)
+    np.testing.assert_array_equal(x.array, 51.0)
+    # a second batch opens a new span
+    cr1.enqueue_mode = True
+    for _ in range(10):
+        x.compute(cr1, 21, "inc", n, 256)
+    cr1.enqueue_mode = False
+    np.testing.assert_array_equal(x.array, 61.0)
+    assert cr1.benchmarks(21)[0] > 0
+    cr1.dispose()
