@@ -10,6 +10,7 @@ splitting the vertices.  Steady state after the balancer has converged.
 (``overhead_aware_balancer``: t = a + b·range per device), which may leave
 the CPU out when its share does not pay for the second device's fixed cost."""
 import argparse
+import statistics
 import time
 
 import numpy as np
@@ -21,6 +22,7 @@ from cekirdekler_amd.models.wave import WaveSurface, grid_mesh
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--frames", type=int, default=200)
+ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--nx", type=int, default=224)
 ap.add_argument("--ny", type=int, default=256)
 a = ap.parse_args()
@@ -30,24 +32,35 @@ base, normals = grid_mesh(a.nx, a.ny)
 configs = [("cpu", cpu)]
 if len(gpus):
     configs += [("gpu", gpus[0]), ("gpu+cpu", gpus[0] + cpu), ("gpu+cpu_fit", gpus[0] + cpu)]
-out = {"config": "wave_cpu_gpu", "vertices": len(base), "local": 64}
+out = {"config": "wave_cpu_gpu", "vertices": len(base), "local": 64,
+       "timing": f"median of {a.rounds} interleaved rounds of {a.frames // a.rounds} frames per config"}
+surfaces = {}
 for name, devs in configs:
     w = WaveSurface(base, normals, devices=devs)
     if name.endswith("_fit"):
         w.cr.overhead_aware_balancer = True
     for _ in range(40):  # balancer converges, buffers resident
         w.update()
-    t = time.perf_counter()
-    for _ in range(a.frames):
-        w.update()
-    ms = (time.perf_counter() - t) * 1e3 / a.frames
-    err = float(np.abs(w.update()["z"] - w.reference()["z"]).max())
-    out[f"{name}_ms_per_frame"] = ms
-    out[f"{name}_max_abs_err"] = err
+    surfaces[name] = w
+# the configs take turns (a round of frames each), so clock and host-load
+# drift over the run hits every config alike
+per = max(1, a.frames // a.rounds)
+runs = {name: [] for name in surfaces}
+for _ in range(a.rounds):
+    for name, w in surfaces.items():
+        t = time.perf_counter()
+        for _ in range(per):
+            w.update()
+        runs[name].append((time.perf_counter() - t) * 1e3 / per)
+for name, w in surfaces.items():
+    out[f"{name}_ms_per_frame"] = statistics.median(runs[name])
+    out[f"{name}_ms_rounds"] = [round(x, 4) for x in runs[name]]
+    out[f"{name}_max_abs_err"] = float(np.abs(w.update()["z"] - w.reference()["z"]).max())
     if name.startswith("gpu+cpu"):
         out[f"{name}_shares"] = [r / sum(w.cr.ranges(1)) for r in w.cr.ranges(1)]
     if name.endswith("_fit"):
         out[f"{name}_predictor"] = {k: v for k, v in w.cr.balancer_predictor_info(1).items()}
+for w in surfaces.values():
     w.cr.dispose()
 if "gpu+cpu_ms_per_frame" in out:
     out["speedup_gpu+cpu_over_cpu"] = out["cpu_ms_per_frame"] / out["gpu+cpu_ms_per_frame"]

@@ -24,6 +24,12 @@
 // fragment read conflict-free (each 16-lane group hits 16 distinct slots).
 #include "cek_kernel.h"
 
+// K-tile index of a stage load; tools/microbench/gemm_loop.hip redefines it
+// to re-read two K-tiles (an L2-resident operand stream) as a probe.
+#ifndef CEK_KTILE
+#define CEK_KTILE(ks, kt) ((ks) + (kt))
+#endif
+
 namespace {
 
 template <int WM, int WN, int FM, int FN, int MODE, bool SK = false, int XCH = 0>
@@ -89,7 +95,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     char* base = smem + buf * STAGE;
 #pragma unroll
     for (int j = 0; j < A_INSTR; ++j) {
-      const char* src = a_wave + ((size_t)j * 8 * K + (size_t)(ks + kt) * BK) * 2;
+      const char* src = a_wave + ((size_t)j * 8 * K + (size_t)CEK_KTILE(ks, kt) * BK) * 2;
       __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
                                        (lds_void*)(base + (sw * A_INSTR + j) * 1024), 16, 0, 0);
     }
@@ -98,7 +104,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     char* base = smem + buf * STAGE + A_BYTES;
 #pragma unroll
     for (int j = 0; j < B_INSTR; ++j) {
-      const char* src = b_wave + ((size_t)j * 8 * K + (size_t)(ks + kt) * BK) * 2;
+      const char* src = b_wave + ((size_t)j * 8 * K + (size_t)CEK_KTILE(ks, kt) * BK) * 2;
       __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off),
                                        (lds_void*)(base + (sw * B_INSTR + j) * 1024), 16, 0, 0);
     }
@@ -315,7 +321,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       char* base = a_base + (kt & 1) * A_BYTES;
 #pragma unroll
       for (int j = 0; j < A_INSTR; ++j) {
-        const char* src = a_wave + ((size_t)j * 8 * K + (size_t)(ks + kt) * BK) * 2;
+        const char* src = a_wave + ((size_t)j * 8 * K + (size_t)CEK_KTILE(ks, kt) * BK) * 2;
         __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off), (lds_void*)(base + (sw * A_INSTR + j) * 1024),
                                          16, 0, 0);
       }
@@ -324,7 +330,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       char* base = b_base + (kt % 3) * B_BYTES;
 #pragma unroll
       for (int j = 0; j < B_INSTR; ++j) {
-        const char* src = b_wave + ((size_t)j * 8 * K + (size_t)(ks + kt) * BK) * 2;
+        const char* src = b_wave + ((size_t)j * 8 * K + (size_t)CEK_KTILE(ks, kt) * BK) * 2;
         __builtin_amdgcn_global_load_lds((glb_cvoid*)(src + lane_off), (lds_void*)(base + (sw * B_INSTR + j) * 1024),
                                          16, 0, 0);
       }

@@ -1,0 +1,102 @@
+// Main-loop probe of the production bf16 GEMM kernels, outside the runtime:
+// times cek_sgemm_bf16_256x256pb (8192³) and the 8-GPU slice kernel
+// cek_sgemm_bf16_256x256pb_sw (1024 × 8192 × 8192) with hipEvents.
+// Built twice by tools/microbench/build_gemm_loop.sh:
+//   gemm_loop      the kernels as shipped
+//   gemm_loop_l2   -DCEK_KTILE: every stage load re-reads K-tiles 0/1 of its
+//                  tile (the operand stream hits L2), same instruction stream
+// The difference between the two is what operand latency/bandwidth costs the
+// ping-pong schedule.
+#ifdef CEK_PROBE_L2
+#define CEK_KTILE(ks, kt) ((ks) + ((kt) & 1))
+#endif
+#include "../../cekirdekler_amd/kernels/sgemm_bf16.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                       \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) {                                                         \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                      \
+    }                                                                               \
+  } while (0)
+
+static float time_kernel(void (*launch)(hipStream_t), int reps) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int i = 0; i < 3; ++i) launch(0);
+  CK(hipEventRecord(a, 0));
+  for (int i = 0; i < reps; ++i) launch(0);
+  CK(hipEventRecord(b, 0));
+  CK(hipEventSynchronize(b));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, a, b));
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+  return ms / reps;
+}
+
+static int *g_dims, *g_dims_slice, *g_cnt;
+static uint16_t *g_A, *g_B;
+static float *g_C, *g_W;
+static const int N = 8192, SLICE = 1024;
+
+static void launch_full(hipStream_t s) {
+  hipLaunchKernelGGL(cek_sgemm_bf16_256x256pb, dim3((N / 256) * (N / 256)), dim3(512), 0, s, g_dims, g_A, g_B, g_C,
+                     0LL, (long long)(N / 256) * (N / 256) * 512);
+}
+
+static void launch_slice(hipStream_t s) {
+  const int tiles = (SLICE / 256) * (N / 256);
+  hipLaunchKernelGGL(cek_sgemm_bf16_256x256pb_sw, dim3(2 * tiles), dim3(512), 0, s, g_dims_slice, g_A, g_B, g_C, g_W,
+                     g_cnt, 0LL, (long long)2 * tiles * 512);
+}
+
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? atoi(argv[1]) : 20;
+  const size_t nab = (size_t)N * N;
+  CK(hipMalloc(&g_A, nab * 2));
+  CK(hipMalloc(&g_B, nab * 2));
+  CK(hipMalloc(&g_C, nab * 4));
+  CK(hipMalloc(&g_W, (size_t)SLICE * N * 4));
+  const int tiles_slice = (SLICE / 256) * (N / 256);
+  CK(hipMalloc(&g_cnt, (4 * tiles_slice + 1) * sizeof(int)));
+  CK(hipMemset(g_cnt, 0, (4 * tiles_slice + 1) * sizeof(int)));
+  // uniform bf16 values in [-1, 1): 0x3f80 bias + random mantissa, random sign
+  std::vector<uint16_t> h(nab);
+  unsigned x = 12345u;
+  for (size_t i = 0; i < nab; ++i) {
+    x = x * 1664525u + 1013904223u;
+    h[i] = (uint16_t)(0x3e00u + ((x >> 9) & 0x1ffu)) | (uint16_t)((x >> 31) << 15);
+  }
+  CK(hipMemcpy(g_A, h.data(), nab * 2, hipMemcpyHostToDevice));
+  CK(hipMemcpy(g_B, h.data(), nab * 2, hipMemcpyHostToDevice));
+  int dims[8] = {N, N, N, 4, 1, 0, 0, 0};
+  int dims_s[8] = {SLICE, N, N, 4, 2, 4, 0, 0};
+  CK(hipMalloc(&g_dims, sizeof dims));
+  CK(hipMalloc(&g_dims_slice, sizeof dims_s));
+  CK(hipMemcpy(g_dims, dims, sizeof dims, hipMemcpyHostToDevice));
+  CK(hipMemcpy(g_dims_slice, dims_s, sizeof dims_s, hipMemcpyHostToDevice));
+#ifdef CEK_PROBE_L2
+  const char* variant = "l2_operands";
+#else
+  const char* variant = "shipped";
+#endif
+  for (int round = 0; round < 2; ++round) {
+    float ms = time_kernel(launch_full, reps);
+    printf("{\"variant\": \"%s\", \"kernel\": \"256x256pb\", \"shape\": \"8192^3\", \"ms\": %.4f, \"tflops\": %.1f}\n",
+           variant, ms, 2.0 * N * N * (double)N / ms / 1e9);
+    ms = time_kernel(launch_slice, reps);
+    printf("{\"variant\": \"%s\", \"kernel\": \"256x256pbw\", \"shape\": \"1024x8192x8192\", \"ms\": %.4f, \"tflops\": %.1f}\n",
+           variant, ms, 2.0 * SLICE * N * (double)N / ms / 1e9);
+  }
+  int err = 0;
+  CK(hipMemcpy(&err, g_cnt + 4 * tiles_slice, sizeof(int), hipMemcpyDeviceToHost));
+  printf("{\"spin_timeouts\": %d}\n", err);
+  return 0;
+}
