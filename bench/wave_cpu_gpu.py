@@ -39,7 +39,7 @@ for name, devs in configs:
     w = WaveSurface(base, normals, devices=devs)
     if name.endswith("_fit"):
         w.cr.overhead_aware_balancer = True
-    for _ in range(40):  # balancer converges, buffers resident
+    for _ in range(100):  # balancer (and the predictor's probe) converge, buffers resident
         w.update()
     surfaces[name] = w
 # the configs take turns (a round of frames each), so clock and host-load
