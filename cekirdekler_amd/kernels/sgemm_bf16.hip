@@ -29,6 +29,11 @@
 #ifndef CEK_KTILE
 #define CEK_KTILE(ks, kt) ((ks) + (kt))
 #endif
+// Per-work-group timeline stamps (tools/microbench/gemm_loop.hip defines it
+// in its timeline build; empty in the library).
+#ifndef CEK_TS
+#define CEK_TS(k)
+#endif
 
 namespace {
 
@@ -55,6 +60,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 
   const int M = dims[0], N = dims[1], K = dims[2], GM = dims[3] > 0 ? dims[3] : 1;
   const int tid = threadIdx.x, lane = tid & 63;
+  CEK_TS(0);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = (wave % NREG) / WN, wc = (wave % NREG) % WN;
   // Split-K (SK): work-group u computes K-tiles [ks, ks + nk) of tile u / S;
@@ -371,6 +377,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
+    CEK_TS(1);
     if (g1) bar();  // G1 runs one section behind
     for (int kt = 0; kt < nk; ++kt) {
       const bool b_issued = g1 && kt + 2 < nk;
@@ -399,6 +406,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       bar();
     }
     if (!g1) bar();  // equal barrier counts for both groups
+    CEK_TS(2);
   }
 
   // Epilogue: acc[i][j][r] is C(row = wr·16FM + i·16 + fq·4 + r, col = wc·16FN + j·16 + fr)
@@ -430,6 +438,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
         for (int j = 0; j < FN; ++j) wt[(((wr * WN + wc) * FM + i) * FN + j) * 64 + lane] = acc[i][j];
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      CEK_TS(3);
       if (tid == 0) {
         // the owner published its XCD when it started (it is dispatched first)
         const int px = spin(&tile_cnt[4 * t + 2]);
@@ -437,6 +446,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
         if (px != (int)my_xcc + 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_store(&tile_cnt[4 * t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      CEK_TS(4);
       return;
     }
     __syncthreads();  // every wave is done with LDS before it holds the flags
@@ -451,6 +461,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       ok[1] = hx == (int)my_xcc + 1;
     }
     __syncthreads();
+    CEK_TS(3);
     if (!ok[1]) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (ok[0]) {
       f32x4 part[FM][FN];
@@ -463,6 +474,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] += part[i][j];
     }
+    CEK_TS(4);
   } else if constexpr (XCH > 0) {
     // Split-K = 2 with exchanged halves (WM = 2): split s finishes row half
     // s of the tile (waves wr == s) and hands its partial of the other half
@@ -590,6 +602,9 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) ct[(((wr * WN + wc) * FM + i) * FN + j) * 64 + lane] = acc[i][j];
+#ifdef CEK_TS_END
+  CEK_TS_END;
+#endif
 }
 
 }  // namespace

@@ -10,8 +10,33 @@
 #ifdef CEK_PROBE_L2
 #define CEK_KTILE(ks, kt) ((ks) + ((kt) & 1))
 #endif
+#ifdef CEK_PROBE_TS
+// timeline build: work-group thread 0 stamps the 100 MHz realtime counter at
+// entry (0), prologue done (1), main loop done (2), hand-over steps (3, 4) and
+// after its C stores have completed (5); slot 6 holds the XCD id
+#include <hip/hip_runtime.h>
+__device__ unsigned long long cek_ts[4096 * 8];
+__device__ __forceinline__ void cek_stamp(int k) {
+  if (threadIdx.x == 0) {
+    cek_ts[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
+    if (k == 0) {
+      unsigned x;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+      cek_ts[blockIdx.x * 8 + 6] = x & 15u;
+    }
+  }
+}
+#define CEK_TS(k) cek_stamp(k)
+#define CEK_TS_END                                \
+  do {                                            \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+    __syncthreads();                              \
+    cek_stamp(5);                                 \
+  } while (0)
+#endif
 #include "../../cekirdekler_amd/kernels/sgemm_bf16.hip"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -57,6 +82,64 @@ static void launch_slice(hipStream_t s) {
                      g_cnt, 0LL, (long long)2 * tiles * 512);
 }
 
+#ifdef CEK_PROBE_TS
+// host copy of cek_xcd_remap (kernels/cek_kernel.h)
+static unsigned host_xcd_remap(unsigned b, unsigned nwg) {
+  const unsigned xcd = b & 7u, q = nwg >> 3, r = nwg & 7u;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+static double pct(std::vector<double> v, double q) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  return v[(size_t)(q * (v.size() - 1))];
+}
+
+// one launch, then per-stamp distributions (µs after the earliest entry) for
+// the owner (even u) and helper (odd u) work-groups
+static void timeline(const char* name, void (*launch)(hipStream_t), int grid) {
+  std::vector<unsigned long long> ts((size_t)grid * 8, 0);
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(cek_ts), ts.data(), ts.size() * 8));
+  launch(0);
+  CK(hipDeviceSynchronize());
+  CK(hipMemcpyFromSymbol(ts.data(), HIP_SYMBOL(cek_ts), ts.size() * 8));
+  unsigned long long t0 = ~0ull, tend = 0;
+  for (int b = 0; b < grid; ++b) {
+    t0 = std::min(t0, ts[b * 8]);
+    for (int k = 1; k < 6; ++k) tend = std::max(tend, ts[b * 8 + k]);
+  }
+  printf("{\"timeline\": \"%s\", \"span_us\": %.2f", name, (tend - t0) / 100.0);
+  for (int role = 0; role < 2; ++role) {
+    for (int k = 0; k < 6; ++k) {
+      std::vector<double> v;
+      for (int b = 0; b < grid; ++b) {
+        const unsigned u = host_xcd_remap((unsigned)b, (unsigned)grid);
+        if ((int)(u & 1) != role || !ts[b * 8 + k]) continue;
+        v.push_back((ts[b * 8 + k] - t0) / 100.0);
+      }
+      if (v.empty()) continue;
+      printf(", \"%s_t%d\": [%.2f, %.2f, %.2f, %.2f]", role ? "odd" : "even", k, pct(v, 0), pct(v, 0.5), pct(v, 0.9),
+             pct(v, 1.0));
+    }
+  }
+  printf("}\n");
+  // per XCD: work-groups run, median main-loop time (t2 - t1) and median end (t5 or t4)
+  printf("{\"timeline_by_xcd\": \"%s\"", name);
+  for (int x = 0; x < 8; ++x) {
+    std::vector<double> loop, end;
+    for (int b = 0; b < grid; ++b) {
+      if ((int)ts[b * 8 + 6] != x || !ts[b * 8 + 2]) continue;
+      loop.push_back((ts[b * 8 + 2] - ts[b * 8 + 1]) / 100.0);
+      const unsigned long long e = ts[b * 8 + 5] ? ts[b * 8 + 5] : ts[b * 8 + 4];
+      end.push_back((e - t0) / 100.0);
+    }
+    printf(", \"xcd%d\": {\"wgs\": %zu, \"loop_us\": [%.2f, %.2f, %.2f], \"end_us\": [%.2f, %.2f]}", x, loop.size(),
+           pct(loop, 0), pct(loop, 0.5), pct(loop, 1.0), pct(end, 0.5), pct(end, 1.0));
+  }
+  printf("}\n");
+}
+#endif
+
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 20;
   const size_t nab = (size_t)N * N;
@@ -95,6 +178,10 @@ int main(int argc, char** argv) {
     printf("{\"variant\": \"%s\", \"kernel\": \"256x256pbw\", \"shape\": \"1024x8192x8192\", \"ms\": %.4f, \"tflops\": %.1f}\n",
            variant, ms, 2.0 * SLICE * N * (double)N / ms / 1e9);
   }
+#ifdef CEK_PROBE_TS
+  timeline("256x256pb 8192^3", launch_full, (N / 256) * (N / 256));
+  timeline("256x256pbw 1024x8192x8192", launch_slice, 2 * tiles_slice);
+#endif
   int err = 0;
   CK(hipMemcpy(&err, g_cnt + 4 * tiles_slice, sizeof(int), hipMemcpyDeviceToHost));
   printf("{\"spin_timeouts\": %d}\n", err);
