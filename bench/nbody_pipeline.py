@@ -39,9 +39,13 @@ import cekirdekler_amd as ck
 from cekirdekler_amd.parallel.pipeline import ClPipelineStage
 
 FORCE = r"""
-// 4 bodies per work item as two packed f32x2 pairs (v_pk_* issue: see
-// kernels/nbody.hip) -- the same structure as the library force kernel,
-// written as a user kernel string and JIT-compiled by hiprtc.
+// 2 bodies per work item as one packed f32x2 pair (v_pk_* issue: see
+// kernels/nbody.hip), written as a user kernel string and JIT-compiled by
+// hiprtc.  Work-group g owns bodies [512 g, 512 g + 512), so a device's range
+// of whole work-groups owns one contiguous body range.  Two bodies per item
+// (not four) keep 4+ work-groups per CU when the force stage is split over
+// 2-6 GPUs: 52 % / 50 % of FP32 peak at 1/2 and 1/4 of the bodies per GPU
+// against 51 % / 45 % with four (tools/nbody_force_probe.py).
 typedef float f2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void force(const float4* pos, const float4* vel, const float* prm,
                                              float4* pos_o, float4* vel_o, float4* acc_o) {
@@ -49,40 +53,31 @@ __global__ __launch_bounds__(256) void force(const float4* pos, const float4* ve
   const int n = (int)prm[2];
   const f2 e2 = {prm[0], prm[0]};
   const long long w = get_global_id(0);
-  const long long i0 = (w / 256) * 1024 + (w % 256);
-  f2 px[2], py[2], pz[2], ax[2], ay[2], az[2];
-  for (int p = 0; p < 2; ++p) {
-    float4 b0 = pos[i0 + 512 * p], b1 = pos[i0 + 512 * p + 256];
-    px[p] = (f2){b0.x, b1.x}; py[p] = (f2){b0.y, b1.y}; pz[p] = (f2){b0.z, b1.z};
-    ax[p] = ay[p] = az[p] = (f2){0.f, 0.f};
-  }
+  const long long i0 = (w / 256) * 512 + (w % 256);
+  const float4 b0 = pos[i0], b1 = pos[i0 + 256];
+  const f2 px = {b0.x, b1.x}, py = {b0.y, b1.y}, pz = {b0.z, b1.z};
+  f2 ax = {0.f, 0.f}, ay = ax, az = ax;
   for (int j0 = 0; j0 < n; j0 += 256) {
     __syncthreads();
     tile[threadIdx.x] = pos[j0 + threadIdx.x];
     __syncthreads();
-#pragma unroll 4
+#pragma unroll 8
     for (int j = 0; j < 256; ++j) {
       const float4 q = tile[j];
       const f2 qx = {q.x, q.x}, qy = {q.y, q.y}, qz = {q.z, q.z}, qm = {q.w, q.w};
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const f2 dx = qx - px[p], dy = qy - py[p], dz = qz - pz[p];
-        const f2 r2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, __builtin_elementwise_fma(dz, dz, e2)));
-        const f2 inv = {__builtin_amdgcn_rsqf(r2.x), __builtin_amdgcn_rsqf(r2.y)};
-        const f2 sc = (qm * inv) * (inv * inv);
-        ax[p] = __builtin_elementwise_fma(dx, sc, ax[p]);
-        ay[p] = __builtin_elementwise_fma(dy, sc, ay[p]);
-        az[p] = __builtin_elementwise_fma(dz, sc, az[p]);
-      }
+      const f2 dx = qx - px, dy = qy - py, dz = qz - pz;
+      const f2 r2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, __builtin_elementwise_fma(dz, dz, e2)));
+      const f2 inv = {__builtin_amdgcn_rsqf(r2.x), __builtin_amdgcn_rsqf(r2.y)};
+      const f2 sc = (qm * inv) * (inv * inv);
+      ax = __builtin_elementwise_fma(dx, sc, ax);
+      ay = __builtin_elementwise_fma(dy, sc, ay);
+      az = __builtin_elementwise_fma(dz, sc, az);
     }
   }
-  for (int p = 0; p < 2; ++p) {
-    const long long a = i0 + 512 * p, b = a + 256;
-    acc_o[a] = make_float4(ax[p].x, ay[p].x, az[p].x, 0.f);
-    acc_o[b] = make_float4(ax[p].y, ay[p].y, az[p].y, 0.f);
-    pos_o[a] = pos[a]; pos_o[b] = pos[b];
-    vel_o[a] = vel[a]; vel_o[b] = vel[b];
-  }
+  acc_o[i0] = make_float4(ax.x, ay.x, az.x, 0.f);
+  acc_o[i0 + 256] = make_float4(ax.y, ay.y, az.y, 0.f);
+  pos_o[i0] = b0; pos_o[i0 + 256] = b1;
+  vel_o[i0] = vel[i0]; vel_o[i0 + 256] = vel[i0 + 256];
 }
 """
 KICK = r"""
@@ -152,17 +147,17 @@ else:
 f4 = lambda: np.zeros(4 * n, np.float32)  # noqa: E731
 prm = np.array([1e-4, 1.0, float(n), 1e-3], np.float32)
 s1, s2, s3 = ClPipelineStage(), ClPipelineStage(), ClPipelineStage()
-s1.add_devices(devs[0]); s1.add_kernels(FORCE, "force", [n // 4], [256])
+s1.add_devices(devs[0]); s1.add_kernels(FORCE, "force", [n // 2], [256])
 s1.add_input_buffers(f4(), f4()); s1.add_hidden_buffers(prm.copy()); s1.add_output_buffers(f4(), f4(), f4())
 s2.add_devices(devs[1]); s2.add_kernels(KICK, "kick", [n], [256])
 s2.add_input_buffers(f4(), f4(), f4()); s2.add_hidden_buffers(prm.copy()); s2.add_output_buffers(f4(), f4())
 s3.add_devices(devs[2]); s3.add_kernels(ENERGY, "energy", [n], [256])
 s3.add_input_buffers(f4(), f4()); s3.add_output_buffers(f4(), f4(), np.zeros(n // 256, np.float32))
-# slice ownership in multi-device stages: a force work item owns 4 bodies
-# (16 floats) of each output, a kick / energy work item one body (4 floats),
+# slice ownership in multi-device stages: a force work item owns 2 bodies
+# (8 floats) of each output, a kick / energy work item one body (4 floats),
 # an energy work-group one partial sum
 for arr in s1.outputs:
-    arr.elements_per_work_item = 16
+    arr.elements_per_work_item = 8
 for arr in s2.outputs + s3.outputs[:2]:
     arr.elements_per_work_item = 4
 s3.outputs[2].elements_per_group = 1
