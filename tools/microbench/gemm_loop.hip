@@ -16,9 +16,11 @@
 // after its C stores have completed (5); slot 6 holds the XCD id
 #include <hip/hip_runtime.h>
 __device__ unsigned long long cek_ts[4096 * 8];
+__device__ unsigned long long cek_clk[4096 * 8];  // s_memtime (shader clock) at the same points
 __device__ __forceinline__ void cek_stamp(int k) {
   if (threadIdx.x == 0) {
     cek_ts[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
+    cek_clk[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memtime();
     if (k == 0) {
       unsigned x;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
@@ -103,6 +105,8 @@ static void timeline(const char* name, void (*launch)(hipStream_t), int grid) {
   launch(0);
   CK(hipDeviceSynchronize());
   CK(hipMemcpyFromSymbol(ts.data(), HIP_SYMBOL(cek_ts), ts.size() * 8));
+  std::vector<unsigned long long> clk((size_t)grid * 8, 0);
+  CK(hipMemcpyFromSymbol(clk.data(), HIP_SYMBOL(cek_clk), clk.size() * 8));
   unsigned long long t0 = ~0ull, tend = 0;
   for (int b = 0; b < grid; ++b) {
     t0 = std::min(t0, ts[b * 8]);
@@ -126,15 +130,18 @@ static void timeline(const char* name, void (*launch)(hipStream_t), int grid) {
   // per XCD: work-groups run, median main-loop time (t2 - t1) and median end (t5 or t4)
   printf("{\"timeline_by_xcd\": \"%s\"", name);
   for (int x = 0; x < 8; ++x) {
-    std::vector<double> loop, end;
+    std::vector<double> loop, end, ghz;
     for (int b = 0; b < grid; ++b) {
       if ((int)ts[b * 8 + 6] != x || !ts[b * 8 + 2]) continue;
       loop.push_back((ts[b * 8 + 2] - ts[b * 8 + 1]) / 100.0);
+      // s_memtime ticks per µs over the main loop (the realtime counter is 100 MHz)
+      ghz.push_back((double)(clk[b * 8 + 2] - clk[b * 8 + 1]) / ((ts[b * 8 + 2] - ts[b * 8 + 1]) * 10.0));
       const unsigned long long e = ts[b * 8 + 5] ? ts[b * 8 + 5] : ts[b * 8 + 4];
       end.push_back((e - t0) / 100.0);
     }
-    printf(", \"xcd%d\": {\"wgs\": %zu, \"loop_us\": [%.2f, %.2f, %.2f], \"end_us\": [%.2f, %.2f]}", x, loop.size(),
-           pct(loop, 0), pct(loop, 0.5), pct(loop, 1.0), pct(end, 0.5), pct(end, 1.0));
+    printf(", \"xcd%d\": {\"wgs\": %zu, \"loop_us\": [%.2f, %.2f, %.2f], \"end_us\": [%.2f, %.2f], \"memtime_ghz\": [%.3f, %.3f, %.3f]}",
+           x, loop.size(), pct(loop, 0), pct(loop, 0.5), pct(loop, 1.0), pct(end, 0.5), pct(end, 1.0), pct(ghz, 0),
+           pct(ghz, 0.5), pct(ghz, 1.0));
   }
   printf("}\n");
 }
