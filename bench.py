@@ -296,34 +296,73 @@ def _mandelbrot_kernel_only(kernel: str = "blk8u", reps: int = 20) -> dict:
     device memory, no D2H, calls enqueued back to back in enqueue mode):
     BASELINE's "kernel >= 50 % of FP32 peak" target.
     The end-to-end number above is PCIe-bound and runs blk8 (the kernel does
-    not change it, tools/mandel_ab_probe.py)."""
+    not change it, tools/mandel_ab_probe.py).
+
+    Two numbers: ``ms`` renders one image over and over on one stream (each
+    launch drains before the next starts); ``frames_in_flight_2`` renders
+    two images alternately in the reference's async enqueue mode
+    (enqueueModeAsyncEnable over 2 queues), so frame k+1's first waves fill
+    the SIMDs that frame k's last waves leave idle (double-buffered frames of
+    an animation; every frame is computed whole, tools/mandel_async_probe.py)."""
     import torch
 
     from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
+    from cekirdekler_amd.ops.library import library
     import cekirdekler_amd as ck
 
     gpus = ck.ClPlatforms.all().gpus()
-    m = MandelbrotRenderer(4096, 4096, max_iter=256, devices=gpus[0], kernel=kernel)
-    m.render(1, pipeline=False)  # image downloaded once: its counts give the FLOPs
-    flops = m.flops()
-    m.out.write = False
-    for _ in range(500):  # ~45 ms: the clock settles (the first runs read up to 10 % slower)
-        m.render(1, pipeline=False)
-    runs = []
-    for _ in range(9):  # median of 9 runs of `reps` calls (clock settling)
+    cr = ck.ClNumberCruncher(gpus[0], "", prebuilt=library("mandelbrot"), queue_concurrency=2)
+    ms = [MandelbrotRenderer(4096, 4096, max_iter=256, cruncher=cr, kernel=kernel) for _ in range(2)]
+    for i, m in enumerate(ms):
+        m.render(i + 1, pipeline=False)  # image downloaded once: its counts give the FLOPs
+    flops = ms[0].flops()
+    for m in ms:
+        m.out.write = False
+
+    def batch(frames_in_flight: int) -> float:
+        """One timed run of `reps` calls enqueued back to back (no host sync
+        per call), ms per call."""
+        cr.enqueue_mode_async_enable = frames_in_flight > 1
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        m.cr.enqueue_mode = True  # back-to-back kernels, no host sync per call
-        for _ in range(reps):
-            m.render(1, pipeline=False)
-        m.cr.enqueue_mode = False
+        cr.enqueue_mode = True
+        for k in range(reps):
+            ms[k % frames_in_flight].render(k % frames_in_flight + 1, pipeline=False)
+        cr.enqueue_mode = False
         torch.cuda.synchronize()
-        runs.append((time.perf_counter() - t0) * 1e3 / reps)
-    ms = sorted(runs)[len(runs) // 2]
-    m.cr.dispose()
-    tf = flops / (ms * 1e-3) / 1e12
-    return {"kernel": m.kernel, "ms": round(ms, 4), "ms_runs": [round(x, 4) for x in runs], "tflops": round(tf, 2),
-            "pct_fp32_peak_157_3": round(100 * tf / 157.3, 1)}
+        cr.enqueue_mode_async_enable = False
+        return (time.perf_counter() - t0) * 1e3 / reps
+
+    for k in range(500):  # ~45 ms: the clock settles (the first runs read up to 10 % slower)
+        ms[0].render(1, pipeline=False)
+    batch(2)
+    # 9 rounds, the two modes taking turns (clock drift hits both alike);
+    # each mode's median
+    runs = {1: [], 2: []}
+    for _ in range(9):
+        for f in (1, 2):
+            runs[f].append(batch(f))
+
+    def summary(runs):
+        ms_ = sorted(runs)[len(runs) // 2]
+        tf = flops / (ms_ * 1e-3) / 1e12
+        return {"ms": round(ms_, 4), "ms_runs": [round(x, 4) for x in runs], "tflops": round(tf, 2),
+                "pct_fp32_peak_157_3": round(100 * tf / 157.3, 1)}
+
+    out = {"kernel": ms[0].kernel, **summary(runs[1])}
+    two = summary(runs[2])
+    # both device images (last written by the overlapped frames) are whole
+    # and equal to the image downloaded before the timed runs
+    ref = ms[0].out.array.copy()
+    equal = True
+    for m in ms:
+        m.out.array[:] = -1
+        cr.download(m.out, 0)
+        equal = equal and bool((m.out.array == ref).all())
+    two["images_equal"] = equal
+    out["frames_in_flight_2"] = two
+    cr.dispose()
+    return out
 
 
 def bench_lb_iters():
