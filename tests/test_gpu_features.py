@@ -33,18 +33,22 @@ def cr(gpu):
     c.dispose()
 
 
-def test_wave_gpu_and_gpu_plus_cpu(gpu):
+@pytest.mark.parametrize("zero_copy", [True, False])
+def test_wave_gpu_and_gpu_plus_cpu(gpu, zero_copy):
+    """Every frame's vertices (GPU alone, GPU + CPU device) against numpy,
+    with the vertices written zero-copy into the host array (default) and
+    copied back by D2H."""
     from cekirdekler_amd.models.wave import WaveSurface, grid_mesh
 
     base, nrm = grid_mesh(224, 256)                 # the Kamera.cs mesh: 57,344 vertices
     for devs in (gpu[0], gpu[0] + ck.ClPlatforms.all().cpus(True)):
-        w = WaveSurface(base, nrm, devices=devs)
+        w = WaveSurface(base, nrm, devices=devs, zero_copy_output=zero_copy)
         for _ in range(8):
             v = w.update()
-        ref = w.reference()
-        for c in "xyz":
-            # device sin/sqrt are not correctly rounded: 2 ulp-scale slack
-            np.testing.assert_allclose(v[c], ref[c], atol=2e-6)
+            ref = w.reference()
+            for c in "xyz":
+                # device sin/sqrt are not correctly rounded: 2 ulp-scale slack
+                np.testing.assert_allclose(v[c], ref[c], atol=2e-6)
         assert sum(w.cr.ranges(1)) == w.range
         w.cr.dispose()
 
