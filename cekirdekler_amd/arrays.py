@@ -362,6 +362,33 @@ class ClArray:
     def __setitem__(self, i, v):
         self.array[i] = v
 
+    # The reference's IList<T> members (ClArray.cs:1105-1353) are all
+    # NotImplementedException stubs there.  Here the read-only queries work
+    # on the host array.  The size-changing ones stay refused: a ClArray has a
+    # fixed length that its device buffers mirror.
+    def __iter__(self):
+        return iter(self.array)
+
+    def __contains__(self, item) -> bool:
+        return bool(np.any(self.array == item))
+
+    def contains(self, item) -> bool:
+        return item in self
+
+    def index_of(self, item) -> int:
+        """First index of ``item`` in the host array, -1 if absent (IList.IndexOf)."""
+        hits = np.flatnonzero(self.array == item)
+        return int(hits[0]) if len(hits) else -1
+
+    is_read_only = property(lambda self: False)
+
+    def _fixed_size(self, *args, **kwargs):
+        raise NotImplementedError("a ClArray has a fixed length (its device buffers mirror it); "
+                                  "resize by creating a new ClArray")
+
+    Contains, IndexOf, IsReadOnly, GetEnumerator = contains, index_of, is_read_only, __iter__
+    Add = Insert = Remove = RemoveAt = Clear = _fixed_size
+
     def ToArray(self) -> np.ndarray:  # noqa: N802
         return self.array.copy()
 

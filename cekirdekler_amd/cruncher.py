@@ -720,6 +720,37 @@ class Cores:
 
     deviceNames = device_names
 
+    # The reference Cores' mode switches and error state (Cores.cs:80-140),
+    # forwarded to the cruncher that runs this Cores.
+    def _fwd(name):  # noqa: N805
+        return property(lambda self: getattr(self.cruncher, name),
+                        lambda self, v: setattr(self.cruncher, name, v))
+
+    enqueue_mode = _fwd("enqueue_mode")
+    enqueue_mode_async_enable = _fwd("enqueue_mode_async_enable")
+    fine_grained_queue_control = _fwd("fine_grained_queue_control")
+    no_compute_mode = _fwd("no_compute_mode")
+    smooth_load_balancer = _fwd("smooth_load_balancer")
+    del _fwd
+    enqueueMode, enqueueModeAsyncEnable = enqueue_mode, enqueue_mode_async_enable
+    fineGrainedQueueControl, noComputeMode, smoothLoadBalancer = (
+        fine_grained_queue_control, no_compute_mode, smooth_load_balancer)
+
+    def error_code(self) -> int:
+        return self.cruncher.error_code()
+
+    def error_message(self) -> str:
+        return self.cruncher.error_message()
+
+    errorCode, errorMessage = error_code, error_message
+
+    @property
+    def all_errors_string(self) -> str:
+        """Every initialisation / build error so far (Cores.allErrorsString)."""
+        return self.cruncher.error_message()
+
+    allErrorsString = all_errors_string
+
     def dispose(self) -> None:
         self.cruncher.dispose()
 

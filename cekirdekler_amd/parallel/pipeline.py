@@ -89,6 +89,10 @@ class ClPipelineStage:
         self.elapsed_time = 0.0
         self.stage_id = 0
         self._resident = False
+        # run this stage's kernels back to back without a host sync between
+        # them (ClPipelineStage.enqueueMode, ClPipeline.cs:212); the stage
+        # still drains before its outputs move on
+        self.enqueue_mode = False
 
     # ---- building -----------------------------------------------------------
     def add_devices(self, devices: ClDevices) -> None:
@@ -136,6 +140,8 @@ class ClPipelineStage:
     addOutputBuffers = add_output_buffers
     prependToStage = prepend_to_stage
     appendToStage = append_to_stage
+    enqueueMode = property(lambda self: self.enqueue_mode,
+                           lambda self, v: setattr(self, "enqueue_mode", bool(v)))
 
     def make_pipeline(self) -> "ClPipeline":
         head = self
@@ -221,8 +227,15 @@ class ClPipelineStage:
     def run(self) -> None:
         t0 = time.perf_counter()
         g = self._group(False)
-        for i, (k, G, L) in enumerate(zip(self.kernel_names, self.global_ranges, self.local_ranges)):
-            g.compute(self.cruncher, 1 + i, k, G, L)
+        enqueue = self.enqueue_mode and len(self.kernel_names) > 1
+        if enqueue:
+            self.cruncher.enqueue_mode = True
+        try:
+            for i, (k, G, L) in enumerate(zip(self.kernel_names, self.global_ranges, self.local_ranges)):
+                g.compute(self.cruncher, 1 + i, k, G, L)
+        finally:
+            if enqueue:
+                self.cruncher.enqueue_mode = False  # drains the stage's queues
         self.elapsed_time = (time.perf_counter() - t0) * 1e3
 
     def _replica_ptr(self, a: ClArray, device: int = 0) -> int:

@@ -70,13 +70,32 @@ class ClTask:
         self._callback_ran = False
         self.device_index: Optional[int] = None  # which device computed it (set by the pool)
         self.elapsed_ms = 0.0
+        # run the task's kernels this many times, with kernel_repeat_name
+        # between repeats (the cruncher's repeatCount / repeatKernelName for
+        # one task; NotImplementedException stubs in ClPipeline.cs:3368-3373)
+        self.kernel_repeats = 1
+        self.kernel_repeat_name = ""
+
+    kernelRepeats = property(lambda self: self.kernel_repeats,
+                             lambda self, v: setattr(self, "kernel_repeats", int(v)))
+    kernelRepeatName = property(lambda self: self.kernel_repeat_name,
+                                lambda self, v: setattr(self, "kernel_repeat_name", str(v)))
+
+    def _apply_repeats(self, call) -> None:
+        call.repeats = max(1, int(self.kernel_repeats))
+        call.repeat_kernel = self.kernel_repeat_name if self.kernel_repeats > 1 else ""
 
     def compute(self, cruncher: ClNumberCruncher) -> None:
         if self.group is None or self.type & ClTaskType.TASK_MESSAGE_NO_COMPUTE and not self.kernels:
             return
-        cruncher._compute_group(self.group, self.compute_id, self.kernels, self.global_range, self.local_range,
-                                self.global_offset, self.pipeline, self.pipeline_type, self.pipeline_blobs,
-                                specs=self.specs)
+        saved = cruncher.repeat_count, cruncher.repeat_kernel_name
+        cruncher.repeat_count, cruncher.repeat_kernel_name = max(1, int(self.kernel_repeats)), self.kernel_repeat_name
+        try:
+            cruncher._compute_group(self.group, self.compute_id, self.kernels, self.global_range, self.local_range,
+                                    self.global_offset, self.pipeline, self.pipeline_type, self.pipeline_blobs,
+                                    specs=self.specs)
+        finally:
+            cruncher.repeat_count, cruncher.repeat_kernel_name = saved
 
     def set_callback(self, fn: Callable[[], None]) -> None:
         self.callback = fn
@@ -268,6 +287,7 @@ class ClDevicePool:
                     pt.call = cr0._build_call(ClParameterGroup(), t.compute_id, t.kernels, t.global_range,
                                               t.local_range, t.global_offset, t.pipeline, t.pipeline_type,
                                               t.pipeline_blobs, specs=t.specs)
+                    t._apply_repeats(pt.call)
                 except ClComputeError as e:
                     raise ClComputeError(f"task {pt.id}: {e}") from None
             copies = ndev if t.type & ClTaskType.TASK_MESSAGE_BROADCAST else 1

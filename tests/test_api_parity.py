@@ -1,0 +1,46 @@
+"""Reference API members that are not compute paths: ClArray's IList<T>
+members (NotImplementedException stubs in ClArray.cs:1105-1353; read-only
+queries work here, size changes are refused) and the usage-type-2 Cores
+mode switches / error state (Cores.cs:80-140)."""
+import numpy as np
+import pytest
+
+import cekirdekler_amd as ck
+
+
+def test_clarray_list_queries():
+    a = ck.ClArray(np.array([1, 2, 3, 2], np.float32))
+    assert list(a) == [1, 2, 3, 2]
+    assert 2 in a and 7 not in a
+    assert a.Contains(3) and not a.contains(9)
+    assert a.IndexOf(2) == 1 and a.index_of(9) == -1
+    assert a.IsReadOnly is False
+    for op in (lambda: a.Add(1), lambda: a.Insert(0, 1), lambda: a.Remove(1), lambda: a.RemoveAt(0),
+               lambda: a.Clear()):
+        with pytest.raises(NotImplementedError):
+            op()
+    assert len(a) == 4
+    b = ck.ClArray(16, np.float32)  # pinned native array
+    b.array[:] = np.arange(16)
+    assert b.IndexOf(5) == 5 and list(b)[:3] == [0, 1, 2]
+
+
+def test_cores_usage_type_2_modes_and_errors():
+    src = "__global__ void k(float* a) { a[get_global_id(0)] += 1.0f; }"
+    c = ck.Cores("cpu", src, ["k"])
+    assert c.errorCode() == 0 and c.errorMessage() == "" and c.allErrorsString == ""
+    assert c.smoothLoadBalancer is True
+    for name in ("enqueueMode", "enqueueModeAsyncEnable", "fineGrainedQueueControl", "noComputeMode"):
+        assert getattr(c, name) is False
+    a = ck.ClArray(np.zeros(256, np.float32))
+    c.enqueueMode = True
+    assert c.cruncher.enqueue_mode
+    for _ in range(3):
+        c.compute("k", 1, "", [a], ["read write"], [1], 256, 1)
+    c.enqueueMode = False  # drains
+    np.testing.assert_array_equal(a.array, 3.0)
+    c.noComputeMode = True
+    c.compute("k", 1, "", [a], ["read write"], [1], 256, 1)
+    c.noComputeMode = False
+    np.testing.assert_array_equal(a.array, 3.0)  # no kernel ran
+    c.dispose()

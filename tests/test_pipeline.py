@@ -130,3 +130,32 @@ def test_device_pipeline_timeline_on_cpu():
     assert dp.query_timeline_overlap_percentage() == 0.0
     assert dp.stages_overlapping_percentages() == [0.0, 0.0]
     dp.dispose()
+
+
+def test_stage_enqueue_mode_runs_its_kernels_back_to_back():
+    """ClPipelineStage.enqueueMode (ClPipeline.cs:212): a stage with two
+    kernels runs them without a host sync between them and gives the same
+    results as the synchronous stage."""
+    cpu = ck.ClPlatforms.all().cpus(True)
+    outs = []
+    for enq in (False, True):
+        x, w = np.zeros(N, np.float32), np.zeros(N, np.float32)
+        s = ClPipelineStage()
+        s.add_devices(cpu)
+        s.add_kernels(K1, "add1", [N], [64])
+        s.add_kernels("__global__ void dbl(const float* x, float* y) { long long i = get_global_id(0); y[i] = y[i] * 2.0f; }",
+                      "dbl", [N], [64])
+        s.add_input_buffers(x)
+        s.add_output_buffers(w)
+        s.enqueueMode = enq
+        assert s.enqueue_mode is enq
+        pipe = s.make_pipeline()
+        res = np.zeros(N, np.float32)
+        got = []
+        for p in range(6):
+            if pipe.push_data([np.full(N, float(p), np.float32)], [res]):
+                got.append(float(res[0]))
+        outs.append(got)
+        assert not s.cruncher.enqueue_mode  # left after every run
+        pipe.dispose()
+    assert outs[0] == outs[1] == [(p + 1) * 2.0 for p in range(len(outs[0]))]

@@ -197,3 +197,32 @@ def test_queue_limit_shrinks_as_pool_drains():
     assert {10, 6, 4}.issubset(h), h
     assert len(pool.marker_reach_speeds()) == 2
     pool.dispose()
+
+
+def test_task_kernel_repeats():
+    """ClTask.kernelRepeats / kernelRepeatName (stubs in the reference,
+    ClPipeline.cs:3368-3373): one task runs its kernel list that many times,
+    through the device pool and through task.compute(cruncher)."""
+    cpu = ck.ClPlatforms.all().cpus(True)
+    pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, False, 2)
+    pool.add_device(cpu + cpu)
+    tp = ClTaskPool()
+    arrays = []
+    for reps in (1, 2, 5):
+        x, t = _task("add", 256, 1.0)
+        t.kernelRepeats = reps
+        assert t.kernel_repeats == reps and t.kernelRepeatName == ""
+        tp.feed(t)
+        arrays.append((reps, x))
+    pool.enqueue_task_pool(tp)
+    pool.finish()
+    for reps, x in arrays:
+        np.testing.assert_array_equal(x.array, float(reps))
+    pool.dispose()
+    cr = ck.ClNumberCruncher(cpu, SRC)
+    x, t = _task("add", 256, 2.0)
+    t.kernel_repeats = 3
+    t.compute(cr)
+    np.testing.assert_array_equal(x.array, 6.0)
+    assert cr.repeat_count == 1  # the cruncher's own setting is restored
+    cr.dispose()
