@@ -65,6 +65,8 @@ class ClUserEvent:
 
     def __init__(self):
         self._ev = cek.UserEvent()
+        self._holds = 0
+        self._lock = threading.Lock()
 
     def add_cruncher(self, cruncher: "ClNumberCruncher", device: int = -1) -> None:
         cruncher.cores.gate(self._ev, int(device))
@@ -73,6 +75,31 @@ class ClUserEvent:
 
     def trigger(self) -> None:
         self._ev.trigger()
+
+    # Counter form (ClUserEvent.inc / dec, ClUserEvent.cs:66-84): every inc()
+    # is a hold on the gated streams, every dec() releases one; the streams
+    # start when the last hold is released.
+    def inc(self) -> None:
+        with self._lock:
+            self._holds += 1
+
+    def dec(self) -> None:
+        with self._lock:
+            if self._holds <= 0:
+                raise RuntimeError("ClUserEvent.dec() without a matching inc()")
+            self._holds -= 1
+            release = self._holds == 0
+        if release:
+            self.trigger()
+
+    @property
+    def count(self) -> int:
+        return self._holds
+
+    def dispose(self) -> None:
+        """Releases any stream still gated (never leaves a queue blocked)."""
+        if self.armed:
+            self.trigger()
 
     @property
     def armed(self) -> bool:
@@ -657,6 +684,9 @@ class Cores:
     with the readWrite token strings ``partial read write all ro wo zc``
     (plus the extension token ``gather``: keep-resident all-gather)
     (ClArray.cs:611-629, Cores.cs:471)."""
+
+    PIPELINE_EVENT = PIPELINE_EVENT    # Cores.cs:416-423
+    PIPELINE_DRIVER = PIPELINE_DRIVER
 
     def __init__(self, device_types, kernel_source: str, kernel_names=None, default_queue: bool = False,
                  local_range: int = 256, num_gpus: int = -1, stream: bool = True, max_cpu: int = -1,

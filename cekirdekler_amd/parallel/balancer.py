@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import math
 from functools import reduce
-from typing import List, Sequence, Tuple
+from typing import Optional, List, Sequence, Tuple
 
 from .._native import cek
 
@@ -165,3 +165,49 @@ class ClusterLoadBalancer:
                 out[i] -= cut
                 return out, cut - excess
         return out, 0
+
+    # ---- the reference's spellings and call shapes (ClusterLoadBalancer.cs):
+    # ranges are filled in place and the mainframe's remainder is returned;
+    # tmpMenziller / tmpHizlar keep the last ranges / per-node throughputs.
+    tmpMenziller: Optional[List[int]] = None
+    tmpHizlar: Optional[List[float]] = None
+
+    def dengeleEsit(self, toplamMenzil: int, menziller: List[int], adim: Sequence[int]) -> int:  # noqa: N802,N803
+        """Equal first split (ClusterLoadBalancer.cs:143)."""
+        ranges, rem = self.equal_split(toplamMenzil, adim)
+        menziller[:] = ranges
+        self.tmpMenziller = list(ranges)
+        return rem
+
+    def balanceOnPerformances(self, sureler: Sequence[float], toplamMenzil: int, menziller: List[int],  # noqa: N802,N803
+                              adim: Sequence[int], anaBilgisayarThread: int = 0,  # noqa: N803
+                              anaBilgisayarSure: float = 0.0) -> int:  # noqa: N803
+        """Damped re-split (ClusterLoadBalancer.cs:233).  Returns the
+        mainframe's remainder, or -1 when an over-subscribed split could not be
+        cut back on any node (the reference's return value in that case)."""
+        ms = [max(abs(t), 0.0001) for t in sureler]
+        self.tmpHizlar = [menziller[i] / ms[i] for i in range(len(menziller))]
+        before = list(menziller)
+        ranges, rem = self.balance(sureler, toplamMenzil, before, adim, anaBilgisayarThread)
+        menziller[:] = ranges
+        self.tmpMenziller = list(ranges)
+        if rem == 0 and sum(ranges) > toplamMenzil:
+            return -1
+        return rem
+
+    def sonuc(self) -> None:
+        """Prints the last ranges and their sum (ClusterLoadBalancer.cs:56)."""
+        if self.tmpMenziller is not None:
+            print(" ".join(str(r) for r in self.tmpMenziller))
+            print(sum(self.tmpMenziller))
+
+    @staticmethod
+    def obeb(a: int, b: int) -> int:
+        """Greatest common divisor (ClusterLoadBalancer.cs:72)."""
+        return _gcd(a, b)
+
+    @staticmethod
+    def okek(data: Sequence[int]) -> int:
+        """Least common multiple of every step (ClusterLoadBalancer.cs:121)."""
+        return lcm(list(data))
+

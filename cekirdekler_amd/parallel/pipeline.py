@@ -437,12 +437,30 @@ class DevicePipelineStage:
         self.local_range = local_range
         self.arrays: List[DevicePipelineArray] = []
         self.index = 0
+        # skip this stage's host↔device copies of its INPUT / OUTPUT arrays
+        # from now on (stopHostDeviceTransmission, ClPipeline.cs:2678): the
+        # stage keeps computing on what its device buffers hold
+        self.stop_host_device_transmission = False
 
     def bind_array(self, arr: DevicePipelineArray) -> None:
         self.arrays.append(arr)
         arr.stages.append(self)
 
+    @property
+    def has_input(self) -> bool:
+        """True if any bound array is an INPUT (ClPipeline.cs:2812)."""
+        return any(a.type == DevicePipelineArrayType.INPUT for a in self.arrays)
+
+    @property
+    def has_output(self) -> bool:
+        """True if any bound array is an OUTPUT (ClPipeline.cs:2829)."""
+        return any(a.type == DevicePipelineArrayType.OUTPUT for a in self.arrays)
+
     bindArray = bind_array
+    hasInput, hasOutput = has_input, has_output
+    stopHostDeviceTransmission = property(
+        lambda self: self.stop_host_device_transmission,
+        lambda self, v: setattr(self, "stop_host_device_transmission", bool(v)))
 
 
 def _coverage(intervals):
@@ -552,10 +570,10 @@ class DevicePipeline:
                 buf.read = buf.write = buf.partial_read = False
             elif a.type == DevicePipelineArrayType.INPUT:
                 buf = a.buffers()[p]          # host fills the other one meanwhile
-                buf.read, buf.write, buf.partial_read = True, False, False
+                buf.read, buf.write, buf.partial_read = not st.stop_host_device_transmission, False, False
             elif a.type == DevicePipelineArrayType.OUTPUT:
                 buf = a.buffers()[p]
-                buf.read, buf.write, buf.partial_read = False, True, False
+                buf.read, buf.write, buf.partial_read = False, not st.stop_host_device_transmission, False
             else:  # TRANSITION: producer (first bound stage) writes p, consumer reads 1-p
                 producer = a.stages[0] is st
                 buf = a.buffers()[p if producer else 1 - p]
@@ -601,6 +619,12 @@ class DevicePipeline:
     feedAsync = feed_async
     feedAsyncBegin = feed_async_begin
     feedAsyncEnd = feed_async_end
+
+    def async_host_work(self) -> None:
+        """Reference placeholder with an empty body (ClPipeline.cs:2663); host
+        work beside a step is :meth:`feed_async`'s callback here."""
+
+    asyncHostWork = async_host_work
 
     def input_buffer(self, arr: DevicePipelineArray) -> ClArray:
         """The host-side INPUT buffer the host may fill for the next feed."""

@@ -44,3 +44,20 @@ def test_cores_usage_type_2_modes_and_errors():
     c.noComputeMode = False
     np.testing.assert_array_equal(a.array, 3.0)  # no kernel ran
     c.dispose()
+
+
+def test_cluster_balancer_reference_call_shapes():
+    """ClusterLoadBalancer.dengeleEsit / balanceOnPerformances / obeb / okek
+    (ClusterLoadBalancer.cs:72-330): ranges filled in place, the mainframe's
+    remainder returned."""
+    from cekirdekler_amd.parallel.balancer import ClusterLoadBalancer
+
+    cb = ClusterLoadBalancer()
+    assert cb.obeb(256, 768) == 256 and cb.okek([256, 768]) == 768
+    r = [0, 0]
+    rem = cb.dengeleEsit(10 * 768, r, [256, 768])
+    assert sum(r) + rem == 10 * 768 and r == cb.tmpMenziller
+    new, rem_t = cb.balance([10.0, 5.0], 10 * 768, list(r), [256, 768])
+    rem2 = cb.balanceOnPerformances([10.0, 5.0], 10 * 768, r, [256, 768])
+    assert r == new and rem2 == rem_t and r[1] > r[0]
+    assert cb.tmpHizlar is not None and len(cb.tmpHizlar) == 2

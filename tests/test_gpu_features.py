@@ -512,3 +512,36 @@ def test_enqueue_batch_span_single_device(gpu):
     np.testing.assert_array_equal(x.array, 61.0)
     assert cr1.benchmarks(21)[0] > 0
     cr1.dispose()
+
+
+def test_device_pipeline_stop_host_device_transmission(gpu):
+    """stopHostDeviceTransmission (ClPipeline.cs:2678): the stage keeps
+    computing on its device buffers, but no INPUT goes up and no OUTPUT comes
+    down until it is cleared again."""
+    from cekirdekler_amd.parallel.pipeline import (DevicePipeline, DevicePipelineArray, DevicePipelineArrayType,
+                                                   DevicePipelineStage)
+
+    n = 4096
+    src = "__global__ void add1(const float* x, float* y) { long long i = get_global_id(0); y[i] = x[i] + 1.0f; }"
+    dp = DevicePipeline(gpu[0], src)
+    inp = DevicePipelineArray(DevicePipelineArrayType.INPUT, np.zeros(n, np.float32))
+    out = DevicePipelineArray(DevicePipelineArrayType.OUTPUT, np.zeros(n, np.float32))
+    st = DevicePipelineStage("add1", n, 256)
+    st.bind_array(inp)
+    st.bind_array(out)
+    dp.add_stage(st)
+    for p in range(4):
+        dp.input_buffer(inp).array[:] = p
+        dp.feed()
+    host_out = sorted(float(x.array[0]) for x in out.buffers())
+    st.stop_host_device_transmission = True
+    for p in range(4):
+        dp.input_buffer(inp).array[:] = 100 + p
+        dp.feed()
+    assert sorted(float(x.array[0]) for x in out.buffers()) == host_out  # nothing came down
+    st.stop_host_device_transmission = False
+    for _ in range(2):
+        dp.input_buffer(inp).array[:] = 7
+        dp.feed()
+    assert float(dp.output_buffer(out).array[0]) == 8.0
+    dp.dispose()

@@ -159,3 +159,40 @@ def test_stage_enqueue_mode_runs_its_kernels_back_to_back():
         assert not s.cruncher.enqueue_mode  # left after every run
         pipe.dispose()
     assert outs[0] == outs[1] == [(p + 1) * 2.0 for p in range(len(outs[0]))]
+
+
+def test_device_pipeline_stage_queries_and_user_event_counter():
+    """DevicePipelineStage.hasInput / hasOutput (ClPipeline.cs:2812-2840), the
+    stopHostDeviceTransmission switch (its effect on copies is checked on a
+    GPU: a CPU device computes in host memory) and the ClUserEvent counter."""
+    cpu = ck.ClPlatforms.all().cpus(True)
+    dp = DevicePipeline(cpu, K1)
+    inp = DevicePipelineArray(DevicePipelineArrayType.INPUT, np.zeros(N, np.float32))
+    out = DevicePipelineArray(DevicePipelineArrayType.OUTPUT, np.zeros(N, np.float32))
+    a = DevicePipelineStage("add1", N, 64)
+    a.bind_array(inp)
+    a.bind_array(out)
+    assert a.hasInput and a.hasOutput
+    assert not DevicePipelineStage("add1", N, 64).has_input
+    dp.add_stage(a)
+    a.stopHostDeviceTransmission = True
+    assert a.stop_host_device_transmission
+    dp.feed()
+    a.stop_host_device_transmission = False
+    dp.input_buffer(inp).array[:] = 7
+    dp.feed()
+    dp.feed()
+    assert float(dp.output_buffer(out).array[0]) == 8.0
+    dp.async_host_work()
+    dp.dispose()
+    ev = ck.ClUserEvent()
+    ev.inc()
+    ev.inc()
+    ev.dec()
+    assert ev.count == 1
+    ev.dec()
+    assert ev.count == 0
+    import pytest
+    with pytest.raises(RuntimeError):
+        ev.dec()
+    ev.dispose()
