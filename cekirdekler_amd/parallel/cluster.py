@@ -23,6 +23,7 @@ from __future__ import annotations
 import socket
 import struct
 import threading
+from dataclasses import dataclass
 import time
 from typing import List, Optional, Sequence
 
@@ -380,13 +381,31 @@ class ClCruncherClient:
 # --------------------------------------------------------------------------- accelerator
 
 
-def find_servers(candidates: Sequence[str], ports: Sequence[int], timeout: float = 0.3) -> List[tuple]:
+@dataclass
+class ServerInfoSimple:
+    """One discovered compute server (ClusterAccelerator.ServerInfoSimple,
+    ClusterAccelerator.cs:41-47): the reference rates a server by
+    1 / (0.1 + ping round trip in ms); here the round trip is the CONTROL
+    handshake's."""
+    port: int
+    ip_string: str
+    name_of_server: str = ""
+    round_trip_performance: float = 0.0
+
+    ipString = property(lambda self: self.ip_string)
+    nameOfServer = property(lambda self: self.name_of_server)
+    roundTripPerformance = property(lambda self: self.round_trip_performance)
+
+
+def find_servers(candidates: Sequence[str], ports: Sequence[int], timeout: float = 0.3,
+                 infos: Optional[List["ServerInfoSimple"]] = None) -> List[tuple]:
     """Probe ``host`` × ``port`` candidates with the CONTROL handshake, in
     parallel (the reference pings then tests each address from a
     ``Parallel.For``, ClusterAccelerator.cs:77-154).  Returns the answering
     ``(host, port)`` pairs in candidate order."""
     pairs = [(h, p) for p in ports for h in candidates]
     ok = [False] * len(pairs)
+    rtt = [0.0] * len(pairs)
 
     def probe(i):
         host, port = pairs[i]
@@ -395,7 +414,9 @@ def find_servers(candidates: Sequence[str], ports: Sequence[int], timeout: float
         except OSError:
             return
         try:
+            t0 = time.perf_counter()
             ok[i] = c.control()
+            rtt[i] = (time.perf_counter() - t0) * 1e3
         finally:
             c.sock.close()
 
@@ -404,6 +425,8 @@ def find_servers(candidates: Sequence[str], ports: Sequence[int], timeout: float
         t.start()
     for t in threads:
         t.join()
+    if infos is not None:
+        infos.extend(ServerInfoSimple(p, h, h, 1.0 / (0.1 + r)) for (h, p), good, r in zip(pairs, ok, rtt) if good)
     return [pr for pr, good in zip(pairs, ok) if good]
 
 
@@ -450,6 +473,8 @@ def sweep_candidates(fast: bool) -> List[str]:
 class ClusterAccelerator(IComputeNode):
     """Range split over compute servers + the local mainframe node."""
 
+    ServerInfoSimple = ServerInfoSimple
+
     def __init__(self):
         self.clients: List[ClCruncherClient] = []
         self.mainframe = None
@@ -457,6 +482,7 @@ class ClusterAccelerator(IComputeNode):
         self._state = {}
         self.last_ms: List[float] = []
         self.discovered: List[tuple] = []
+        self.servers: List[ServerInfoSimple] = []  # discovery results with round-trip ratings
 
     def setup_nodes(self, nodes, *args, **kwargs) -> None:
         """``nodes`` is an explicit ``[(host, port), ...]`` list (then
@@ -476,7 +502,8 @@ class ClusterAccelerator(IComputeNode):
         (:func:`sweep_candidates`), sets every server up with the string's
         device types and builds the ``node0_g``/``node0_c`` mainframe."""
         spec = parse_cluster_devices(device_types)
-        self.discovered = find_servers(sweep_candidates(spec["fast_search"]), spec["ports"])
+        self.servers = []
+        self.discovered = find_servers(sweep_candidates(spec["fast_search"]), spec["ports"], infos=self.servers)
         self._setup_list(self.discovered, spec["server_devices"] or "gpu", kernels, kernel_names, local_range,
                          num_gpus, stream, max_cpu, spec["mainframe"])
 

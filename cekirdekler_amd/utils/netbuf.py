@@ -178,6 +178,37 @@ class NetworkBuffer:
     def record_string(r: Record) -> str:
         return r.data.astype("<u2").tobytes().decode("utf-16-le")
 
+    # ---- the reference's spellings (NetworkBuffer.cs:52-830) ----------------
+    SETUP, COMPUTE, DISPOSE = SETUP, COMPUTE, DISPOSE
+    ANSWER_SUCCESS, ANSWER_DELETED, ANSWER_COMPUTE_COMPLETE = ANSWER_SUCCESS, ANSWER_DELETED, ANSWER_COMPUTE_COMPLETE
+    SERVER_STOP, ANSWER_STOPPED, SERVER_CONTROL, ANSWER_CONTROL = (SERVER_STOP, ANSWER_STOPPED, SERVER_CONTROL,
+                                                                  ANSWER_CONTROL)
+    SERVER_NUMBER_OF_DEVICES, ANSWER_NUMBER_OF_DEVICES = SERVER_NUMBER_OF_DEVICES, ANSWER_NUMBER_OF_DEVICES
+    receiveSendBufferSize = 8 * 1024  # socket send/receive buffer (NetworkBuffer.cs:52)
+
+    def bufferCommand(self) -> int:  # noqa: N802
+        return int(self.command)
+
+    def komutBelirle(self, k: int) -> None:  # noqa: N802  (set the command)
+        self.command = int(k)
+
+    @staticmethod
+    def komutOku(b: bytes) -> int:  # noqa: N802  (read the command of a serialized buffer)
+        return NetworkBuffer.parse(b)[0]
+
+    readLengthOfBuffer = read_length
+
+    def elemanSay(self) -> int:  # noqa: N802  (number of records)
+        return len(self._parts) // 2
+
+    def addArray(self, arr, hash_: int, ref: int = 0, range_: int = -1, epw: int = 1) -> None:  # noqa: N802
+        self.add_array(np.asarray(arr), hash_, ref, range_, epw)
+
+    @staticmethod
+    def oku(b: bytes):
+        """Parse a serialized buffer: (command, records) (NetworkBuffer.oku)."""
+        return NetworkBuffer.parse(b)
+
 
 def _i32(v: int) -> int:
     v = int(v) & 0xFFFFFFFF

@@ -80,6 +80,10 @@ def test_cluster_setup_by_device_string(monkeypatch):
         ports = ",".join(str(s.port) for s in servers)
         acc.setupNodes(f"cpu cluster:{ports} fast-search node0_c", SRC, ["saxpy"], 64)
         assert sorted(acc.discovered) == sorted(("127.0.0.1", s.port) for s in servers)
+        # ServerInfoSimple records (ClusterAccelerator.cs:41-47) with round-trip ratings
+        assert sorted((i.ipString, i.port) for i in acc.servers) == sorted(acc.discovered)
+        assert all(i.roundTripPerformance > 0 for i in acc.servers)
+        assert isinstance(acc.servers[0], ClusterAccelerator.ServerInfoSimple)
         assert acc.mainframe is not None
         n = 64 * 50 + 64
         a = np.array([4.0], np.float32)
