@@ -155,6 +155,18 @@ class FastArr:
 
     copy_from = CopyFrom
 
+    # native-to-native copies of elements [index, N) between equal-length
+    # arrays (FastArr.CopyTo_ / CopyFrom_, CSpaceArrays.cs:710-740)
+    def CopyTo_(self, dst: "FastArr", index: int = 0) -> None:  # noqa: N802
+        if len(dst) != len(self):
+            raise ValueError("CopyTo_ needs arrays of equal length")
+        dst.array[index:] = self.array[index:]
+
+    def CopyFrom_(self, src: "FastArr", index: int = 0) -> None:  # noqa: N802
+        if len(src) != len(self):
+            raise ValueError("CopyFrom_ needs arrays of equal length")
+        self.array[index:] = src.array[index:]
+
     @property
     def pinned(self) -> bool:
         return bool(cek.host_is_pinned(self._ptr))
