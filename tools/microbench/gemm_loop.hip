@@ -149,6 +149,7 @@ static void timeline(const char* name, void (*launch)(hipStream_t), int grid) {
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 20;
+  const int shift = argc > 2 ? atoi(argv[2]) : 4;  // the slice helper's K-tile deficit (dims[5])
   const size_t nab = (size_t)N * N;
   CK(hipMalloc(&g_A, nab * 2));
   CK(hipMalloc(&g_B, nab * 2));
@@ -167,7 +168,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(g_A, h.data(), nab * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(g_B, h.data(), nab * 2, hipMemcpyHostToDevice));
   int dims[8] = {N, N, N, 4, 1, 0, 0, 0};
-  int dims_s[8] = {SLICE, N, N, 4, 2, 4, 0, 0};
+  int dims_s[8] = {SLICE, N, N, 4, 2, shift, 0, 0};
   CK(hipMalloc(&g_dims, sizeof dims));
   CK(hipMalloc(&g_dims_slice, sizeof dims_s));
   CK(hipMemcpy(g_dims, dims, sizeof dims, hipMemcpyHostToDevice));
@@ -182,8 +183,8 @@ int main(int argc, char** argv) {
     printf("{\"variant\": \"%s\", \"kernel\": \"256x256pb\", \"shape\": \"8192^3\", \"ms\": %.4f, \"tflops\": %.1f}\n",
            variant, ms, 2.0 * N * N * (double)N / ms / 1e9);
     ms = time_kernel(launch_slice, reps);
-    printf("{\"variant\": \"%s\", \"kernel\": \"256x256pbw\", \"shape\": \"1024x8192x8192\", \"ms\": %.4f, \"tflops\": %.1f}\n",
-           variant, ms, 2.0 * SLICE * N * (double)N / ms / 1e9);
+    printf("{\"variant\": \"%s\", \"kernel\": \"256x256pbw\", \"shift\": %d, \"shape\": \"1024x8192x8192\", \"ms\": %.4f, \"tflops\": %.1f}\n",
+           variant, shift, ms, 2.0 * SLICE * N * (double)N / ms / 1e9);
   }
 #ifdef CEK_PROBE_TS
   timeline("256x256pb 8192^3", launch_full, (N / 256) * (N / 256));
