@@ -301,9 +301,10 @@ def _mandelbrot_kernel_only(kernel: str = "blk8u", reps: int = 20) -> dict:
     Two numbers: ``ms`` renders one image over and over on one stream (each
     launch drains before the next starts); ``frames_in_flight_2`` renders
     two images alternately in the reference's async enqueue mode
-    (enqueueModeAsyncEnable over 2 queues), so frame k+1's first waves fill
-    the SIMDs that frame k's last waves leave idle (double-buffered frames of
-    an animation; every frame is computed whole, tools/mandel_async_probe.py)."""
+    (enqueueModeAsyncEnable over 2 queues): the two frames' launches run side
+    by side, so the SIMDs stay full through each launch's ramp-up and drain
+    (double-buffered frames of an animation; every frame is computed whole,
+    tools/mandel_async_probe.py, profiles/mandelbrot_r3.md)."""
     import torch
 
     from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
