@@ -61,3 +61,17 @@ def test_cluster_balancer_reference_call_shapes():
     rem2 = cb.balanceOnPerformances([10.0, 5.0], 10 * 768, r, [256, 768])
     assert r == new and rem2 == rem_t and r[1] > r[0]
     assert cb.tmpHizlar is not None and len(cb.tmpHizlar) == 2
+
+
+def test_native_array_copy_to_from_index():
+    """FastArr.CopyTo_ / CopyFrom_ (CSpaceArrays.cs:710-740): elements
+    [index, N) between equal-length native arrays."""
+    a, b = ck.ClFloatArray(8), ck.ClFloatArray(8)
+    a.array[:] = np.arange(8)
+    b.array[:] = -1
+    a.CopyTo_(b, 3)
+    np.testing.assert_array_equal(b.array, [-1, -1, -1, 3, 4, 5, 6, 7])
+    b.CopyFrom_(a, 0)
+    np.testing.assert_array_equal(b.array, np.arange(8))
+    with pytest.raises(ValueError):
+        a.CopyTo_(ck.ClFloatArray(4), 0)
