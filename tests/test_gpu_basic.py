@@ -308,3 +308,30 @@ def test_gemm_f32_host_shells_matches_fp64():
     assert float(np.abs(got - ref).max() / np.abs(ref).max()) < 1e-5
     assert g.verify_shells(2, samples=4) < 1e-5
     g.cr.dispose()
+
+
+def test_mandelbrot_two_frames_in_flight_async_enqueue():
+    """bench.py's frames_in_flight_2: two renderers on one cruncher, rendered
+    alternately in async enqueue mode over 2 queues (launches run side by
+    side); both device images equal the numpy reference afterwards."""
+    from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
+    from cekirdekler_amd.ops.library import library
+
+    cr = ck.ClNumberCruncher(_gpu()[0], "", prebuilt=library("mandelbrot"), queue_concurrency=2)
+    ms = [MandelbrotRenderer(1024, 512, max_iter=100, cruncher=cr, kernel="blk8u") for _ in range(2)]
+    for i, m in enumerate(ms):
+        m.render(i + 1, pipeline=False)
+        m.out.write = False
+    ref = ms[0].reference()
+    cr.enqueue_mode_async_enable = True
+    cr.enqueue_mode = True
+    for k in range(8):
+        ms[k % 2].render(k % 2 + 1, pipeline=False)
+    cr.enqueue_mode = False
+    cr.enqueue_mode_async_enable = False
+    for m in ms:
+        m.out.array[:] = -1
+        cr.download(m.out, 0)
+        img = m.out.array.reshape(m.height, m.width)
+        assert np.mean(img != ref) < 2e-3
+    cr.dispose()
