@@ -28,6 +28,37 @@ class PyExchanger : public Exchanger {
   int world() const override { PYBIND11_OVERRIDE_PURE(int, Exchanger, world, ); }
 };
 
+// A data plane implemented in Python (e.g. torch.distributed gloo over host
+// memory for CPU devices): pointers and streams cross as integers.  Called
+// from compute() with the GIL released, so every override re-acquires it.
+class PyComm : public Comm {
+ public:
+  int rank() const override { PYBIND11_OVERRIDE_PURE(int, Comm, rank, ); }
+  int world() const override { PYBIND11_OVERRIDE_PURE(int, Comm, world, ); }
+  void broadcast(void* dptr, uint64_t bytes, int root, hipStream_t s) override {
+    call("broadcast", reinterpret_cast<uint64_t>(dptr), bytes, root, reinterpret_cast<uint64_t>(s));
+  }
+  void allgatherv(void* dptr, const std::vector<uint64_t>& offsets, const std::vector<uint64_t>& sizes,
+                  hipStream_t s) override {
+    call("allgatherv", reinterpret_cast<uint64_t>(dptr), offsets, sizes, reinterpret_cast<uint64_t>(s));
+  }
+  void allreduce_sum_f32(void* dptr, uint64_t count, hipStream_t s) override {
+    call("allreduce_sum_f32", reinterpret_cast<uint64_t>(dptr), count, reinterpret_cast<uint64_t>(s));
+  }
+  void allreduce_sum_f64(void* dptr, uint64_t count, hipStream_t s) override {
+    call("allreduce_sum_f64", reinterpret_cast<uint64_t>(dptr), count, reinterpret_cast<uint64_t>(s));
+  }
+
+ private:
+  template <typename... A>
+  void call(const char* name, A&&... args) {
+    py::gil_scoped_acquire g;
+    py::function f = py::get_override(static_cast<const Comm*>(this), name);
+    if (!f) throw Error(std::string("Comm.") + name + " is not implemented by this communicator");
+    f(std::forward<A>(args)...);
+  }
+};
+
 uint64_t py_host_alloc(uint64_t bytes, uint64_t align) {
   bool pinned = false;
   return reinterpret_cast<uint64_t>(host_alloc(bytes, align, &pinned));
@@ -285,21 +316,24 @@ PYBIND11_MODULE(_cek, m) {
       .def("allgather", &ShmExchanger::allgather, py::call_guard<py::gil_scoped_release>())
       .def("unlink", &ShmExchanger::unlink);
 
-  py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
-      .def_static("unique_id", []() { return py::bytes(Comm::unique_id()); })
+  py::class_<Comm, PyComm, std::shared_ptr<Comm>>(m, "Comm")
+      .def(py::init<>())
+      .def("rank", &Comm::rank)
+      .def("world", &Comm::world);
+
+  py::class_<RcclComm, Comm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
       .def(py::init([](py::bytes uid, int rank, int world, int device) {
         // copy the id while holding the GIL; only the RCCL rendezvous runs
         // without it (the bytes object is released by pybind11, GIL held)
         std::string id(uid);
         py::gil_scoped_release r;
-        return std::make_shared<Comm>(id, rank, world, device);
+        return std::make_shared<RcclComm>(id, rank, world, device);
       }))
-      .def_property_readonly("rank", &Comm::rank)
-      .def_property_readonly("world", &Comm::world)
-      .def("broadcast", [](Comm& c, uint64_t p, uint64_t bytes, int root, uint64_t stream) {
+      .def("broadcast", [](RcclComm& c, uint64_t p, uint64_t bytes, int root, uint64_t stream) {
         c.broadcast(reinterpret_cast<void*>(p), bytes, root, reinterpret_cast<hipStream_t>(stream));
       }, py::call_guard<py::gil_scoped_release>())
-      .def("allreduce_sum_f32", [](Comm& c, uint64_t p, uint64_t n, uint64_t stream) {
+      .def("allreduce_sum_f32", [](RcclComm& c, uint64_t p, uint64_t n, uint64_t stream) {
         c.allreduce_sum_f32(reinterpret_cast<void*>(p), n, reinterpret_cast<hipStream_t>(stream));
       }, py::call_guard<py::gil_scoped_release>());
 

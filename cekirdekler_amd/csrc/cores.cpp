@@ -1090,6 +1090,14 @@ void Cores::full_reads(Worker& wk, hipStream_t s, const ComputeCall& c, uint64_t
   }
 }
 
+// The call issues RCCL collectives (broadcast / split-read all-gather /
+// written-slice all-gather) that every rank must join, whatever its range.
+bool Cores::collective(const ComputeCall& c) const {
+  if (!comm_) return false;
+  if (dist_gather_writes || dist_broadcast_reads || dist_split_reads) return true;
+  return std::any_of(c.arrays.begin(), c.arrays.end(), [](const ArraySpec& a) { return a.gather && !a.zc; });
+}
+
 void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref, long long range,
                        uint64_t* h2d, uint64_t* d2h) {
   hipStream_t s = nullptr;
@@ -1390,8 +1398,9 @@ void Cores::run_device_body(int w, const ComputeCall& c, long long ref, long lon
       run_event_pipeline(wk, gidx, c, ref, range, h2d, d2h);
     else
       run_driver_pipeline(wk, gidx, c, ref, range, h2d, d2h);
-  } else if (comm_ && (dist_gather_writes || dist_broadcast_reads || dist_split_reads)) {
-    // still take part in the collectives
+  } else if (collective(c)) {
+    // still take part in the collectives (a rank the split rounded down to
+    // an empty range must join every RCCL call the others make)
     run_3phase(wk, gidx, c, ref, 0, h2d, d2h);
   }
   double el = now_ms() - t0 - t_phase_wait;
@@ -1524,7 +1533,7 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
   bool pipelined = pipe_req && c.repeats <= 1 && !enqueue_mode_ && !hazard && gather_idx.empty();
   for (int i = 0; i < D && pipelined; ++i)
     if (st.ranges[i] != 0 && (st.ranges[i] % (B * U) != 0 || st.ranges[i] < B * U)) pipelined = false;
-  if (comm_ && (dist_gather_writes || dist_broadcast_reads || dist_split_reads)) pipelined = false;
+  if (collective(c)) pipelined = false;
 
   std::vector<double> ms(nloc, 0.0);
   std::vector<uint64_t> h2d(nloc, 0), d2h(nloc, 0);
@@ -1543,7 +1552,7 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
   int participants = 0;
   std::vector<char> part(nloc, 0);
   for (int w = 0; w < nloc; ++w)
-    if (st.ranges[global_base_ + w] > 0 || (comm_ && (dist_gather_writes || dist_broadcast_reads || dist_split_reads))) {
+    if (st.ranges[global_base_ + w] > 0 || collective(c)) {
       part[w] = 1;
       ++participants;
     }

@@ -338,6 +338,7 @@ class Cores {
 
  private:
   PhaseBarrier* phase_ = nullptr;  // set while a hazardous compute runs
+  bool collective(const ComputeCall& c) const;
   void run_device(int w, const ComputeCall& c, long long ref, long long range, bool pipelined,
                   double* out_ms, uint64_t* h2d, uint64_t* d2h);
   void run_device_body(int w, const ComputeCall& c, long long ref, long long range, bool pipelined,

@@ -118,13 +118,13 @@ std::vector<double> ShmExchanger::allgather(const std::vector<double>& local) {
       throw Error(std::string("RCCL error in " #expr ": ") + ncclGetErrorString(_r)); \
   } while (0)
 
-std::string Comm::unique_id() {
+std::string RcclComm::unique_id() {
   ncclUniqueId id;
   CEK_NCCL(ncclGetUniqueId(&id));
   return std::string(id.internal, sizeof(id.internal));
 }
 
-Comm::Comm(const std::string& uid, int rank, int world, int device)
+RcclComm::RcclComm(const std::string& uid, int rank, int world, int device)
     : rank_(rank), world_(world), device_(device) {
   if (uid.size() != sizeof(ncclUniqueId)) throw Error("bad RCCL unique id size");
   ncclUniqueId id;
@@ -135,16 +135,16 @@ Comm::Comm(const std::string& uid, int rank, int world, int device)
   comm_ = c;
 }
 
-Comm::~Comm() {
+RcclComm::~RcclComm() {
   if (comm_) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
 }
 
-void Comm::broadcast(void* dptr, uint64_t bytes, int root, hipStream_t s) {
+void RcclComm::broadcast(void* dptr, uint64_t bytes, int root, hipStream_t s) {
   if (bytes == 0 || world_ == 1) return;
   CEK_NCCL(ncclBroadcast(dptr, dptr, bytes, ncclChar, root, static_cast<ncclComm_t>(comm_), s));
 }
 
-void Comm::allgatherv(void* dptr, const std::vector<uint64_t>& offsets,
+void RcclComm::allgatherv(void* dptr, const std::vector<uint64_t>& offsets,
                       const std::vector<uint64_t>& sizes, hipStream_t s) {
   if (world_ == 1) return;
   auto* base = static_cast<char*>(dptr);
@@ -166,11 +166,11 @@ void Comm::allgatherv(void* dptr, const std::vector<uint64_t>& offsets,
   CEK_NCCL(ncclGroupEnd());
 }
 
-void Comm::allreduce_sum_f32(void* dptr, uint64_t count, hipStream_t s) {
+void RcclComm::allreduce_sum_f32(void* dptr, uint64_t count, hipStream_t s) {
   CEK_NCCL(ncclAllReduce(dptr, dptr, count, ncclFloat32, ncclSum, static_cast<ncclComm_t>(comm_), s));
 }
 
-void Comm::allreduce_sum_f64(void* dptr, uint64_t count, hipStream_t s) {
+void RcclComm::allreduce_sum_f64(void* dptr, uint64_t count, hipStream_t s) {
   CEK_NCCL(ncclAllReduce(dptr, dptr, count, ncclFloat64, ncclSum, static_cast<ncclComm_t>(comm_), s));
 }
 

@@ -45,20 +45,38 @@ class ShmExchanger : public Exchanger {
   uint64_t epoch_ = 0;
 };
 
+// Data plane of a distributed job: broadcast / all-gather-v / all-reduce on
+// device (or, for CPU devices, host) memory, ordered on stream s.
 class Comm {
  public:
-  static std::string unique_id();  // bytes of an ncclUniqueId
-  Comm(const std::string& uid, int rank, int world, int device);
-  ~Comm();
-  int rank() const { return rank_; }
-  int world() const { return world_; }
+  virtual ~Comm() = default;
+  virtual int rank() const = 0;
+  virtual int world() const = 0;
   // In-place broadcast of `bytes` at dptr from root.
-  void broadcast(void* dptr, uint64_t bytes, int root, hipStream_t s);
+  virtual void broadcast(void* dptr, uint64_t bytes, int root, hipStream_t s) = 0;
   // In-place all-gather-v: rank r owns [offsets[r], offsets[r]+sizes[r]) bytes.
+  virtual void allgatherv(void* dptr, const std::vector<uint64_t>& offsets,
+                          const std::vector<uint64_t>& sizes, hipStream_t s) = 0;
+  virtual void allreduce_sum_f32(void* dptr, uint64_t count, hipStream_t s) = 0;
+  virtual void allreduce_sum_f64(void* dptr, uint64_t count, hipStream_t s) = 0;
+};
+
+// RCCL communicator over xGMI (one GPU per rank).
+class RcclComm : public Comm {
+ public:
+  static std::string unique_id();  // bytes of an ncclUniqueId
+  RcclComm(const std::string& uid, int rank, int world, int device);
+  ~RcclComm() override;
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  void broadcast(void* dptr, uint64_t bytes, int root, hipStream_t s) override;
+  // Equal contiguous slices: one ring all-gather.  Uneven slices (after the
+  // balancer moved work): one grouped broadcast per owner; with W of them in
+  // flight each link carries about (W-1)/W of the array, as a ring would.
   void allgatherv(void* dptr, const std::vector<uint64_t>& offsets,
-                  const std::vector<uint64_t>& sizes, hipStream_t s);
-  void allreduce_sum_f32(void* dptr, uint64_t count, hipStream_t s);
-  void allreduce_sum_f64(void* dptr, uint64_t count, hipStream_t s);
+                  const std::vector<uint64_t>& sizes, hipStream_t s) override;
+  void allreduce_sum_f32(void* dptr, uint64_t count, hipStream_t s) override;
+  void allreduce_sum_f64(void* dptr, uint64_t count, hipStream_t s) override;
 
  private:
   void* comm_ = nullptr;  // ncclComm_t

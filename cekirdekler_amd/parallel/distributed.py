@@ -93,6 +93,71 @@ class TorchExchanger(cek.Exchanger):
         return self._world
 
 
+class TorchComm(cek.Comm):
+    """The data plane of :class:`DistributedCruncher` over ``torch.distributed``
+    (gloo) on HOST memory: the broadcast of ``read`` arrays, the split-read
+    all-gather and the all-gather of written slices for ranks whose devices
+    are CPU devices (their "device replica" is the host array itself).  The
+    native scheduler calls it exactly where it calls RCCL on GPUs, so the
+    whole keep-resident / broadcast-reads protocol — including which ranks
+    must join which collective — runs in the GPU-less test tier."""
+
+    def __init__(self, rank: int, world: int, group=None):
+        super().__init__()
+        self._rank, self._world, self._group = rank, world, group
+
+    def rank(self) -> int:
+        return self._rank
+
+    def world(self) -> int:
+        return self._world
+
+    @staticmethod
+    def _view(ptr: int, nbytes: int, dtype=None):
+        import ctypes
+
+        import numpy as np
+        import torch
+
+        buf = (ctypes.c_uint8 * nbytes).from_address(ptr)
+        a = np.frombuffer(buf, dtype=np.uint8)
+        if dtype is not None:
+            a = a.view(dtype)
+        return torch.from_numpy(a)
+
+    def broadcast(self, ptr: int, nbytes: int, root: int, stream: int) -> None:
+        import torch.distributed as dist
+
+        if nbytes and self._world > 1:
+            dist.broadcast(self._view(ptr, nbytes), src=root, group=self._group)
+
+    def allgatherv(self, ptr: int, offsets, sizes, stream: int) -> None:
+        import torch.distributed as dist
+
+        if self._world <= 1:
+            return
+        for r in range(self._world):  # every rank joins every owner's broadcast
+            if sizes[r]:
+                dist.broadcast(self._view(ptr + offsets[r], sizes[r]), src=r, group=self._group)
+
+    def _allreduce(self, ptr: int, count: int, dtype) -> None:
+        import numpy as np
+        import torch.distributed as dist
+
+        if count and self._world > 1:
+            dist.all_reduce(self._view(ptr, count * np.dtype(dtype).itemsize, dtype), group=self._group)
+
+    def allreduce_sum_f32(self, ptr: int, count: int, stream: int) -> None:
+        import numpy as np
+
+        self._allreduce(ptr, count, np.float32)
+
+    def allreduce_sum_f64(self, ptr: int, count: int, stream: int) -> None:
+        import numpy as np
+
+        self._allreduce(ptr, count, np.float64)
+
+
 def _broadcast_object(obj, ctx: DistContext):
     import torch.distributed as dist
 
@@ -133,7 +198,7 @@ class DistributedCruncher(ClNumberCruncher):
             if comm and self._cores.num_devices == 1 and self.devices.device(0).is_gpu:
                 # a one-rank RCCL communicator: the data-plane code path (broadcast
                 # of reads, all-gather of written slices) runs exactly as at N ranks
-                self._comm = cek.Comm(cek.Comm.unique_id(), 0, 1, self.devices.device(0).info.ordinal)
+                self._comm = cek.RcclComm(cek.RcclComm.unique_id(), 0, 1, self.devices.device(0).info.ordinal)
                 self._cores.set_distributed(None, self._comm, 1, 0)
             return
         import torch.distributed as dist
@@ -156,8 +221,12 @@ class DistributedCruncher(ClNumberCruncher):
         else:
             self._exchanger = TorchExchanger(self.ctx.rank, self.ctx.world)
         if comm and nloc == 1 and self.devices.device(0).is_gpu:
-            uid = _broadcast_object(cek.Comm.unique_id() if self.ctx.rank == 0 else None, self.ctx)
-            self._comm = cek.Comm(uid, self.ctx.rank, self.ctx.world, self.devices.device(0).info.ordinal)
+            uid = _broadcast_object(cek.RcclComm.unique_id() if self.ctx.rank == 0 else None, self.ctx)
+            self._comm = cek.RcclComm(uid, self.ctx.rank, self.ctx.world, self.devices.device(0).info.ordinal)
+        elif comm and nloc == 1 and not self.devices.device(0).is_gpu:
+            # CPU devices compute on the host arrays: the collectives run over
+            # torch.distributed (gloo) on host memory
+            self._comm = TorchComm(self.ctx.rank, self.ctx.world)
         self._cores.set_distributed(self._exchanger, self._comm, self.ctx.world * nloc, self.ctx.rank * nloc)
 
     @property

@@ -83,3 +83,82 @@ def test_two_rank_balancing(exch, world):
     assert all(res[r][1] for r in range(world))  # each rank computed its own slice correctly
     last = res[0][0][-1]
     assert sum(last) == 64 * 512 and last[0] > last[1]  # faster rank 0 got more work
+
+
+GATHER_SRC = """
+__global__ void g(float* x) { long long i = get_global_id(0); x[i] = 2.0f * (float)i + 1.0f; }
+"""
+
+
+def _gather_worker(rank, world, port, q):
+    """a rank the split leaves with an EMPTY range must
+    still join the all-gather of a gather-flagged array, or every other rank
+    blocks in the collective.  The empty range comes from the reference law
+    itself: a restored state in which rank 1 held no range and measured as
+    stalled (Functions.loadBalance gives a zero-range device G·rate/Σ, which
+    rounds to 0)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), CEK_CPU_THREADS="2")
+    import cekirdekler_amd as ck
+    from cekirdekler_amd.parallel.distributed import DistributedCruncher, TorchComm, init_distributed
+
+    ctx = init_distributed("gloo")
+    cr = DistributedCruncher(GATHER_SRC, ctx=ctx, devices=ck.ClPlatforms.all().cpus(True), comm=True)
+    assert isinstance(cr._comm, TorchComm)
+    out = []
+    L, n = 64, 8 * 64
+    x = ck.ClArray(np.full(n, -1.0, np.float32))
+    x.read = False
+    x.write = False
+    x.gather_resident = True
+    x.compute(cr, 1, "g", n, L)  # creates the state of compute id 1
+    cr.cores.set_state(1, [n, 0], [[0.0, 0.0] for _ in range(10)], [1.0, 1e9])
+    for it in range(3):
+        x.array[:] = -1.0
+        x.compute(cr, 1, "g", n, L)
+        out.append((cr.ranges(1), bool(np.all(x.array == 2.0 * np.arange(n, dtype=np.float32) + 1.0))))
+    # broadcast of reads from rank 0 through the same communicator
+    src = ck.ClArray(np.arange(4 * L, dtype=np.float32) * (1.0 if rank == 0 else 0.0))
+    dst = ck.ClArray(np.zeros(4 * L, np.float32))
+    src.write = False
+    dst.read = False
+    cr2 = DistributedCruncher("""__global__ void c(const float* s, float* d) {
+        long long i = get_global_id(0); d[i] = s[i] + 0.5f; }""", ctx=ctx,
+                              devices=ck.ClPlatforms.all().cpus(True), comm=True)
+    cr2.broadcast_reads = True
+    src.next_param(dst).compute(cr2, 1, "c", 4 * L, L)
+    lo = cr2.references(1)[rank]
+    hi = lo + cr2.ranges(1)[rank]
+    bc_ok = bool(np.all(dst.array[lo:hi] == np.arange(lo, hi, dtype=np.float32) + 0.5))
+    q.put((rank, out, bc_ok))
+    import torch.distributed as dist
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_zero_range_rank_joins_gather():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, out, bc_ok = q.get(timeout=180)
+            res[r] = (out, bc_ok)
+    finally:
+        for p in procs:
+            p.join(60)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    for r in range(world):
+        out, bc_ok = res[r]
+        assert bc_ok, f"rank {r}: broadcast read wrong"
+        assert out[0][0] == [512, 0], out  # the empty-range case really happened
+        assert all(ok for (_, ok) in out), out  # every rank's host replica holds every slice
+    assert [o[0] for o in res[0][0]] == [o[0] for o in res[1][0]]

@@ -127,7 +127,7 @@ def test_rccl_data_plane_one_rank():
     assert cr.last_record()["h2d_bytes"] == a.array.nbytes
     cr.dispose()
 
-    comm = cek.Comm(cek.Comm.unique_id(), 0, 1, gpu.device(0).info.ordinal)
+    comm = cek.RcclComm(cek.RcclComm.unique_id(), 0, 1, gpu.device(0).info.ordinal)
     t = torch.arange(1024, dtype=torch.float32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     comm.allreduce_sum_f32(t.data_ptr(), t.numel(), s)

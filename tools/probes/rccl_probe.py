@@ -19,7 +19,7 @@ if which == "torch":
     dist.destroy_process_group()
 else:
     from cekirdekler_amd._native import cek
-    uid = cek.Comm.unique_id()
+    uid = cek.RcclComm.unique_id()
     print("unique id bytes", len(uid), flush=True)
-    c = cek.Comm(uid, 0, 1, 0)
+    c = cek.RcclComm(uid, 0, 1, 0)
     print("cek comm ok", c.rank, c.world, flush=True)
