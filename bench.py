@@ -21,8 +21,7 @@ device-resident after the first call and C stays in device memory
 C slices downloaded each call) is reported separately.  Data: synthetic
 uniform [-1, 1) bf16.  After the timed loops every rank downloads its device
 replica of C and compares sampled tiles of its own range with a float64 host
-product; the bench exits non-zero when the relative error exceeds 5e-3 or a
-K-split partner wait timed out.  Rank 0 prints one JSON line.
+product; the bench exits non-zero when the relative error exceeds 5e-3.  Rank 0 prints one JSON line.
 
 In a container without a GPU the headline runs a plain kernel-string GEMM on
 each rank's CPU device instead (``"device": "cpu"`` in the config): that is
@@ -157,7 +156,9 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     # against a float64 host product (before the host-resident run below
     # re-splits compute id 2 and overwrites the host copy)
     err = _max_over_ranks(ctx, g.verify(compute_id=1))
-    timeouts = int(_sum_over_ranks(ctx, g.spin_timeouts()))
+    # owners that found their split-K helper late and multiplied its K-range
+    # themselves (C correct either way; nonzero = a shared GPU)
+    fallbacks = int(_sum_over_ranks(ctx, g.handover_fallbacks()))
     host_steps = max(2, min(steps, 5))
     # host-resident: A and B uploaded and C downloaded on every call, through
     # the event-driven read/compute/write pipeline in 8 blobs (B a full
@@ -203,7 +204,7 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
             "host_resident_pipelined": host_piped, "host_resident_mode": mode,
             "host_resident_blob_pipeline_ms": ms_blobs, "host_resident_shells_ms": ms_shells,
             "ranges": ranges, "max_rel_err": max(err, err_host), "max_rel_err_host_resident": err_host,
-            "spin_timeouts": timeouts, "device": "gpu"}
+            "handover_fallbacks": fallbacks, "device": "gpu"}
 
 
 CPU_GEMM_SRC = """
@@ -254,7 +255,7 @@ def bench_sgemm_cpu(ctx, steps, warmup, size=256):
     return {"ms": ms, "gflops": flops / (ms * 1e-3) / 1e9, "tile": "cpu-naive", "balancer_setup_calls": converge,
             "sync_per_step_ms": ms, "sync_per_step_gflops": flops / (ms * 1e-3) / 1e9,
             "host_resident_ms": ms, "host_resident_gflops": flops / (ms * 1e-3) / 1e9,
-            "ranges": ranges, "max_rel_err": err, "spin_timeouts": 0, "device": "cpu"}
+            "ranges": ranges, "max_rel_err": err, "handover_fallbacks": 0, "device": "cpu"}
 
 
 def _all_ranges(ctx, ranges):
@@ -532,7 +533,7 @@ def main(argv=None) -> int:
         dist.destroy_process_group()  # the other ranks exit here; rank 0 goes on alone
     node = {} if (ctx.rank != 0 or args.skip_node_configs or not use_gpu) else bench_node_configs(ctx.world)
     peers = _peer_topology(ctx.world) if (ctx.rank == 0 and use_gpu) else {}
-    ok = sg["max_rel_err"] <= MAX_REL_ERR and sg["spin_timeouts"] == 0
+    ok = sg["max_rel_err"] <= MAX_REL_ERR
     if ctx.rank == 0:
         size = args.size if use_gpu else min(args.size, 512)
         out = {
@@ -566,7 +567,7 @@ def main(argv=None) -> int:
                 "sgemm_host_resident_blob_pipeline_ms": sg.get("host_resident_blob_pipeline_ms"),
                 "sgemm_host_resident_shells_ms": sg.get("host_resident_shells_ms"),
                 "sgemm_max_rel_err": sg["max_rel_err"],
-                "sgemm_spin_timeouts": sg["spin_timeouts"],
+                "sgemm_handover_fallbacks": sg["handover_fallbacks"],
                 "sgemm_balancer_setup_calls": sg["balancer_setup_calls"],
                 "sgemm_ranges": sg["ranges"],
                 "sgemm_ranges_identical_on_all_ranks": all(r == all_ranges[0] for r in all_ranges),
@@ -583,7 +584,7 @@ def main(argv=None) -> int:
         print(json.dumps(out), flush=True)
         if not ok:
             print(f"bench.py: SGEMM output check failed: max rel err {sg['max_rel_err']:.3e} "
-                  f"(limit {MAX_REL_ERR}), {sg['spin_timeouts']} spin timeouts", file=sys.stderr, flush=True)
+                  f"(limit {MAX_REL_ERR})", file=sys.stderr, flush=True)
     return 0 if ok else 1
 
 

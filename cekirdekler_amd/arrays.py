@@ -268,6 +268,11 @@ class ClArray:
         # kernels every device's slice of this array is copied into every
         # other device's replica (GPU↔GPU over xGMI, RCCL across ranks)
         self.gather_resident = False
+        # per cruncher (id): the split of the last compute this array took
+        # part in without the read-only hint — (compute id, elements per work
+        # item, elements per group, local range).  A device-resident array's
+        # replicas each hold the slice of that split (checkpoint.save).
+        self._split_log = {}
         self._registered = False
         self._disposed = False
 

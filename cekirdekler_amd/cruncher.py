@@ -567,6 +567,12 @@ class ClNumberCruncher:
         call = self._build_call(group, compute_id, kernels, global_range, local_range, global_offset,
                                 pipeline, pipeline_type, pipeline_blobs, specs, granularity)
         self._cores.compute(call)
+        if specs is None:
+            me = id(self)
+            for a in group.arrays:
+                if not a._ro:
+                    a._split_log[me] = (int(compute_id), int(a.elements_per_work_item), int(a.elements_per_group),
+                                        int(local_range))
         if self.performance_feed:
             self.performance_report(compute_id)
         if _RECORD_LOG is not None:

@@ -366,6 +366,7 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("serial", &Cores::serial)
       .def_readwrite("peer_reads", &Cores::peer_reads)
       .def_readwrite("device_spans", &Cores::device_spans)
+      .def_readwrite("zc_release", &Cores::zc_release)
       .def_readwrite("pipeline_writes_on_compute_stream", &Cores::pipeline_writes_on_compute_stream)
       .def_readwrite("pipeline_reads_on_main_stream", &Cores::pipeline_reads_on_main_stream)
       .def_readwrite("pipeline_writes_one_stream", &Cores::pipeline_writes_one_stream)
@@ -470,7 +471,9 @@ PYBIND11_MODULE(_cek, m) {
       .def_readonly("error", &PoolCompletion::error);
 
   py::class_<DevicePool, std::shared_ptr<DevicePool>>(m, "DevicePool")
-      .def(py::init<std::vector<std::shared_ptr<Cores>>, int>(), py::call_guard<py::gil_scoped_release>())
+      .def(py::init<std::vector<std::shared_ptr<Cores>>, int, int>(), py::arg("devices"), py::arg("max_in_flight"),
+           py::arg("policy") = 0, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("policy", &DevicePool::policy)
       .def("enqueue", &DevicePool::enqueue, py::call_guard<py::gil_scoped_release>())
       .def("finish", &DevicePool::finish, py::call_guard<py::gil_scoped_release>())
       .def("completions", &DevicePool::completions, py::arg("timeout_ms") = 0.0,

@@ -46,6 +46,7 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
   spans_.resize(workers_.size());
   if (const char* e = std::getenv("CEK_DEVICE_SPANS")) device_spans = std::string(e) != "0";
   if (const char* e = std::getenv("CEK_KERNEL_D2H")) set_kernel_d2h(std::string(e) != "0");
+  if (const char* e = std::getenv("CEK_ZC_RELEASE")) zc_release = std::string(e) != "0";
   time_scale_.assign(workers_.size(), 1.0);
   time_offset_.assign(workers_.size(), 0.0);
   enabled_.assign(workers_.size(), true);
@@ -138,29 +139,42 @@ void Cores::wait_gather(Worker& wk, hipStream_t s) {
 // device's slices from host memory, pushes its own slice to every other
 // replica (peer copies over xGMI), and records pushed_[g].  No host sync in
 // enqueue mode; otherwise the copies are complete when compute() returns.
-uint64_t Cores::issue_gather(const ComputeCall& c, const BalancerState& st, const std::vector<int>& arrays) {
+uint64_t Cores::issue_gather(const ComputeCall& c, const BalancerState& st, const std::vector<int>& arrays,
+                             const std::vector<std::vector<std::pair<long long, long long>>>* owned) {
   const int n = num_devices();
   std::vector<int> on;  // enabled local devices: they hold replicas
   for (int w = 0; w < n; ++w)
     if (enabled_[w]) on.push_back(w);
   if (on.size() < 2 || arrays.empty()) return 0;
+  // the work-item ranges each device holds fresh results for: its own slice
+  // of this call's split, or (after a failover) its slice plus the slices it
+  // recomputed for failed devices
+  std::vector<std::vector<std::pair<long long, long long>>> own(n);
+  for (int w : on) {
+    if (owned)
+      own[w] = (*owned)[w];
+    else
+      own[w].push_back({st.references[global_base_ + w], st.ranges[global_base_ + w]});
+  }
   uint64_t moved = 0;
   struct Piece {
     std::vector<char*> ptr;
-    std::vector<uint64_t> off, len;
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> seg;  // per worker: (byte offset, bytes)
   };
   std::vector<Piece> pcs(arrays.size());
   for (size_t i = 0; i < arrays.size(); ++i) {
     const ArraySpec& a = c.arrays[arrays[i]];
     Piece& p = pcs[i];
     p.ptr.assign(n, nullptr);
-    p.off.assign(n, 0);
-    p.len.assign(n, 0);
+    p.seg.assign(n, {});
     for (int w : on) {
-      uint64_t b, k;
-      a.slice(st.references[global_base_ + w], st.ranges[global_base_ + w], c.local_range, b, k);
-      p.off[w] = std::min<uint64_t>(b * a.elem_size, a.bytes);
-      p.len[w] = std::min<uint64_t>(k * a.elem_size, a.bytes - p.off[w]);
+      for (auto& r : own[w]) {
+        uint64_t b, k;
+        a.slice(r.first, r.second, c.local_range, b, k);
+        const uint64_t off = std::min<uint64_t>(b * a.elem_size, a.bytes);
+        const uint64_t len = std::min<uint64_t>(k * a.elem_size, a.bytes - off);
+        if (len) p.seg[w].push_back({off, len});
+      }
       workers_[w]->set_device();
       p.ptr[w] = static_cast<char*>(workers_[w]->buffer(a));
     }
@@ -178,21 +192,24 @@ uint64_t Cores::issue_gather(const ComputeCall& c, const BalancerState& st, cons
       const ArraySpec& a = c.arrays[arrays[i]];
       Piece& p = pcs[i];
       for (int s : on) {  // the CPU device's slices: host → this replica
-        if (workers_[s]->gpu() || !p.len[s]) continue;
-        CEK_HIP(hipMemcpyAsync(p.ptr[g] + p.off[s], static_cast<const char*>(a.host) + p.off[s], p.len[s],
-                               hipMemcpyHostToDevice, m));
-        moved += p.len[s];
+        if (workers_[s]->gpu()) continue;
+        for (auto& sg : p.seg[s]) {
+          CEK_HIP(hipMemcpyAsync(p.ptr[g] + sg.first, static_cast<const char*>(a.host) + sg.first, sg.second,
+                                 hipMemcpyHostToDevice, m));
+          moved += sg.second;
+        }
       }
-      if (!p.len[g]) continue;
-      for (int d : on) {  // this GPU's slice → every other replica
-        if (d == g || p.ptr[d] == p.ptr[g]) continue;
-        if (workers_[d]->gpu()) {
-          moved += d2d_copy(g, d, p.ptr[d] + p.off[g], p.ptr[g] + p.off[g], p.len[g], m);
-          log_op(global_base_ + d, "gather", 0, static_cast<long long>(p.off[g]), static_cast<long long>(p.len[g]),
-                 global_base_ + g);
-        } else {
-          CEK_HIP(hipMemcpyAsync(p.ptr[d] + p.off[g], p.ptr[g] + p.off[g], p.len[g], hipMemcpyDeviceToHost, m));
-          moved += p.len[g];
+      for (auto& sg : p.seg[g]) {
+        for (int d : on) {  // this GPU's slices → every other replica
+          if (d == g || p.ptr[d] == p.ptr[g]) continue;
+          if (workers_[d]->gpu()) {
+            moved += d2d_copy(g, d, p.ptr[d] + sg.first, p.ptr[g] + sg.first, sg.second, m);
+            log_op(global_base_ + d, "gather", 0, static_cast<long long>(sg.first), static_cast<long long>(sg.second),
+                   global_base_ + g);
+          } else {
+            CEK_HIP(hipMemcpyAsync(p.ptr[d] + sg.first, p.ptr[g] + sg.first, sg.second, hipMemcpyDeviceToHost, m));
+            moved += sg.second;
+          }
         }
       }
     }
@@ -370,6 +387,12 @@ void Cores::set_enqueue_mode(bool on) {
     enqueue_t0_ = now_ms();
   } else if (!on && enqueue_mode_) {
     close_batch_spans();
+    if (zc_release)  // one system-scope release per device for the whole batch (zero-copy stores)
+      for (auto& w : workers_)
+        if (w->gpu()) {
+          w->join_streams(w->main_stream());
+          w->system_release(w->main_stream());
+        }
     finish();
     double el = now_ms() - enqueue_t0_;
     auto it = state_.find(last_id_);
@@ -635,18 +658,22 @@ void Cores::copy_between(int src_dev, const ArraySpec& src, int dst_dev, const A
   }
   std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   if (ws.gpu() && wd.gpu()) {
-    // On the source's main stream after the destination's queued work; the
-    // destination's main stream then waits for the copy (no host sync in
-    // enqueue mode).
+    // On the source's main stream, after everything queued on either
+    // device (every stream: with async enqueue a compute may sit on a
+    // compute queue, still writing the source or reading the destination).
+    // Later work on ANY stream of either device waits for the copy through
+    // the gather-pending events (no host sync in enqueue mode).
     ws.set_device();
     void* sp = ws.buffer(src);
     wd.set_device();
     void* dp = wd.buffer(dst);
+    wd.join_streams(wd.main_stream());
     hipEvent_t before = gather_event(kdone_, dst_dev);
     CEK_HIP(hipEventRecord(before, wd.main_stream()));
     ws.set_device();
     hipStream_t s = ws.main_stream();
     wait_gather(ws, s);
+    ws.join_streams(s);
     CEK_HIP(hipStreamWaitEvent(s, before, 0));
     d2d_ = D2DCount();
     d2d_copy(src_dev, dst_dev, static_cast<char*>(dp), static_cast<const char*>(sp), bytes, s);
@@ -654,9 +681,11 @@ void Cores::copy_between(int src_dev, const ArraySpec& src, int dst_dev, const A
     CEK_HIP(hipEventRecord(after, s));
     wd.set_device();
     CEK_HIP(hipStreamWaitEvent(wd.main_stream(), after, 0));
+    gather_pending_ = true;  // compute streams of both devices wait on `after` too
     if (!enqueue_mode_) {
       ws.set_device();
       CEK_HIP(hipStreamSynchronize(s));
+      gather_pending_ = false;
     }
     return;
   }
@@ -1098,6 +1127,12 @@ bool Cores::collective(const ComputeCall& c) const {
   return std::any_of(c.arrays.begin(), c.arrays.end(), [](const ArraySpec& a) { return a.gather && !a.zc; });
 }
 
+// Kernels that may store into zero-copy (host) memory: close the device's
+// work with a system-scope release (the span events carry none).
+static bool writes_host_memory(const ComputeCall& c) {
+  return std::any_of(c.arrays.begin(), c.arrays.end(), [](const ArraySpec& a) { return a.zc && !a.ro; });
+}
+
 void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref, long long range,
                        uint64_t* h2d, uint64_t* d2h) {
   hipStream_t s = nullptr;
@@ -1187,6 +1222,7 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
     }
   }
   span_end(wk, s);
+  if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(s);
   if (fine_grained) wk.add_marker(s);
   if (!enqueue_mode_ && wk.gpu()) CEK_HIP(hipStreamSynchronize(s));
 }
@@ -1288,6 +1324,7 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
     }
   }
   span_end(wk, m);
+  if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(m);
   if (fine_grained) wk.add_marker(m);
   if (wk.gpu()) CEK_HIP(hipStreamSynchronize(m));
 }
@@ -1357,6 +1394,7 @@ void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long
     }
   }
   span_end(wk, m);
+  if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(m);
   if (fine_grained) wk.add_marker(m);
   if (wk.gpu()) CEK_HIP(hipStreamSynchronize(m));
 }
@@ -1429,11 +1467,32 @@ void Cores::compute(const ComputeCall& c) {
     if (enabled_[w]) survivor = w;
   if (survivor < 0) throw Error(std::string("every device failed: ") + f.what());
   auto& st = state_[c.compute_id];
+  // keep-resident arrays: the recomputed slices must reach every surviving
+  // replica too (the regular gather was skipped for this call)
+  std::vector<int> gather_idx;
+  for (size_t i = 0; i < c.arrays.size(); ++i)
+    if (c.arrays[i].gather && !c.arrays[i].zc) gather_idx.push_back(static_cast<int>(i));
+  const bool regather = !gather_idx.empty() && !comm_ && num_devices() > 1;
+  call_gathers_ = regather;  // the survivor records its kernels-done event
   for (int w : f.devices) {
     const int g = global_base_ + w;
     double ms = 0;
     uint64_t h = 0, d = 0;
-    run_device(survivor, c, st.references[g], st.ranges[g], false, &ms, &h, &d);
+    try {
+      run_device(survivor, c, st.references[g], st.ranges[g], false, &ms, &h, &d);
+    } catch (...) {
+      call_gathers_ = false;
+      throw;
+    }
+  }
+  call_gathers_ = false;
+  if (regather) {
+    std::vector<std::vector<std::pair<long long, long long>>> owned(num_devices());
+    for (int w = 0; w < num_devices(); ++w)
+      if (enabled_[w]) owned[w].push_back({st.references[global_base_ + w], st.ranges[global_base_ + w]});
+    for (int w : f.devices) owned[survivor].push_back({st.references[global_base_ + w], st.ranges[global_base_ + w]});
+    d2d_ = D2DCount();
+    last_record_.gather_bytes = issue_gather(c, st, gather_idx, &owned);
   }
   ++failovers_;
 }

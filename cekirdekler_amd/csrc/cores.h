@@ -396,7 +396,8 @@ class Cores {
   bool call_gathers_ = false;  // the running call gathers in-process
   hipEvent_t gather_event(std::vector<hipEvent_t>& v, int w);
   void wait_gather(Worker& wk, hipStream_t s);
-  uint64_t issue_gather(const ComputeCall& c, const struct BalancerState& st, const std::vector<int>& arrays);
+  uint64_t issue_gather(const ComputeCall& c, const struct BalancerState& st, const std::vector<int>& arrays,
+                        const std::vector<std::vector<std::pair<long long, long long>>>* owned = nullptr);
 
   std::vector<std::unique_ptr<Worker>> workers_;
   std::map<int, BalancerState> state_;
@@ -459,6 +460,10 @@ class Cores {
   std::vector<DevSpans> spans_;
  public:
   bool device_spans = true;  // CEK_DEVICE_SPANS=0: host wall clock instead
+  // a system-scope release marker after kernels that may store into
+  // zero-copy host memory (per compute in sync mode, once per batch when
+  // enqueue mode is left); CEK_ZC_RELEASE=0 turns it off
+  bool zc_release = true;
  private:
   bool spans_on() const;
   void close_batch_spans();

@@ -6,9 +6,10 @@
 
 namespace cek {
 
-DevicePool::DevicePool(std::vector<std::shared_ptr<Cores>> devices, int max_in_flight)
-    : devs_(std::move(devices)), max_in_flight_(std::max(1, std::min(16, max_in_flight))) {
+DevicePool::DevicePool(std::vector<std::shared_ptr<Cores>> devices, int max_in_flight, int policy)
+    : devs_(std::move(devices)), max_in_flight_(std::max(1, std::min(16, max_in_flight))), policy_(policy) {
   if (devs_.empty()) throw Error("device pool needs at least one device");
+  if (policy != 0 && policy != 1) throw Error("device pool policy must be 0 (compute at will) or 1 (round robin)");
   for (auto& d : devs_) {
     if (!d) throw Error("device pool: null cruncher");
     if (d->num_devices() != 1) throw Error("device pool: every entry must be a single-device cruncher");
@@ -34,8 +35,13 @@ void DevicePool::close() {
     closed_ = true;
   }
   work_cv_.notify_all();
-  for (auto& t : threads_)
-    if (t.joinable()) t.join();
+  for (auto& t : threads_) {
+    if (!t.joinable()) continue;
+    if (t.get_id() == std::this_thread::get_id())
+      t.detach();  // the last reference dropped on a consumer thread: it exits on return
+    else
+      t.join();
+  }
   threads_.clear();
 }
 
@@ -62,6 +68,16 @@ void DevicePool::enqueue(const std::vector<PoolTask>& tasks) {
           ++pools_[pid].total;
         }
       } else {
+        if (policy_ == 1 && !(it.task.type & kTaskSyncFirst)) {
+          // strict rotation; a select/serial group keeps its first task's device
+          if (rr_group_ >= 0) {
+            it.target = rr_group_;
+          } else {
+            it.target = static_cast<int>(rr_next_++ % num_devices());
+            if (t.type & (kTaskSelectBegin | kTaskSerialBegin)) rr_group_ = it.target;
+          }
+          if (t.type & (kTaskSelectEnd | kTaskSerialEnd)) rr_group_ = -1;
+        }
         queue_.push_back(std::move(it));
         ++outstanding_;
         ++pools_[pid].total;

@@ -38,6 +38,11 @@
 //     the device idle for the host turnaround between tasks);
 //   * each device keeps a smoothed marker-reach speed (markers retired per
 //     ms, 15-sample moving average).
+// Device policy (ClDevicePoolType, ClPipeline.cs:3792-3806): COMPUTE_AT_WILL
+// (0) — an idle device takes the next task; ROUND_ROBIN (1, a stub in the
+// reference, "better for identical devices") — task k of the stream goes to
+// device k mod D in strict rotation (a select/serial group as a whole takes
+// one rotation slot; barriers stay untargeted so every device stops at them).
 #pragma once
 #include <condition_variable>
 #include <deque>
@@ -77,7 +82,8 @@ class DevicePool {
  public:
   // One consumer thread per entry of `devices` (the same physical device may
   // appear several times, ClPipeline.cs:4337, as separate Cores).
-  DevicePool(std::vector<std::shared_ptr<Cores>> devices, int max_in_flight);
+  DevicePool(std::vector<std::shared_ptr<Cores>> devices, int max_in_flight, int policy = 0);
+  int policy() const { return policy_; }
   ~DevicePool();
 
   // Appends one task pool (FIFO order kept); broadcast tasks are duplicated
@@ -124,6 +130,9 @@ class DevicePool {
 
   std::vector<std::shared_ptr<Cores>> devs_;
   int max_in_flight_;
+  int policy_ = 0;
+  long long rr_next_ = 0;  // round robin: next device in the rotation
+  int rr_group_ = -1;      // round robin: device of the open select/serial group
   std::mutex mu_;
   std::condition_variable work_cv_, done_cv_, comp_cv_;
   std::deque<Item> queue_;

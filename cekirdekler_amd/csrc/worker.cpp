@@ -101,6 +101,9 @@ Worker::~Worker() {
     for (auto& dq : dyn_queues_) (void)hipFree(dq.second);
     for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
     for (auto e : events_) (void)hipEventDestroy(e);
+    for (auto e : join_ev_)
+      if (e) (void)hipEventDestroy(e);
+    if (sys_ev_) (void)hipEventDestroy(sys_ev_);
     if (main_) (void)hipStreamDestroy(main_);
     for (auto s : cq_)
       if (s) (void)hipStreamDestroy(s);
@@ -282,6 +285,32 @@ hipEvent_t Worker::event(int slot) {
     events_.push_back(e);
   }
   return events_[slot];
+}
+
+void Worker::join_streams(hipStream_t target) {
+  if (!gpu()) return;
+  set_device();
+  if (join_ev_.empty()) join_ev_.assign(32, nullptr);
+  auto join = [&](hipStream_t s) {
+    if (!s || s == target) return;
+    hipEvent_t& e = join_ev_[stream_slot(s)];
+    if (!e) CEK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    CEK_HIP(hipEventRecord(e, s));
+    CEK_HIP(hipStreamWaitEvent(target, e, 0));
+  };
+  join(main_);
+  for (auto s : cq_) join(s);
+  for (auto& h : pq_)
+    for (auto s : h) join(s);
+}
+
+void Worker::system_release(hipStream_t s) {
+  if (!gpu()) return;
+  if (!sys_ev_) {
+    set_device();
+    CEK_HIP(hipEventCreateWithFlags(&sys_ev_, hipEventDisableTiming));  // system fence kept
+  }
+  CEK_HIP(hipEventRecord(sys_ev_, s));
 }
 
 void Worker::sync_all() {

@@ -104,6 +104,16 @@ class Worker {
   int next_compute_queue();                 // round robin (Worker.cs:435-458)
   int queue_concurrency() const { return qconc_; }
   hipEvent_t event(int slot);               // pooled, timing disabled
+  // `target` waits for everything queued so far on every other stream of
+  // this worker (compute queues and pipeline streams): a copy issued next on
+  // `target` neither overtakes a kernel still reading its destination nor
+  // reads a source a kernel is still writing
+  void join_streams(hipStream_t target);
+  // A marker with a SYSTEM-scope release on s (a default-flag event): stores
+  // that kernels made straight into host memory (zero-copy arrays) are
+  // visible to the host once s is synchronised, independent of the
+  // fence-free timing events around them
+  void system_release(hipStream_t s);
   void sync_all();                          // finish every created stream
   void set_device() const;
 
@@ -193,6 +203,8 @@ class Worker {
   std::vector<hipStream_t> cq_;
   hipStream_t pq_[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
   std::vector<hipEvent_t> events_;
+  std::vector<hipEvent_t> join_ev_;  // one per stream slot (join_streams)
+  hipEvent_t sys_ev_ = nullptr;      // system_release
   std::atomic<int> rr_{0};
 
   // markers: one 64-bit word per stream slot in pinned host memory

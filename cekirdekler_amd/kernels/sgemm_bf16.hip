@@ -69,10 +69,10 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   const long long u = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
   const int S = SK ? max(dims[4], 1) : 1;
   const long long t = u / S;
-  // XCH 2 / 3: the K-split of u odd (the helper) takes K/64/2 − dims[5]
-  // K-tiles from the start, u even (the owner) the rest (dims[5] = 0: halves)
-  const int kt_all = dims[2] / 64, shift = XCH >= 2 ? dims[5] : 0;
-  const int ks = XCH >= 2 ? ((u & 1) ? 0 : kt_all / 2 - shift) : SK ? (int)(u % S) * (kt_all / S) : 0;
+  // XCH 3: the K-split of u odd (the helper) takes K/64/2 − dims[5] K-tiles
+  // from the start, u even (the owner) the rest
+  const int kt_all = dims[2] / 64, shift = XCH == 3 ? dims[5] : 0;
+  int ks = XCH == 3 ? ((u & 1) ? 0 : kt_all / 2 - shift) : SK ? (int)(u % S) * (kt_all / S) : 0;
   // Grouped tile order (dims[3] = GM row panels per group, tiles walk down
   // the group's rows first): the 32 work-groups an XCD runs at once cover a
   // GM × (32/GM) block of C, so A and B K-slices are shared through that
@@ -137,14 +137,30 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = XCH >= 2 ? ((u & 1) ? kt_all / 2 - shift : kt_all / 2 + shift) : K / BK / S;
+  int nk = XCH == 3 ? ((u & 1) ? kt_all / 2 - shift : kt_all / 2 + shift) : K / BK / S;
   unsigned my_xcc = 0;
-  if constexpr (XCH == 2 || XCH == 3) {
-    // publish this work-group's XCD for the partner split (flags[4t + 2 + s])
+  // XCH 3 flags per tile: [4t] hand-over state (0 open, 1 partial ready, 2
+  // claimed by the owner), [4t + 2] owner's XCD + 1, [4t + 3] helper's XCD + 1;
+  // the word after the last tile counts owner fall-backs.
+  bool claimed = false;  // owner: it will compute the helper's K-range itself
+  if constexpr (XCH == 3) {
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(my_xcc));
     my_xcc &= 15u;
     if (tid == 0)
       __hip_atomic_store(&tile_cnt[4 * t + 2 + (u & 1)], (int)my_xcc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!(u & 1) && dims[7] < 0) {
+      // debug (dims[7] < 0): the owner claims the hand-over before its main
+      // loop, so the fall-back pass runs (tests of the co-residency-safe path)
+      int* st = reinterpret_cast<int*>(smem);
+      if (tid == 0) {
+        int open = 0;
+        st[0] = __hip_atomic_compare_exchange_strong(&tile_cnt[4 * t], &open, 2, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      claimed = st[0] != 0;
+      __syncthreads();
+    }
   }
   if constexpr (MODE == 0) {
     stage(0, 0);
@@ -408,28 +424,93 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     if (!g1) bar();  // equal barrier counts for both groups
     CEK_TS(2);
   }
+  if constexpr (XCH == 3) {
+    if (!(u & 1)) {
+      // Owner, main loop done: is the helper's partial there?  A helper that
+      // is not co-resident (the GPU shared with other kernels) may not even
+      // have started.  After a bounded wait the owner CLAIMS the hand-over
+      // (one CAS against the helper's) and multiplies the helper's K-range
+      // itself, so C is correct whatever the residency; a late helper finds
+      // the claim and leaves.  Exactly one side's CAS wins, and the last one
+      // to touch the state word re-arms it (0) for the next launch.
+      __syncthreads();  // every wave is done with LDS before it holds the flags
+      int* st = reinterpret_cast<int*>(smem);
+      if (tid == 0) {
+        int v = claimed ? 2 : 0;
+        if (!claimed) {
+          const int limit = dims[7] > 0 ? dims[7] : (1 << 16);
+          for (int spins = 0; (v = __hip_atomic_load(&tile_cnt[4 * t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0;) {
+            if (++spins > limit) {
+              int open = 0;
+              if (__hip_atomic_compare_exchange_strong(&tile_cnt[4 * t], &open, 2, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT))
+                v = 2;
+              else
+                v = open;  // the helper got there first: 1
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+        }
+        int same = 0;
+        if (v == 2) {
+          __hip_atomic_fetch_add(&tile_cnt[(size_t)4 * ntm * ntn], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {  // ready: the helper published its XCD before its partial
+          const int hx = __hip_atomic_load(&tile_cnt[4 * t + 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          tile_cnt[4 * t + 3] = 0;
+          tile_cnt[4 * t] = 0;  // re-arm: the owner is the last to touch the state
+          same = hx == (int)my_xcc + 1;
+        }
+        tile_cnt[4 * t + 2] = 0;  // this launch's XCD word retires with the owner
+        st[0] = v;
+        st[1] = same;
+      }
+      __syncthreads();
+      claimed = st[0] == 2;
+      const bool same = st[1] != 0;
+      __syncthreads();  // st[] read by every wave before LDS is restaged
+      if (claimed) {
+        // fall-back: the helper's K-tiles [0, K/64/2 - shift), one LDS stage
+        // in flight, the first half of the waves staging (rare path: kept
+        // simple, outside the tuned loop)
+        const bool g1 = wave >= NWAVES / 2;
+        ks = 0;
+        nk = kt_all / 2 - shift;
+        if (!g1) stage(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int kt = 0; kt < nk; ++kt) {
+          const int cur = kt & 1;
+          if (!g1 && kt + 1 < nk) stage(cur ^ 1, kt + 1);
+          const char* base = smem + cur * STAGE;
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            bf16x8 a[FM], b[FN];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) b[j] = *(const bf16x8*)(base + b_off[s2] + j * 2048);
+#pragma unroll
+            for (int i = 0; i < FM; ++i) a[i] = *(const bf16x8*)(base + a_off[s2] + i * 2048);
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+              for (int j = 0; j < FN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+        }
+      } else if (!same) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+    }
+  }
 
   // Epilogue: acc[i][j][r] is C(row = wr·16FM + i·16 + fq·4 + r, col = wc·16FN + j·16 + fr)
   if constexpr (XCH == 3) {
     // Uneven split-K = 2, one-way hand-over: the helper ran `shift` K-tiles
     // fewer than half, so it stores its whole partial tile (fragment order,
     // 1 KiB per wave instruction) while the owner still multiplies; the owner
-    // then finds the partial ready, adds it and stores the whole C tile.  The
-    // end of the launch carries one read-back (no write) and the C stores of
-    // half the CUs; the other half's partial stores overlapped the main loop.
-    // Flags per tile: [4t] ready, [4t + 2] owner's XCD, [4t + 3] helper's XCD.
-    int* err = &tile_cnt[(size_t)4 * ntm * ntn];
-    auto spin = [&](int* w) -> int {
-      int v, spins = 0;
-      while ((v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1 << 21)) {
-          __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          return 0;
-        }
-      }
-      return v;
-    };
+    // (pass loop above) found it ready, adds it and stores the whole C tile.
     f32x4* wt = reinterpret_cast<f32x4*>(W + (size_t)t * BM * BN);
     if (u & 1) {  // helper: publish the partial and leave
 #pragma unroll
@@ -440,30 +521,25 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       __syncthreads();
       CEK_TS(3);
       if (tid == 0) {
-        // the owner published its XCD when it started (it is dispatched first)
-        const int px = spin(&tile_cnt[4 * t + 2]);
-        tile_cnt[4 * t + 2] = 0;  // re-arm
+        // the owner's XCD word (0 once the owner has finished or before it
+        // started: then release through the L2 write-back to be safe)
+        const int px = __hip_atomic_load(&tile_cnt[4 * t + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (px != (int)my_xcc + 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_store(&tile_cnt[4 * t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int open = 0;
+        if (!__hip_atomic_compare_exchange_strong(&tile_cnt[4 * t], &open, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)) {
+          // the owner claimed the hand-over and computed our K-range itself:
+          // this work-group is the last to touch the tile's words
+          tile_cnt[4 * t] = 0;
+          tile_cnt[4 * t + 3] = 0;
+        }
       }
       CEK_TS(4);
       return;
     }
-    __syncthreads();  // every wave is done with LDS before it holds the flags
-    int* ok = reinterpret_cast<int*>(smem);
-    if (tid == 0) {
-      const int hx = spin(&tile_cnt[4 * t + 3]);
-      tile_cnt[4 * t + 3] = 0;
-      int good = hx != 0;
-      if (good) good = spin(&tile_cnt[4 * t]) != 0;
-      tile_cnt[4 * t] = 0;
-      ok[0] = good;
-      ok[1] = hx == (int)my_xcc + 1;
-    }
-    __syncthreads();
     CEK_TS(3);
-    if (!ok[1]) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (ok[0]) {
+    if (!claimed) {
       f32x4 part[FM][FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -475,81 +551,6 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
         for (int j = 0; j < FN; ++j) acc[i][j] += part[i][j];
     }
     CEK_TS(4);
-  } else if constexpr (XCH > 0) {
-    // Split-K = 2 with exchanged halves (WM = 2): split s finishes row half
-    // s of the tile (waves wr == s) and hands its partial of the other half
-    // to the partner split.  Both work-groups of a tile end at about the
-    // same time, so the reduction tail is exposed; exchanging halves moves
-    // 128 KiB out + 128 KiB in + 128 KiB of C per CU instead of the 256 KiB
-    // ×3 of a last-arriver reduction.  Partials use a fragment-native layout
-    // (16 B per lane, 1 KiB per wave instruction).
-    static_assert(WM == 2, "exchanged halves need two wave rows");
-    const int s = (int)(u & 1);
-    constexpr int HALF = BM / 2 * BN;
-    f32x4* wh = reinterpret_cast<f32x4*>(W + (size_t)t * BM * BN + (size_t)wr * HALF);
-    if (wr != s) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) wh[((wc * FM + i) * FN + j) * 64 + lane] = acc[i][j];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* ok = reinterpret_cast<int*>(smem);
-    // XCH 1: flags[2t + h] = 1 once half h of tile t is in W (agent-scope
-    // release/acquire: an L2 write-back and invalidate per hand-over).
-    // XCH 2: flags[4t + h] plus each split's XCD in flags[4t + 2 + s]; two
-    // work-groups on one XCD share its L2, so the hand-over needs no L2
-    // write-back (the partial is in L2 once the stores are acknowledged, and
-    // no L1 holds those lines); across XCDs it falls back to XCH 1's fences.
-    // The partner has always stored (and published its XCD) before it waits,
-    // so neither side can wait on the other's wait; it is at most 8 dispatch
-    // slots away (XCD remap).  Every spin is bounded: a timeout counts in the
-    // last flag word (checked by the host) instead of hanging the GPU.
-    constexpr int FPT = XCH == 2 ? 4 : 2;  // flag words per tile
-    int* err = &tile_cnt[(size_t)FPT * ntm * ntn];
-    auto spin = [&](int* w) -> int {
-      int v, spins = 0;
-      while ((v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1 << 21)) {
-          __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          return 0;
-        }
-      }
-      return v;
-    };
-    if (tid == 0) {
-      bool same = false;
-      int good = 1;
-      if constexpr (XCH == 2) {
-        const int px = spin(&tile_cnt[4 * t + 2 + (1 - s)]);
-        tile_cnt[4 * t + 2 + (1 - s)] = 0;  // re-arm the partner's word
-        same = px == (int)my_xcc + 1;
-        good = px != 0;
-      }
-      if (!same) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __hip_atomic_store(&tile_cnt[FPT * t + (1 - s)], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (good) good = spin(&tile_cnt[FPT * t + s]) != 0;
-      tile_cnt[FPT * t + s] = 0;  // re-arm for the next call
-      ok[0] = good;
-      ok[1] = same;
-    }
-    __syncthreads();
-    if (wr != s) return;
-    if (!ok[1]) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (ok[0]) {
-      const f32x4* rh = reinterpret_cast<const f32x4*>(W + (size_t)t * BM * BN + (size_t)s * HALF);
-      f32x4 part[FM][FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) part[i][j] = rh[((wc * FM + i) * FN + j) * 64 + lane];
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] += part[i][j];
-    }
   } else if constexpr (SK) {
     if (S > 1) {
       // Every split stores its partial tile; the last of the S to arrive
@@ -633,15 +634,6 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sk(
     const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
   __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
   gemm_tile<2, 4, 8, 4, 4, true>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
-}
-
-// same, with the hand-over through a shared L2 when both splits of a tile run
-// on one XCD (flags: 4 per tile + 1); the 8-GPU slice kernel (1024 rows of
-// 8192²: 128 tiles of 256² for 256 CUs)
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sy(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
-  gemm_tile<2, 4, 8, 4, 4, true, 2>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
 }
 
 // uneven split-K = 2 with a one-way hand-over (dims[5] = the helper's

@@ -27,11 +27,11 @@ TILES = {
     # balanced-DMA ping-pong (G0 stages A, G1 stages Bt two K-tiles ahead):
     # the full-problem tile (1.47-1.50 PF at 8192³)
     "256x256pb": (256, 256, 512, "cek_sgemm_bf16_256x256pb"),
-    # the same with split-K = 2, the two splits exchanging row halves through
-    # their XCD's L2: the 8-GPU slice (1024 rows of 8192², 128 tiles)
-    "256x256pby": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sy"),
     # uneven split-K = 2 (the helper runs `exchange_shift` K-tiles fewer and
-    # hands its whole partial to the owner while the owner still multiplies)
+    # hands its whole partial to the owner while the owner still multiplies):
+    # the 8-GPU slice (1024 rows of 8192², 128 tiles for 256 CUs).  The
+    # hand-over is co-residency-safe: an owner whose helper is late claims
+    # the hand-over and multiplies the helper's K-range itself.
     "256x256pbw": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sw"),
     # 256×128 fallbacks (twice the tiles): even chunk-split DMA, three stages / balanced DMA
     "256x128pe": (256, 128, 512, "cek_sgemm_bf16_256x128pe"),
@@ -50,7 +50,7 @@ GEMM_LIBS = ("sgemm_bf16",)
 # each): the kernels store a C tile in fragment order (one dwordx4 per lane
 # per fragment), which tile_to_rows / rows_to_tile convert.
 TILE_WAVES = {
-    "256x256pb": (2, 4, 8, 4), "256x256pby": (2, 4, 8, 4), "256x256pbw": (2, 4, 8, 4), "256x256": (2, 4, 8, 4), "256x256pp": (2, 4, 8, 4),
+    "256x256pb": (2, 4, 8, 4), "256x256pbw": (2, 4, 8, 4), "256x256": (2, 4, 8, 4), "256x256pp": (2, 4, 8, 4),
     "256x128pe": (4, 2, 4, 4), "256x128pb": (4, 2, 4, 4), "128x128": (2, 2, 4, 4),
 }
 
@@ -94,12 +94,11 @@ F32_TILES = {
 
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
 SPLIT_K_TILES = {"256x256pp", "256x256pb"}
-# tiles whose kernel always runs two K-splits that exchange row halves
-EXCHANGE_TILES = {"256x256pby": 4, "256x256pbw": 4}  # flag words per tile
-# K-tile deficit of the split that finishes first (dims[5]; exchange tiles):
-# pby hands its give-half over early and waits for the partner's, pbw hands
-# its whole partial over and leaves
-EXCHANGE_SHIFT = {"256x256pby": 0, "256x256pbw": 4}
+# tiles whose kernel always runs two K-splits with a hand-over (flag words per tile)
+EXCHANGE_TILES = {"256x256pbw": 4}
+# K-tile deficit of the helper split (dims[5]): it hands its whole partial
+# over and leaves while the owner still multiplies
+EXCHANGE_SHIFT = {"256x256pbw": 4}
 
 
 def to_bf16_bits(x: np.ndarray) -> np.ndarray:
@@ -140,7 +139,7 @@ class GemmBf16:
     def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256",
                  cruncher: ClNumberCruncher | None = None, fill: str = "random", seed: int = 0,
                  group_m: int = 4, split_k: int = 1, wave_granularity: bool | None = None,
-                 exchange_shift: int | None = None):
+                 exchange_shift: int | None = None, handover_spin_limit: int = 0):
         BM, BN, L, kname = TILES[tile]
         if M % BM or N % BN or K % 64:
             raise ValueError(f"M%{BM}, N%{BN} and K%64 must be 0 (got {M},{N},{K})")
@@ -167,7 +166,9 @@ class GemmBf16:
         self.global_range = self.tiles * self.split_k * L
         self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library(*GEMM_LIBS))
         self.group_m = group_m
-        self.dims = ClArray(np.array([M, N, K, group_m, self.split_k, shift, 0, 0], np.int32))
+        # dims[7]: the owner's wait for the helper's partial, in polls (0: the
+        # kernel default, 65536; < 0: claim at once — forces the fall-back)
+        self.dims = ClArray(np.array([M, N, K, group_m, self.split_k, shift, 0, int(handover_spin_limit)], np.int32))
         self.dims.write = False
         self.A = ClArray(M * K, "bfloat16")
         self.B = ClArray(N * K, "bfloat16")
@@ -334,9 +335,12 @@ class GemmBf16:
         """One C tile as stored (``BM·BN`` floats) → row-major ``[BM][BN]``."""
         return flat.reshape(self.BM, self.BN) if self.geom is None else tile_to_rows(flat, self.geom)
 
-    def spin_timeouts(self) -> int:
-        """Exchange tiles only: how many work-groups gave up waiting for their
-        partner's half (summed over devices; nonzero means a wrong result)."""
+    def handover_fallbacks(self) -> int:
+        """Exchange tiles only: how many owners found their helper's partial
+        missing after the bounded wait and multiplied the helper's K-range
+        themselves (summed over devices and calls).  C is correct either way;
+        a nonzero count means the GPU was shared (helpers not co-resident)
+        and those tiles ran at half speed."""
         if not self.exchange:
             return 0
         total = 0
@@ -344,6 +348,8 @@ class GemmBf16:
             self.cr.download(self.counters, dev)
             total += int(self.counters.array[-1])
         return total
+
+    spin_timeouts = handover_fallbacks  # round-3 name
 
     def verify(self, compute_id: int = 1, tiles_per_device: int = 8, seed: int = 1,
                host: bool = False) -> float:

@@ -45,7 +45,11 @@ class ClTaskType(enum.IntFlag):
 
 
 class ClDevicePoolType(enum.IntEnum):
+    """ClPipeline.cs:3792-3806: an idle device takes the next task (at will),
+    or tasks go to the devices in strict rotation (round robin: the
+    reference's stub "better for identical devices", e.g. 8 MI355X)."""
     DEVICE_COMPUTE_AT_WILL = 0
+    DEVICE_ROUND_ROBIN = 1
 
 
 class ClTask:
@@ -226,7 +230,7 @@ class ClDevicePool:
                 counts[i] = c
             self._native.close()
         self._counts_base = counts
-        self._native = cek.DevicePool([c.cores for c in self.crunchers], self.max_queues)
+        self._native = cek.DevicePool([c.cores for c in self.crunchers], self.max_queues, int(self.pool_type))
         if self._dispatcher is None:
             self._dispatcher = threading.Thread(target=self._dispatch_loop, daemon=True)
             self._dispatcher.start()

@@ -14,6 +14,16 @@ the per-compute-id range/offset tables + timing history (Cores.cs:130-135,
 
 so a resumed cruncher re-balances from where it stopped instead of from the
 equal split.
+
+Device-resident arrays (``write=False``) are saved as the devices hold them:
+each device's replica is authoritative only for the slice of the split it
+computed (Worker.cs:1349-1352 — the reference's slice ownership; the split is
+the per-compute-id state of Cores.cs:130-135).  ``save`` assembles every such
+array from each device's own slice, by the split of the last compute the
+array took part in (``ClArray._split_log``; override per array with
+``compute_ids``).  A keep-resident (``gather_resident``) array is whole in
+any replica.  In a :class:`DistributedCruncher` job every rank contributes
+its devices' slices and rank 0 writes the one file.
 """
 from __future__ import annotations
 
@@ -29,39 +39,129 @@ _ARRAY_TAG = 0x41525200  # "ARR\0"
 _STATE_TAG = 0x53544100  # "STA\0"
 
 
-def save(path: str, arrays: Dict[str, ClArray], cruncher=None, download: bool = True) -> int:
+def _owned_slices(a: ClArray, cruncher, compute_id: Optional[int] = None) -> Optional[List[tuple]]:
+    """(local device, first element, end element) of every slice this
+    process's devices own in ``a``, or None when the array's device replicas
+    are whole (gathered) or it never took part in a compute of ``cruncher``."""
+    if a.gather_resident:
+        return None
+    log = a._split_log.get(id(cruncher))
+    if log is None and compute_id is None:
+        return None
+    cid, epw, epg, L = log if log is not None else (compute_id, a.elements_per_work_item, a.elements_per_group, 0)
+    if compute_id is not None:
+        cid = compute_id
+    cores = cruncher.cores
+    ranges, refs = cores.ranges(cid), cores.references(cid)
+    if not ranges:
+        return None
+    L = L or 1
+    out = []
+    for dev in range(cores.num_devices):
+        g = cores.global_base + dev
+        if epg > 0:
+            lo, n = refs[g] // L * epg, ranges[g] // L * epg
+        else:
+            lo, n = refs[g] * epw, ranges[g] * epw
+        lo, hi = min(lo, a.N), min(lo + n, a.N)
+        if hi > lo:
+            out.append((dev, lo, hi))
+    return out
+
+
+def _assemble(a: ClArray, cruncher, compute_id: Optional[int]) -> List[tuple]:
+    """Fill ``a``'s host copy from the device replicas: device 0's whole
+    replica, then every other local device's own slice from its replica.
+    Returns the (first, end) element ranges this process owns."""
+    cores = cruncher.cores
+    owned = _owned_slices(a, cruncher, compute_id)
+    cruncher.download(a, 0)
+    if not owned:
+        return [(0, a.N)]
+    host = a.array
+    if any(dev != 0 for dev, _, _ in owned):
+        base = host.copy()
+        for dev in range(1, cores.num_devices):
+            mine = [(lo, hi) for d, lo, hi in owned if d == dev]
+            if not mine:
+                continue
+            cruncher.download(a, dev)
+            for lo, hi in mine:
+                base[lo:hi] = host[lo:hi]
+        host[:] = base
+    return [(lo, hi) for _, lo, hi in owned]
+
+
+def save(path: str, arrays: Dict[str, ClArray], cruncher=None, download: bool = True,
+         compute_ids: Optional[Dict[str, int]] = None) -> int:
     """Write arrays (+ the cruncher's balancer state) to ``path``.  With
-    ``download`` the device replicas of device 0 are read back first for
-    arrays that are device-resident (``write=False``).  Returns bytes."""
-    nb = NetworkBuffer(CHECKPOINT)
+    ``download``, device-resident arrays (``write=False``) are assembled from
+    the devices first: each device contributes the slice it owns under the
+    split of the array's last compute (``compute_ids`` names another compute
+    id per array).  In a distributed job every rank must call ``save``; rank
+    0 gathers the other ranks' slices and writes the file.  Returns bytes
+    written (on every rank)."""
+    compute_ids = compute_ids or {}
     names = list(arrays)
-    nb.add_string("\n".join(names), _STATE_TAG - 1)
-    for i, name in enumerate(names):
+    ctx = getattr(cruncher, "ctx", None)
+    dist_job = ctx is not None and ctx.is_distributed
+    pieces: Dict[str, list] = {}
+    for name in names:
         a = arrays[name]
-        if download and cruncher is not None and not a.write:
-            cruncher.download(a, 0)
-        nb.add_array(a.array, _ARRAY_TAG + i)
-    if cruncher is not None:
-        c = cruncher.cores
-        for cid in c.compute_ids():
-            rng = np.asarray(c.ranges(cid), np.int64)
-            hist = np.asarray(c.history(cid), np.float64)
-            nb.add_ints([cid, len(rng), hist.shape[0]], _STATE_TAG)
-            nb.add_array(rng, _STATE_TAG + 1)
-            nb.add_doubles(c.benchmarks(cid), _STATE_TAG + 2)
-            nb.add_doubles(hist.reshape(-1), _STATE_TAG + 3)
-    data = nb.to_bytes()
-    tmp = path + ".tmp"
-    with open(tmp, "wb") as f:
-        f.write(data)
-    os.replace(tmp, path)
-    return len(data)
+        if download and cruncher is not None and not a.write and not a.zero_copy:
+            owned = _assemble(a, cruncher, compute_ids.get(name))
+            if dist_job and _owned_slices(a, cruncher, compute_ids.get(name)) is not None:
+                pieces[name] = [(lo, hi, a.array[lo:hi].tobytes()) for lo, hi in owned]
+    if dist_job:
+        import torch.distributed as dist
+
+        got = [None] * ctx.world if ctx.rank == 0 else None
+        dist.gather_object(pieces, got, dst=0)
+        if ctx.rank == 0:
+            for r, part in enumerate(got):
+                if r == 0:
+                    continue
+                for name, segs in part.items():
+                    host = arrays[name].array
+                    for lo, hi, raw in segs:
+                        host[lo:hi] = np.frombuffer(raw, dtype=host.dtype, count=hi - lo)
+    nbytes = 0
+    if not dist_job or ctx.rank == 0:
+        nb = NetworkBuffer(CHECKPOINT)
+        nb.add_string("\n".join(names), _STATE_TAG - 1)
+        for i, name in enumerate(names):
+            nb.add_array(arrays[name].array, _ARRAY_TAG + i)
+        if cruncher is not None:
+            c = cruncher.cores
+            for cid in c.compute_ids():
+                rng = np.asarray(c.ranges(cid), np.int64)
+                hist = np.asarray(c.history(cid), np.float64)
+                nb.add_ints([cid, len(rng), hist.shape[0]], _STATE_TAG)
+                nb.add_array(rng, _STATE_TAG + 1)
+                nb.add_doubles(c.benchmarks(cid), _STATE_TAG + 2)
+                nb.add_doubles(hist.reshape(-1), _STATE_TAG + 3)
+        data = nb.to_bytes()
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as f:
+            f.write(data)
+        os.replace(tmp, path)
+        nbytes = len(data)
+    if dist_job:
+        import torch.distributed as dist
+
+        box = [nbytes]
+        dist.broadcast_object_list(box, src=0)
+        nbytes = int(box[0])
+    return nbytes
 
 
 def load(path: str, arrays: Optional[Dict[str, ClArray]] = None, cruncher=None) -> Dict[str, np.ndarray]:
-    """Read a checkpoint.  Arrays given in ``arrays`` are filled in place
-    (and re-uploaded on their next compute); balancer state is restored into
-    ``cruncher``.  Returns every array by name."""
+    """Read a checkpoint.  Arrays given in ``arrays`` are filled in place;
+    with a ``cruncher`` they are also uploaded to every local device replica
+    (device-resident arrays resume where they stopped, their flags
+    untouched), without one they are re-uploaded on their next compute.
+    Balancer state is restored into ``cruncher``.  Returns every array by
+    name.  In a distributed job every rank loads the same file."""
     with open(path, "rb") as f:
         data = f.read()
     cmd, recs = NetworkBuffer.parse(data)
@@ -77,7 +177,11 @@ def load(path: str, arrays: Optional[Dict[str, ClArray]] = None, cruncher=None) 
         if arrays is not None and name in arrays:
             dst = arrays[name].array
             dst[:] = r.data.view(dst.dtype) if r.data.dtype.itemsize == dst.dtype.itemsize else r.data
-            arrays[name].read = True
+            if cruncher is not None and not arrays[name].zero_copy:
+                for dev in range(cruncher.cores.num_devices):
+                    cruncher.upload(arrays[name], dev)
+            else:
+                arrays[name].read = True
     while i + 3 < len(recs) + 1 and i < len(recs):
         head = recs[i]
         if head.type != TYPE_INT or head.hash != _STATE_TAG:

@@ -162,3 +162,66 @@ def test_zero_range_rank_joins_gather():
         assert out[0][0] == [512, 0], out  # the empty-range case really happened
         assert all(ok for (_, ok) in out), out  # every rank's host replica holds every slice
     assert [o[0] for o in res[0][0]] == [o[0] for o in res[1][0]]
+
+
+CK_SRC = """
+__global__ void fill(float* y) { long long i = get_global_id(0); y[i] = 3.0f * (float)i + 1.0f; }
+"""
+
+
+def _ckpt_worker(rank, world, port, path, q):
+    """VERDICT r3 #4 across ranks: each rank's device holds only its own
+    slices of a write=False array; checkpoint.save gathers them to rank 0,
+    which writes one file every rank can load."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), CEK_CPU_THREADS="2")
+    import cekirdekler_amd as ck
+    from cekirdekler_amd.parallel.distributed import DistributedCruncher, init_distributed
+    from cekirdekler_amd.utils import checkpoint
+
+    ctx = init_distributed("gloo")
+    cr = DistributedCruncher(CK_SRC, ctx=ctx, devices=ck.ClPlatforms.all().cpus(True))
+    if rank == 1:
+        cr.set_time_scale(0, 2.5)  # uneven split
+    n = 64 * 256
+    y = ck.ClArray(np.zeros(n, np.float32))
+    y.read = False
+    y.write = False
+    for _ in range(4):
+        y.compute(cr, 1, "fill", n, 64)
+    ranges = cr.ranges(1)
+    nbytes = checkpoint.save(path, {"y": y}, cr)
+    import torch.distributed as dist
+    dist.barrier()
+    y2 = ck.ClArray(np.zeros(n, np.float32))
+    checkpoint.load(path, {"y": y2})
+    ok = bool(np.array_equal(y2.array, 3.0 * np.arange(n, dtype=np.float32) + 1.0))
+    q.put((rank, ranges, nbytes, ok))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_checkpoint_gathers_rank_slices(tmp_path):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    path = str(tmp_path / "dist.cek")
+    procs = [ctx.Process(target=_ckpt_worker, args=(r, world, port, path, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, ranges, nbytes, ok = q.get(timeout=180)
+            res[r] = (ranges, nbytes, ok)
+    finally:
+        for p in procs:
+            p.join(60)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    assert res[0][0][0] != res[0][0][1]  # uneven
+    assert res[0][1] == res[1][1] > 0
+    assert res[0][2] and res[1][2]

@@ -545,3 +545,54 @@ def test_device_pipeline_stop_host_device_transmission(gpu):
         dp.feed()
     assert float(dp.output_buffer(out).array[0]) == 8.0
     dp.dispose()
+
+
+PART_SRC = """
+__global__ void fill(const int* it, float* y) {
+  long long i = get_global_id(0);
+  y[i] = (float)(i % 1000) * 0.5f + (float)it[0];
+}
+"""
+
+
+@pytest.mark.parametrize("ndev", [2, 4])
+def test_checkpoint_partitioned_device_state(gpu, tmp_path, ndev):
+    """a device-resident array (write=False, no gather) is
+    held by slices — each device's replica is right only for its own range.
+    save() assembles it from every device's slice under an uneven split, and
+    load() puts the assembled array back into every replica."""
+    from cekirdekler_amd.utils import checkpoint
+
+    devs = gpu[0]
+    for _ in range(ndev - 1):
+        devs = devs + gpu[0]
+    cr = ck.ClNumberCruncher(devs, PART_SRC)
+    cr.set_time_scale(ndev - 1, 2.5)  # uneven split
+    n = 1 << 16
+    it = ck.ClArray(np.zeros(1, np.int32))
+    y = ck.ClArray(np.full(n, -1.0, np.float32))
+    it.write = False
+    y.read = False
+    y.write = False
+    for k in range(5):
+        it.array[0] = k
+        it.next_param(y).compute(cr, 7, "fill", n, 256)
+    ranges = cr.ranges(7)
+    assert len(set(ranges)) > 1, ranges
+    want = (np.arange(n) % 1000).astype(np.float32) * 0.5 + 4.0
+    cr.download(y, 0)
+    assert not np.array_equal(y.array, want)  # device 0's replica alone is not the array
+    path = str(tmp_path / "part.cek")
+    checkpoint.save(path, {"y": y}, cr)
+    y2 = ck.ClArray(np.zeros(n, np.float32))
+    checkpoint.load(path, {"y": y2})
+    np.testing.assert_array_equal(y2.array, want)
+    # resume: load into the same cruncher's replicas; a download of every
+    # device now gives the whole array
+    y.array[:] = 0
+    checkpoint.load(path, {"y": y}, cr)
+    for d in range(ndev):
+        y.array[:] = 0
+        cr.download(y, d)
+        np.testing.assert_array_equal(y.array, want)
+    cr.dispose()

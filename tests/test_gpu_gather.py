@@ -243,3 +243,78 @@ def test_graph_exit_keeps_the_user_exception():
             1 / 0
     assert not cr.cores.capturing
     cr.dispose()
+
+
+def test_failover_regathers_recomputed_slice():
+    """when a device fails, a survivor recomputes its
+    slice; with a keep-resident array that slice must still reach every
+    surviving replica, or later steps read stale values."""
+    cr = ck.ClNumberCruncher(_gpus(3), SRC)
+    cr.auto_failover = True
+    n = 3 * (1 << 14)
+    x0 = np.random.default_rng(7).standard_normal(n).astype(np.float32)
+    a = ck.ClArray(x0.copy())
+    b = ck.ClArray(np.zeros(n, np.float32))
+    for arr in (a, b):
+        arr.write = False
+    ref = x0.copy()
+    src, dst = a, b
+    for it in range(6):
+        if it == 2:
+            cr.cores.inject_failure(2, 1)  # device 2 fails once, is dropped
+        src.read = it == 0
+        dst.read = False
+        src.gather_resident, dst.gather_resident = False, True
+        src.next_param(dst).compute(cr, 5, "hop", n, 64)
+        ref = _step(ref)
+        src, dst = dst, src
+    assert cr.cores.failovers == 1
+    assert not cr.device_enabled(2)
+    for d in (0, 1):  # both survivors hold the whole, current result
+        src.array[:] = 0
+        cr.download(src, d)
+        np.testing.assert_allclose(src.array, ref, rtol=1e-6, atol=1e-6)
+    cr.dispose()
+
+
+COPY_SRC = """
+__global__ void slowfill(float* x) {
+  long long i = get_global_id(0);
+  float v = (float)i;
+  for (int k = 0; k < 4000; ++k) v = v * 1.0000001f + 0.0f;
+  x[i] = v > -1.0f ? (float)i + 1.0f : 0.0f;
+}
+__global__ void add1(float* x) { long long i = get_global_id(0); x[i] = x[i] + 1.0f; }
+"""
+
+
+def test_copy_between_orders_against_async_compute_queues():
+    """with async enqueue a compute sits on a compute
+    queue, not the main stream.  copy_between must wait for it (the source
+    is still being written) and later computes on any queue must wait for
+    the copy (they read the destination)."""
+    g0 = ck.ClPlatforms.all().gpus()[0]
+    cr = ck.ClNumberCruncher(g0 + g0, COPY_SRC, queue_concurrency=4)
+    n = 1 << 18
+    x = ck.ClArray(np.zeros(n, np.float32))
+    y = ck.ClArray(np.zeros(n, np.float32))
+    x.read = y.read = False
+    x.write = y.write = False
+    # establish buffers on both devices (one device each, full range)
+    x.compute(cr, 11, "add1", n, 256)
+    y.compute(cr, 12, "add1", n, 256)
+    cr.enqueue_mode = True
+    cr.enqueue_mode_async_enable = True
+    # device 0: slow fill of x on a compute queue, then copy x(dev0) -> y(dev1)
+    cr.cores.set_device_enabled(1, False)
+    x.compute(cr, 13, "slowfill", n, 256)
+    cr.cores.copy_between(0, x._spec(), 1, y._spec(), n * 4)
+    cr.cores.set_device_enabled(1, True)
+    cr.cores.set_device_enabled(0, False)
+    y.compute(cr, 14, "add1", n, 256)  # on device 1, a compute queue: must see the copy
+    cr.cores.set_device_enabled(0, True)
+    cr.enqueue_mode = False
+    cr.enqueue_mode_async_enable = False
+    cr.download(y, 1)
+    np.testing.assert_array_equal(y.array, np.arange(n, dtype=np.float32) + 2.0)
+    cr.dispose()

@@ -226,3 +226,44 @@ def test_task_kernel_repeats():
     np.testing.assert_array_equal(x.array, 6.0)
     assert cr.repeat_count == 1  # the cruncher's own setting is restored
     cr.dispose()
+
+
+@pytest.mark.parametrize("fine", [False, True])
+def test_round_robin_rotates_tasks(fine):
+    """ClDevicePoolType.DEVICE_ROUND_ROBIN (ClPipeline.cs:3801-3806): task k
+    runs on device k mod D; a serial group takes one rotation slot as a
+    whole and stays in order on its device; a global barrier is untargeted."""
+    cpu = ck.ClPlatforms.all().cpus(True)
+    D = 3
+    pool = ClDevicePool(ClDevicePoolType.DEVICE_ROUND_ROBIN, SRC, fine, 3)
+    pool.add_device(cpu + cpu + cpu)
+    tp = ClTaskPool()
+    tasks, arrays = [], []
+    for i in range(12):
+        x, t = _task("fill", 256, float(i))
+        tp.feed(t)
+        tasks.append(t)
+        arrays.append(x)
+    shared = ck.ClArray(np.zeros(128, np.float32))
+    group = []
+    for k in range(4):  # serial group: rotation slot 12 -> device 0
+        _, t = _task("add", 128, 1.0, shared)
+        t.type = (ClTaskType.TASK_MESSAGE_SERIAL_MODE_BEGIN if k == 0 else
+                  ClTaskType.TASK_MESSAGE_SERIAL_MODE_END if k == 3 else ClTaskType.TASK_MESSAGE_DEFAULT)
+        tp.feed(t)
+        group.append(t)
+    x, t = _task("fill", 256, 99.0)  # rotation slot 13 -> device 1
+    tp.feed(t)
+    tasks.append(t)
+    arrays.append(x)
+    pool.enqueue_task_pool(tp)
+    pool.finish()
+    for i, t in enumerate(tasks[:12]):
+        assert t.device_index == i % D, (i, t.device_index)
+    assert {t.device_index for t in group} == {12 % D}
+    assert tasks[12].device_index == 13 % D
+    np.testing.assert_array_equal(shared.array, 4.0)
+    for i, x in enumerate(arrays[:12]):
+        np.testing.assert_array_equal(x.array, float(i))
+    assert pool.device_task_counts() == [8, 5, 4]
+    pool.dispose()

@@ -68,5 +68,5 @@ for (m, t), v in res.items():
     err = float(abs(c - g.reference(slice(0, 256))).max())
     out[f"{m}x{n}x{k}/{t}/g{gm}"] = {"median_tflops": round(statistics.median(v), 1),
                                     "min_tflops": round(min(v), 1), "max_tflops": round(max(v), 1),
-                                    "max_err_rows0_255": err, "spin_timeouts": g.spin_timeouts()}
+                                    "max_err_rows0_255": err, "handover_fallbacks": g.handover_fallbacks()}
 print(json.dumps(out, indent=1))
