@@ -575,17 +575,39 @@ long long Worker::markers_reached() {
   return r;
 }
 
+static double env_spin_us() {
+  const char* e = std::getenv("CEK_SPIN_US");
+  return e ? std::max(0.0, std::atof(e)) : 50.0;
+}
+double Worker::spin_us = env_spin_us();
+
+static inline void cpu_relax() { __builtin_ia32_pause(); }
+
 void Worker::post(std::function<void()> fn) {
   {
     std::lock_guard<std::mutex> g(mu_);
     q_.push_back(std::move(fn));
+    posted_.fetch_add(1, std::memory_order_release);
   }
-  cv_.notify_one();
+  if (sleeping_.load(std::memory_order_acquire)) cv_.notify_one();
 }
 
 void Worker::wait() {
+  const uint64_t target = posted_.load(std::memory_order_acquire);
+  if (finished_.load(std::memory_order_acquire) < target && spin_us > 0) {
+    const double until = now_ms() + spin_us * 1e-3;
+    int n = 0;
+    while (finished_.load(std::memory_order_acquire) < target) {
+      cpu_relax();
+      if ((++n & 63) == 0 && now_ms() > until) break;
+    }
+  }
   std::unique_lock<std::mutex> lk(mu_);
-  idle_cv_.wait(lk, [&] { return q_.empty() && !busy_; });
+  if (finished_.load(std::memory_order_acquire) < target) {
+    waiter_blocked_.store(true, std::memory_order_release);
+    idle_cv_.wait(lk, [&] { return q_.empty() && !busy_; });
+    waiter_blocked_.store(false, std::memory_order_release);
+  }
   if (err_) {
     auto e = err_;
     err_ = nullptr;
@@ -597,9 +619,23 @@ void Worker::thread_loop() {
   bool device_set = false;
   for (;;) {
     std::function<void()> job;
+    // spin for new work first (a hot loop of computes posts every few µs)
+    if (spin_us > 0 && !stop_) {
+      const uint64_t seen = finished_.load(std::memory_order_acquire);
+      const double until = now_ms() + spin_us * 1e-3;
+      int n = 0;
+      while (posted_.load(std::memory_order_acquire) == seen) {
+        cpu_relax();
+        if ((++n & 63) == 0 && now_ms() > until) break;
+      }
+    }
     {
       std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty() && !stop_) {
+        sleeping_.store(true, std::memory_order_release);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        sleeping_.store(false, std::memory_order_release);
+      }
       if (stop_ && q_.empty()) return;
       job = std::move(q_.front());
       q_.pop_front();
@@ -618,8 +654,9 @@ void Worker::thread_loop() {
     {
       std::lock_guard<std::mutex> g(mu_);
       busy_ = false;
+      finished_.fetch_add(1, std::memory_order_release);
     }
-    idle_cv_.notify_all();
+    if (waiter_blocked_.load(std::memory_order_acquire)) idle_cv_.notify_all();
   }
 }
 

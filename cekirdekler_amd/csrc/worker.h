@@ -164,8 +164,14 @@ class Worker {
   size_t graphs_cached() const { return graphs_.size(); }
 
   // --- job thread --------------------------------------------------------
+  // Hand-off to the worker thread.  Both sides spin (with pause) for up to
+  // spin_us before blocking on a condition variable: back-to-back computes
+  // (a loop of enqueue-mode calls, ~10-20 µs apart) then cost an atomic
+  // store and a cache-line transfer per device instead of a futex wake-up
+  // (tens of µs on a busy host).  CEK_SPIN_US sets it (0: block at once).
   void post(std::function<void()> fn);
   void wait();  // rethrows the first job exception
+  static double spin_us;
 
   // --- timing (Worker.cs:753-807) ---------------------------------------
   std::map<int, double> bench_ms;
@@ -222,6 +228,8 @@ class Worker {
   std::condition_variable cv_, idle_cv_;
   std::deque<std::function<void()>> q_;
   bool busy_ = false, stop_ = false;
+  std::atomic<uint64_t> posted_{0}, finished_{0};  // jobs handed over / completed
+  std::atomic<bool> sleeping_{false}, waiter_blocked_{false};
   std::exception_ptr err_;
 };
 

@@ -18,7 +18,7 @@ LIBRARY = {
     # losers of rounds 1-2 live in git history and profiles/gemm_*.md)
     "sgemm_bf16": ["cek_sgemm_bf16_256x256", "cek_sgemm_bf16_256x256pp", "cek_sgemm_bf16_256x256pb",
                    "cek_sgemm_bf16_256x128pb", "cek_sgemm_bf16_256x128pe", "cek_sgemm_bf16_128x128",
-                   "cek_sgemm_bf16_256x256pp_sk", "cek_sgemm_bf16_256x256pb_sk", "cek_sgemm_bf16_256x256pb_sy",
+                   "cek_sgemm_bf16_256x256pp_sk", "cek_sgemm_bf16_256x256pb_sk",
                    "cek_sgemm_bf16_256x256pb_sw"],
     "sgemm_f32": ["cek_sgemm_f32_128x128", "cek_sgemm_f32_256x128", "cek_sgemm_f32_256x256",
                   "cek_sgemm_f32_256x256ir", "cek_sgemm_f32_256x256ib7", "cek_sgemm_f32_256x128ie",
@@ -36,7 +36,7 @@ LIBRARY = {
 # "name:arity" so a compute() whose array list does not match the kernel's
 # signature is rejected on the host instead of faulting on the device.
 ARITY = {
-    **{k: (6 if k.endswith(("_sk", "_sy", "_sw")) else 4) for k in LIBRARY["sgemm_bf16"]},
+    **{k: (6 if k.endswith(("_sk", "_sw")) else 4) for k in LIBRARY["sgemm_bf16"]},
     **{k: 4 for k in LIBRARY["sgemm_f32"]},
     **{k: 3 for k in LIBRARY["mandelbrot"]},
     **{k: 4 for k in LIBRARY["nbody"] if "energy" not in k},
