@@ -464,13 +464,21 @@ HOST_RESIDENT_PANELS = 16
 
 
 def _peer_topology(world: int) -> dict:
-    """hipDeviceCanAccessPeer among this job's GPUs (query only) and the
-    device-to-device path the runtime takes between them."""
+    """hipDeviceCanAccessPeer among this job's GPUs, the device-to-device path
+    the runtime takes between them, and measured copy bandwidth by engine
+    (SDMA vs copy kernel; a few pairs, every pair at once, inside GPU 0),
+    every copy checked byte for byte (utils/multigpu.peer_bandwidth_report)."""
     from cekirdekler_amd._native import cek
+    from cekirdekler_amd.utils.multigpu import peer_bandwidth_report
 
     full = cek.can_access_peer_matrix()
     m = [row[:world] for row in full[:world]]
-    return {"gpus_visible": len(full), "job_gpus": world, "can_access_peer": m, "path": cek.peer_path(m)}
+    out = {"gpus_visible": len(full), "job_gpus": world, "can_access_peer": m, "path": cek.peer_path(m)}
+    try:  # an extra: a failure is reported in its field
+        out["bandwidth"] = peer_bandwidth_report(list(range(world)))
+    except Exception as e:  # pragma: no cover
+        out["bandwidth"] = {"error": repr(e)[:300]}
+    return out
 
 
 def _free_port() -> int:

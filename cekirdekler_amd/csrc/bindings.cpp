@@ -12,6 +12,7 @@
 #include "jit.h"
 #include "memory.h"
 #include "pool.h"
+#include "xgmi.h"
 
 namespace py = pybind11;
 using namespace cek;
@@ -336,6 +337,50 @@ PYBIND11_MODULE(_cek, m) {
       .def("allreduce_sum_f32", [](RcclComm& c, uint64_t p, uint64_t n, uint64_t stream) {
         c.allreduce_sum_f32(reinterpret_cast<void*>(p), n, reinterpret_cast<hipStream_t>(stream));
       }, py::call_guard<py::gil_scoped_release>());
+
+  // device→device copy engines (xgmi.h)
+  m.def("measure_copy", [](int src, int dst, uint64_t bytes, int engine, int reps, int stream_ordinal) {
+        CopyMeasure r;
+        {
+          py::gil_scoped_release rel;
+          r = measure_copy(src, dst, bytes, engine, reps, stream_ordinal);
+        }
+        py::dict d;
+        d["src"] = r.src;
+        d["dst"] = r.dst;
+        d["engine"] = r.engine == kCopyKernel ? "kernel" : "sdma";
+        d["stream_gpu"] = r.stream_ordinal;
+        d["bytes"] = r.bytes;
+        d["reps"] = r.reps;
+        d["ms"] = r.ms;
+        d["gbps"] = r.gbps;
+        d["verified"] = r.verified;
+        return d;
+      }, py::arg("src"), py::arg("dst"), py::arg("bytes"), py::arg("engine"), py::arg("reps") = 5,
+      py::arg("stream_ordinal") = -1);
+  m.def("measure_all_pairs", [](const std::vector<int>& ords, uint64_t bytes, int engine, int reps) {
+        ConcurrentMeasure r;
+        {
+          py::gil_scoped_release rel;
+          r = measure_all_pairs(ords, bytes, engine, reps);
+        }
+        py::dict d;
+        d["gpus"] = r.gpus;
+        d["copies"] = r.copies;
+        d["engine"] = r.engine == kCopyKernel ? "kernel" : "sdma";
+        d["bytes_per_copy"] = r.bytes_per_copy;
+        d["wall_ms"] = r.wall_ms;
+        d["aggregate_gbps"] = r.aggregate_gbps;
+        d["per_copy_gbps"] = r.per_copy_gbps;
+        d["verified"] = r.verified;
+        return d;
+      }, py::arg("ordinals"), py::arg("bytes"), py::arg("engine"), py::arg("reps") = 3);
+  m.def("calibrate_copy_engines", &calibrate, py::arg("ordinals"), py::arg("sizes"), py::arg("reps") = 3,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("choose_copy_engine", &choose_engine);
+  m.def("set_copy_engine_override", &set_engine_override);
+  m.def("copy_engine_table", &engine_table);
+  m.def("record_copy_engine", &record_engine);
 
   py::class_<UserEvent>(m, "UserEvent")
       .def(py::init<>())

@@ -1,5 +1,7 @@
 #include "copy_engine.h"
 
+#include "xgmi.h"
+
 #include <cstring>
 
 #include "device.h"
@@ -75,7 +77,8 @@ void CopyEngine::copy(void* dst, int dst_dev, const void* src, int src_dev, uint
     CEK_HIP(hipEventRecord(p.b, s));
   }
   if (dst_dev >= 0 && src_dev >= 0) {
-    CEK_HIP(hipMemcpyPeerAsync(dst, dst_dev, src, src_dev, bytes, s));
+    // SDMA or a pull kernel on the destination, by the calibrated table (xgmi.h)
+    peer_copy(dst, dst_dev, src, src_dev, bytes, s, on);
     p2p_bytes += bytes;
     p.kind = "p2p";
   } else if (dst_dev >= 0) {

@@ -10,6 +10,7 @@
 
 #include "memory.h"
 #include "trace.h"
+#include "xgmi.h"
 
 namespace cek {
 
@@ -95,16 +96,19 @@ void Cores::count_d2d(int ws, int wd, uint64_t bytes) {
     d2d_.staged += bytes;
 }
 
-// One device→device copy on stream s (of either device): a plain D2D copy
-// inside one GPU, a peer copy between GPUs (over xGMI when peer access is on;
-// the runtime stages it through host memory otherwise).
-uint64_t Cores::d2d_copy(int ws, int wd, char* dst, const char* src, uint64_t bytes, hipStream_t s) {
+// One device→device copy on stream s of local worker sw (either end): a D2D
+// copy inside one GPU, a peer copy between GPUs (over xGMI when peer access
+// is on; the runtime stages it through host memory otherwise), by SDMA or a
+// copy kernel on sw's GPU, whichever the calibrated engine table says is
+// faster for this pair and size (xgmi.h; SDMA for an uncalibrated pair).
+uint64_t Cores::d2d_copy(int ws, int wd, char* dst, const char* src, uint64_t bytes, hipStream_t s, int sw) {
   if (!bytes || dst == src) return 0;
   const int os = workers_[ws]->dev().ordinal, od = workers_[wd]->dev().ordinal;
-  if (os == od)
-    CEK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+  const bool peer_ok = os == od || can_peer(ws, wd);
+  if (peer_ok)
+    peer_copy(dst, od, src, os, bytes, s, workers_[sw]->dev().ordinal);
   else
-    CEK_HIP(hipMemcpyPeerAsync(dst, od, src, os, bytes, s));
+    CEK_HIP(hipMemcpyPeerAsync(dst, od, src, os, bytes, s));  // staged by the runtime
   count_d2d(ws, wd, bytes);
   return bytes;
 }
@@ -203,7 +207,7 @@ uint64_t Cores::issue_gather(const ComputeCall& c, const BalancerState& st, cons
         for (int d : on) {  // this GPU's slices → every other replica
           if (d == g || p.ptr[d] == p.ptr[g]) continue;
           if (workers_[d]->gpu()) {
-            moved += d2d_copy(g, d, p.ptr[d] + sg.first, p.ptr[g] + sg.first, sg.second, m);
+            moved += d2d_copy(g, d, p.ptr[d] + sg.first, p.ptr[g] + sg.first, sg.second, m, g);
             log_op(global_base_ + d, "gather", 0, static_cast<long long>(sg.first), static_cast<long long>(sg.second),
                    global_base_ + g);
           } else {
@@ -676,7 +680,7 @@ void Cores::copy_between(int src_dev, const ArraySpec& src, int dst_dev, const A
     ws.join_streams(s);
     CEK_HIP(hipStreamWaitEvent(s, before, 0));
     d2d_ = D2DCount();
-    d2d_copy(src_dev, dst_dev, static_cast<char*>(dp), static_cast<const char*>(sp), bytes, s);
+    d2d_copy(src_dev, dst_dev, static_cast<char*>(dp), static_cast<const char*>(sp), bytes, s, src_dev);
     hipEvent_t after = gather_event(pushed_, src_dev);
     CEK_HIP(hipEventRecord(after, s));
     wd.set_device();
@@ -1055,7 +1059,7 @@ uint64_t Cores::stage_peer_reads(const ComputeCall& c, const std::vector<long lo
         if (j == k || !len[j]) continue;
         Worker& ws = *workers_[part[j]];
         CEK_HIP(hipStreamWaitEvent(m, peer_ev_[part[j]].up, 0));
-        p2p += d2d_copy(part[j], part[k], ptr[k] + off[j], ptr[j] + off[j], len[j], m);
+        p2p += d2d_copy(part[j], part[k], ptr[k] + off[j], ptr[j] + off[j], len[j], m, part[k]);
         (void)ws;
         log_op(global_base_ + part[k], "p2p", 0, static_cast<long long>(off[j]), static_cast<long long>(len[j]),
                global_base_ + part[j]);

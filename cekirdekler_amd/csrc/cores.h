@@ -386,7 +386,7 @@ class Cores {
     bool pcie_fallback = false;
   } d2d_;
   void count_d2d(int ws, int wd, uint64_t bytes);
-  uint64_t d2d_copy(int ws, int wd, char* dst, const char* src, uint64_t bytes, hipStream_t s);
+  uint64_t d2d_copy(int ws, int wd, char* dst, const char* src, uint64_t bytes, hipStream_t s, int stream_worker);
   // keep-resident gather (ArraySpec::gather): kernels-done event per worker,
   // copies-done event per GPU worker; later work waits on every copies-done
   // event while gather_pending_

@@ -172,3 +172,70 @@ def test_cl_pipeline_mixed_cpu_gpu_stage():
     r = s1.cruncher.ranges(1)
     assert all(x > 0 for x in r), r  # both devices computed a slice
     pipe.dispose()
+
+
+@pytest.mark.parametrize("engine", [0, 1])
+@pytest.mark.parametrize("nbytes", [4 << 20, (1 << 20) + 4, 256 << 20])
+def test_copy_engines_byte_exact_same_gpu(engine, nbytes):
+    """both device→device engines (SDMA, copy kernel) on one
+    GPU, byte for byte (a size that is not a multiple of 16 takes the
+    kernel's SDMA tail)."""
+    from cekirdekler_amd._native import cek
+
+    r = cek.measure_copy(0, 0, nbytes, engine, 2)
+    assert r["verified"], r
+    assert r["gbps"] > 0
+
+
+def test_gather_through_kernel_copy_engine():
+    """The keep-resident gather with the copy-kernel engine forced: same
+    result as with SDMA (Cores::d2d_copy → peer_copy)."""
+    from cekirdekler_amd._native import cek
+
+    g0 = ck.ClPlatforms.all().gpus()[0]
+    src = """__global__ void hop(const float* x, float* y) {
+      long long i = get_global_id(0); long long n = get_global_size(0);
+      y[i] = x[(i * 7919) % n] * 0.5f + 1.0f; }"""
+    results = []
+    for engine in (0, 1):
+        cek.set_copy_engine_override(engine)
+        try:
+            cr = ck.ClNumberCruncher(g0 + g0 + g0, src)
+            cr.set_time_scale(2, 1.6)
+            n = 3 * (1 << 15)
+            x0 = np.random.default_rng(5).standard_normal(n).astype(np.float32)
+            a, b = ck.ClArray(x0.copy()), ck.ClArray(np.zeros(n, np.float32))
+            a.write = b.write = False
+            s, d = a, b
+            for it in range(5):
+                s.read = it == 0
+                d.read = False
+                s.gather_resident, d.gather_resident = False, True
+                s.next_param(d).compute(cr, 1, "hop", n, 64)
+                s, d = d, s
+            outs = []
+            for dev in range(3):
+                s.array[:] = 0
+                cr.download(s, dev)
+                outs.append(s.array.copy())
+            cr.dispose()
+        finally:
+            cek.set_copy_engine_override(-1)
+        for o in outs[1:]:
+            np.testing.assert_array_equal(o, outs[0])
+        results.append(outs[0])
+    np.testing.assert_array_equal(results[0], results[1])
+
+
+def test_peer_bandwidth_report_on_visible_gpus():
+    """The bench's xGMI section on whatever this box has (one GPU: the
+    same-GPU rows only, no crash)."""
+    from cekirdekler_amd.utils.multigpu import peer_bandwidth_report, visible_gpus
+
+    n = visible_gpus()
+    rep = peer_bandwidth_report(list(range(min(n, 8))), pair_bytes=64 << 20, all_bytes=16 << 20, reps=2)
+    assert rep["gpus_visible"] == n
+    assert rep["all_verified"], rep
+    assert set(rep["same_gpu"]) == {"sdma", "kernel"}
+    if n >= 2:
+        assert rep["pairs"] and rep["all_pairs"]

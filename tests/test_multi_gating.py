@@ -70,3 +70,35 @@ def test_rank_worker_control_plane_two_gloo_ranks():
     out = json.loads(lines[-1])
     assert out["ok"] and out["splits_identical"] and out["ranks"] == 2, out
     assert out["per_rank"][0]["uneven"], out
+
+
+def test_peer_pairs_and_report_shape(monkeypatch):
+    """The xGMI bandwidth report's structure, on a fake measurement backend
+    (the real one needs GPUs): pairs chosen, both engines per pair, the
+    faster one named, verification folded into all_verified."""
+    from cekirdekler_amd.utils import multigpu
+
+    assert multigpu.peer_pairs(1) == []
+    assert multigpu.peer_pairs(2) == [(0, 1), (1, 0)]
+    assert multigpu.peer_pairs(8) == [(0, 1), (0, 7), (1, 2), (7, 0)]
+
+    class Fake:
+        @staticmethod
+        def measure_copy(s, d, b, e, reps=5, stream_ordinal=-1):
+            return {"src": s, "dst": d, "engine": ["sdma", "kernel"][e], "bytes": b, "gbps": 50.0 + 10 * e,
+                    "ms": 1.0, "verified": True}
+
+        @staticmethod
+        def measure_all_pairs(ords, b, e, reps=3):
+            return {"gpus": len(ords), "aggregate_gbps": 1000.0, "verified": True}
+
+    import cekirdekler_amd._native as nat
+
+    monkeypatch.setattr(nat, "cek", Fake)
+    monkeypatch.setattr(multigpu, "visible_gpus", lambda: 4)
+    rep = multigpu.peer_bandwidth_report([0, 1, 2, 3])
+    assert rep["gpus_visible"] == 4 and rep["job_gpus"] == 4
+    assert [(r["src"], r["dst"]) for r in rep["pairs"]] == [(0, 1), (0, 3), (1, 2), (3, 0)]
+    assert all(r["faster"] == "kernel" for r in rep["pairs"])
+    assert rep["all_verified"] and rep["min_pair_gbps"] == 60.0
+    assert set(rep["all_pairs"]) == {"sdma", "kernel"}
