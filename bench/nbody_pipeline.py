@@ -18,10 +18,16 @@ every push advances one system by one step through all three stages.  The
 first stepped system is checked against a float64 host step on sampled
 bodies.
 
-Placement (BASELINE config 4: 4 GPUs): with 3 or more GPUs the stages run
-on distinct GPUs (force on all but two, kick and energy on one each: 2 + 1
-+ 1 on four); with fewer, round-robin.  ``--logical 4`` rehearses the
-four-GPU placement on one GPU (four logical devices of GPU 0).  Stage times
+Placement (BASELINE config 4: 4 GPUs).  ``shared`` (default): every stage
+spans every GPU — the stages share devices, as the reference allows
+(ClPipeline.cs:1728) — so the O(n²) force stage is range-split over all of
+them and the O(n) kick and energy stages run beside it on their own
+streams; no GPU idles for a push.  ``split``: distinct GPUs per stage
+(force on all but two, kick and energy on one each: 2 + 1 + 1 on four), the
+round-3 placement whose last two GPUs sat idle 99 % of a push.
+``--logical 4`` rehearses the four-GPU placement on one GPU (four logical
+devices of GPU 0).  ``device_busy_fraction``: per device, the union of its
+kernel spans (every stage) over the steady pushes' wall time.  Stage times
 are device times from hipEvent timelines; the stage-transition copies are
 timed by hipEvents on the copy engine's streams, and both are put on one
 host-anchored clock, so ``copy_overlap`` measures how much of the transfer
@@ -36,7 +42,8 @@ import numpy as np
 from common import FP32_PEAK_TFLOPS, emit, sync
 
 import cekirdekler_amd as ck
-from cekirdekler_amd.parallel.pipeline import ClPipelineStage
+from cekirdekler_amd._native import cek
+from cekirdekler_amd.parallel.pipeline import ClPipelineStage, _intersection
 
 FORCE = r"""
 // 2 bodies per work item as one packed f32x2 pair (v_pk_* issue: see
@@ -127,6 +134,7 @@ ap.add_argument("--n", type=int, default=1 << 20)
 ap.add_argument("--pushes", type=int, default=14)
 ap.add_argument("--gpus", type=int, default=0, help="0 = all visible")
 ap.add_argument("--logical", type=int, default=0, help="rehearsal: act as if GPU 0 were this many GPUs")
+ap.add_argument("--placement", choices=("shared", "split"), default="shared")
 a = ap.parse_args()
 n = a.n
 g = ck.ClPlatforms.all().gpus()
@@ -136,13 +144,19 @@ if a.logical > 1:
         g0 = g0 + g[0]
     g = g0
 ng = len(g) if a.gpus <= 0 else min(a.gpus, len(g))
-if ng >= 3:
+if a.placement == "shared":
+    # every stage on every GPU: device index k of each stage is GPU k
+    devs = [g[0:ng]] * 3
+    dev_of = [list(range(ng))] * 3
+elif ng >= 3:
     # distinct GPUs per stage: the O(n²) force stage gets every GPU but the
     # last two (range-split by the load balancer); kick-drift and the energy
     # diagnostic get one each
     devs = [g[0:ng - 2], g[ng - 2], g[ng - 1]]
+    dev_of = [list(range(ng - 2)), [ng - 2], [ng - 1]]
 else:
     devs = [g[i % ng] for i in range(3)]
+    dev_of = [[i % ng] for i in range(3)]
 
 f4 = lambda: np.zeros(4 * n, np.float32)  # noqa: E731
 prm = np.array([1e-4, 1.0, float(n), 1e-3], np.float32)
@@ -183,13 +197,16 @@ res_pos, res_vel = np.zeros((n, 4), np.float32), np.zeros((n, 4), np.float32)
 energy = np.zeros(n // 256, np.float32)
 kinetic = {}
 times, ready_at, check = [], None, None
+windows = []  # (begin, end) of every push on the runtime clock
 for k in range(a.pushes):
     j = k % M
     sync()
     t = time.perf_counter()
+    w0 = cek.now_ms()
     ready = pipe.push_data([states[j][0].reshape(-1), states[j][1].reshape(-1)],
                            [res_pos.reshape(-1), res_vel.reshape(-1), energy])
     sync()
+    windows.append((w0, cek.now_ms()))
     times.append((time.perf_counter() - t) * 1e3)
     if ready:
         if ready_at is None:
@@ -225,11 +242,39 @@ def stage_device_ms(i):
 
 
 stage_ms = [stage_device_ms(i) for i in range(3)]
+
+
+def device_busy_fraction():
+    """Per device of the placement (logical devices count separately): the
+    union of its kernel spans, every stage, inside the steady pushes'
+    windows, over those windows' total length."""
+    skip = L if len(windows) > L + 1 else 2
+    wins = [(b - tl["t0"], e - tl["t0"]) for b, e in windows[skip:]]
+    total = sum(e - b for b, e in wins)
+    spans = {}
+    for st, d, b, e in tl["kernels"]:
+        spans.setdefault(dev_of[st][d], []).append((b, e))
+    out = []
+    for dev in range(ng):
+        iv = spans.get(dev, [])
+        union = []
+        for b, e in sorted(iv):
+            if union and b <= union[-1][1]:
+                union[-1][1] = max(union[-1][1], e)
+            else:
+                union.append([b, e])
+        busy = sum(_intersection(wb, we, [tuple(u) for u in union]) for wb, we in wins)
+        out.append(round(busy / total, 4) if total > 0 else 0.0)
+    return out
+
+
+busy = device_busy_fraction()
 ov_force = pipe.copy_overlap(tl, stage=0)
 ov_any = pipe.copy_overlap(tl)
 xfer = pipe.transfer_stats()
 emit({"config": "nbody_pipeline_3stage", "n": n, "systems_in_flight": M, "gpus_used": ng,
-      "stage_gpus": [len(d) if hasattr(d, "__len__") else 1 for d in devs], "push_ms_median": ms,
+      "placement_mode": a.placement, "stage_gpus": [len(d) if hasattr(d, "__len__") else 1 for d in devs],
+      "push_ms_median": ms, "device_busy_fraction": busy, "min_device_busy_fraction": min(busy),
       "stage_device_ms": stage_ms, "ready_after_pushes": ready_at,
       "interactions_per_s": n * n / (ms * 1e-3), "tflops_20flop": 20 * n * n / (ms * 1e-3) / 1e12,
       # per PHYSICAL GPU of the force stage (logical devices of one GPU share it)

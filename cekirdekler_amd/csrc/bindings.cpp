@@ -130,6 +130,7 @@ PYBIND11_MODULE(_cek, m) {
   m.def("parse_kernels", &parse_kernels);
   m.def("is_opencl_dialect", &is_opencl_dialect);
   m.def("gpu_rewrite", &gpu_rewrite);
+  m.def("now_ms", &now_ms, "the runtime's host clock (steady clock, ms): the clock of every timeline");
   m.def("cpu_rewrite", &cpu_rewrite);
   m.def("cache_dir", &cache_dir);
   m.def("hash_hex", &hash_hex);

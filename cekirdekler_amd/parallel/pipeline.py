@@ -363,14 +363,15 @@ class ClPipeline:
 
     def timeline(self) -> dict:
         """``{"kernels": [(stage, device, begin, end)], "copies": [(kind,
-        device, bytes, begin, end)]}`` in host-clock ms since the first
-        recorded event; waits for the recorded work and clears it."""
+        device, bytes, begin, end)], "t0": origin}`` in host-clock ms since
+        the first recorded event (``t0`` on the runtime clock,
+        ``cek.now_ms()``); waits for the recorded work and clears it."""
         ks = [(i, t["device"], t["abs_begin_ms"], t["abs_end_ms"])
               for i, st in enumerate(self.stages) for t in st.cruncher.timeline()]
         cs = [(c["kind"], c["device"], c["bytes"], c["abs_begin_ms"], c["abs_end_ms"]) for c in self.engine.timeline()]
         t0 = min([k[2] for k in ks] + [c[3] for c in cs], default=0.0)
         return {"kernels": [(i, d, b - t0, e - t0) for i, d, b, e in ks],
-                "copies": [(k, d, n, b - t0, e - t0) for k, d, n, b, e in cs]}
+                "copies": [(k, d, n, b - t0, e - t0) for k, d, n, b, e in cs], "t0": t0}
 
     @staticmethod
     def copy_overlap(tl: dict, stage: Optional[int] = None) -> dict:

@@ -1,0 +1,138 @@
+"""GPU probe: variants of the N-body pipeline's JIT force kernel (user
+kernel strings, hiprtc) on one GPU at the body share one GPU computes when
+the force stage spans 1, 2 or 4 GPUs.  Same signature and body mapping as
+bench/nbody_pipeline.py's FORCE (work-group g owns 256·B bodies).
+
+    python tools/nbody_force_variants.py [n] [fractions] [out.json]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import cekirdekler_amd as ck  # noqa: E402
+
+HEAD = "typedef float f2 __attribute__((ext_vector_type(2)));\n"
+
+
+def variant(name, B, prefetch, tile, unroll):
+    """B bodies per work item (B/2 packed pairs); `tile` bodies per LDS tile
+    (256 or 512); `prefetch`: the next tile is loaded into registers while
+    the current one is consumed."""
+    NP = B // 2
+    loads = tile // 256
+    s = [f"__global__ __launch_bounds__(256) void {name}(const float4* pos, const float4* vel, const float* prm,",
+         "    float4* pos_o, float4* vel_o, float4* acc_o) {",
+         f"  __shared__ float4 t[{tile}];",
+         "  const int n = (int)prm[2];",
+         "  const f2 e2 = {prm[0], prm[0]};",
+         "  const long long w = get_global_id(0);",
+         f"  const long long i0 = (w / 256) * {256 * B} + (w % 256);",
+         f"  f2 px[{NP}], py[{NP}], pz[{NP}], ax[{NP}], ay[{NP}], az[{NP}];",
+         f"  for (int p = 0; p < {NP}; ++p) {{",
+         "    const float4 b0 = pos[i0 + (2 * p) * 256], b1 = pos[i0 + (2 * p + 1) * 256];",
+         "    px[p] = f2{b0.x, b1.x}; py[p] = f2{b0.y, b1.y}; pz[p] = f2{b0.z, b1.z};",
+         "    ax[p] = ay[p] = az[p] = f2{0.f, 0.f};",
+         "  }",
+         "  const int l = threadIdx.x;"]
+    if prefetch:
+        s += [f"  float4 nx[{loads}];", f"  for (int k = 0; k < {loads}; ++k) nx[k] = pos[k * 256 + l];"]
+    s += [f"  for (int j0 = 0; j0 < n; j0 += {tile}) {{", "    __syncthreads();"]
+    if prefetch:
+        s += [f"    for (int k = 0; k < {loads}; ++k) t[k * 256 + l] = nx[k];", "    __syncthreads();",
+              f"    if (j0 + {tile} < n) for (int k = 0; k < {loads}; ++k) nx[k] = pos[j0 + {tile} + k * 256 + l];"]
+    else:
+        s += [f"    for (int k = 0; k < {loads}; ++k) t[k * 256 + l] = pos[j0 + k * 256 + l];", "    __syncthreads();"]
+    s += [f"#pragma unroll {unroll}",
+          f"    for (int j = 0; j < {tile}; ++j) {{",
+          "      const float4 q = t[j];",
+          "      const f2 qx = {q.x, q.x}, qy = {q.y, q.y}, qz = {q.z, q.z}, qm = {q.w, q.w};",
+          "#pragma unroll",
+          f"      for (int p = 0; p < {NP}; ++p) {{",
+          "        const f2 dx = qx - px[p], dy = qy - py[p], dz = qz - pz[p];",
+          "        const f2 r2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, __builtin_elementwise_fma(dz, dz, e2)));",
+          "        const f2 inv = {__builtin_amdgcn_rsqf(r2.x), __builtin_amdgcn_rsqf(r2.y)};",
+          "        const f2 sc = (qm * inv) * (inv * inv);",
+          "        ax[p] = __builtin_elementwise_fma(dx, sc, ax[p]);",
+          "        ay[p] = __builtin_elementwise_fma(dy, sc, ay[p]);",
+          "        az[p] = __builtin_elementwise_fma(dz, sc, az[p]);",
+          "      }", "    }", "  }",
+          f"  for (int p = 0; p < {NP}; ++p) {{",
+          "    const long long a = i0 + (2 * p) * 256, b = a + 256;",
+          "    acc_o[a] = make_float4(ax[p].x, ay[p].x, az[p].x, 0.f);",
+          "    acc_o[b] = make_float4(ax[p].y, ay[p].y, az[p].y, 0.f);",
+          "    pos_o[a] = pos[a]; pos_o[b] = pos[b]; vel_o[a] = vel[a]; vel_o[b] = vel[b];",
+          "  }", "}"]
+    return "\n".join(s) + "\n"
+
+
+VARIANTS = {  # name: (B, prefetch, tile, unroll)
+    "b2_plain": (2, False, 256, 8),
+    "b2_pf": (2, True, 256, 8),
+    "b2_pf512": (2, True, 512, 8),
+    "b4_pf": (4, True, 256, 4),
+    "b4_pf512": (4, True, 512, 4),
+}
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+    fracs = [float(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,0.5,0.25").split(",")]
+    src = HEAD + "".join(variant(k, *v) for k, v in VARIANTS.items())
+    g0 = ck.ClPlatforms.all().gpus()[0]
+    cr = ck.ClNumberCruncher(g0, src)
+    if cr.error_code():
+        raise SystemExit(cr.error_message())
+    rng = np.random.default_rng(0)
+    pos = np.zeros((n, 4), np.float32)
+    pos[:, :3] = rng.standard_normal((n, 3))
+    pos[:, 3] = 1.0 / n
+    vel = np.zeros((n, 4), np.float32)
+    prm = np.array([1e-4, 1.0, float(n), 1e-3], np.float32)
+    arrs = [ck.ClArray(pos.reshape(-1)), ck.ClArray(vel.reshape(-1)), ck.ClArray(prm)] + [
+        ck.ClArray(np.zeros(4 * n, np.float32)) for _ in range(3)]
+    for a in arrs[:3]:
+        a.write = False
+    for a in arrs[3:]:
+        a.read = False
+        a.write = False
+    res = {}
+    cid = 1
+    ref_acc = None
+    for f in fracs:
+        for name, (B, *_rest) in VARIANTS.items():
+            g = int(n // B * f) // 256 * 256
+            call = lambda: arrs[0].next_param(*arrs[1:]).compute(cr, cid, name, g, 256)  # noqa: E731
+            call()
+            torch.cuda.synchronize()
+            best = 1e30
+            for _ in range(3):
+                t = time.perf_counter()
+                call()
+                torch.cuda.synchronize()
+                best = min(best, (time.perf_counter() - t) * 1e3)
+            inter = g * B * n
+            cr.download(arrs[5], 0)
+            acc = arrs[5].array[: 4 * g * B].copy()
+            if ref_acc is None or len(ref_acc) != len(acc):
+                ref_acc = acc
+            err = float(np.abs(acc - ref_acc).max() / max(np.abs(ref_acc).max(), 1e-30))
+            res[f"{name}/{f}"] = {"work_groups": g // 256, "ms": round(best, 2),
+                                  "pct_fp32_peak": round(100 * 20 * inter / best / 1e9 / 157.3, 1),
+                                  "rel_diff_vs_first": err}
+            print(name, f, res[f"{name}/{f}"], flush=True)
+            cid += 1
+    cr.dispose()
+    if len(sys.argv) > 3:
+        with open(sys.argv[3], "w") as fh:
+            json.dump(res, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
