@@ -268,6 +268,11 @@ class ClArray:
         # kernels every device's slice of this array is copied into every
         # other device's replica (GPU↔GPU over xGMI, RCCL across ranks)
         self.gather_resident = False
+        # explicit per-blob slices for a compute with explicit pipeline blobs
+        # (compute(..., blob_bounds=...)): ((first element, count) per blob),
+        # e.g. row panel k of a GEMM operand for shell k; None: the slice
+        # proportional to each blob's work items
+        self.blob_slices = None
         # per cruncher (id): the split of the last compute this array took
         # part in without the read-only hint — (compute id, elements per work
         # item, elements per group, local range).  A device-resident array's
@@ -551,7 +556,8 @@ class ClArray:
         # The native spec is cached per (storage uid, flags): the uid changes
         # whenever the host storage does, so the pointer inside stays valid.
         key = (self._uid, self._read, self._partial, self._write, self._write_all, self._ro, self._wo,
-               self.zero_copy, self.elements_per_work_item, self.elements_per_group, self.gather_resident, pin)
+               self.zero_copy, self.elements_per_work_item, self.elements_per_group, self.gather_resident, pin,
+               None if self.blob_slices is None else tuple(self.blob_slices))
         cached = getattr(self, "_spec_cache", None)
         if cached is not None and cached[0] == key:
             return cached[1]
@@ -574,6 +580,9 @@ class ClArray:
                              self._read, self._partial, self._write, self._write_all,
                              self._ro, self._wo, zc, int(self.elements_per_work_item),
                              int(self.elements_per_group), bool(self.gather_resident))
+        if self.blob_slices is not None:
+            spec.blob_begin = [int(b) for b, _ in self.blob_slices]
+            spec.blob_count = [int(n) for _, n in self.blob_slices]
         self._spec_cache = (key, spec)
         return spec
 

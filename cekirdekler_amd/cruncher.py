@@ -18,6 +18,8 @@ import threading
 import time
 from typing import List, Optional, Sequence
 
+import numpy as np
+
 from ._native import cek, kernel_dir
 from .arrays import ClArray, ClParameterGroup, _register_cores, as_clarray
 from .hardware import ClDevices, ClPlatforms
@@ -549,6 +551,10 @@ class ClNumberCruncher:
         if not names:
             raise ClComputeError("no kernel name given")
         for a in group.arrays:
+            if a.blob_slices is not None:  # explicit per-blob slices: checked natively
+                if any(b < 0 or n < 0 or b + n > a.N for b, n in a.blob_slices):
+                    raise ClComputeError(f"Array-size error: a blob slice exceeds the array length ({a.N}).")
+                continue
             if a._partial or (a._write and not a._write_all):
                 if a.elements_per_group > 0:
                     if a.N < (G // L) * a.elements_per_group:
@@ -585,9 +591,15 @@ class ClNumberCruncher:
         """Validate a compute and freeze it into a native ComputeCall."""
         names = split_kernel_names(kernels)
         G, L = int(global_range), int(local_range)
+        # pipeline_blobs: a count (equal blobs), or explicit work-item bounds
+        # [0, b1, ..., G] of uneven blobs (one device; ClArray.blob_slices)
+        bounds = None
+        if not isinstance(pipeline_blobs, (int, np.integer)):
+            bounds = [int(x) for x in pipeline_blobs]
+            pipeline_blobs = max(1, len(bounds) - 1)
         try:
-            self._validate(group if specs is None else ClParameterGroup(), names, G, L, pipeline,
-                           int(pipeline_blobs))
+            self._validate(group if specs is None else ClParameterGroup(), names, G, L,
+                           pipeline and bounds is None, int(pipeline_blobs))
         except ClComputeError:
             self.number_of_errors_happened += 1
             raise
@@ -604,6 +616,8 @@ class ClNumberCruncher:
         call.pipeline = bool(pipeline)
         call.pipeline_event = bool(pipeline_type)
         call.blobs = int(pipeline_blobs)
+        if bounds is not None:
+            call.blob_bounds = bounds
         if granularity:
             if granularity % L or G % granularity:
                 self.number_of_errors_happened += 1

@@ -267,7 +267,9 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("zc", &ArraySpec::zc)
       .def_readwrite("epw", &ArraySpec::epw)
       .def_readwrite("epg", &ArraySpec::epg)
-      .def_readwrite("gather", &ArraySpec::gather);
+      .def_readwrite("gather", &ArraySpec::gather)
+      .def_readwrite("blob_begin", &ArraySpec::blob_begin)
+      .def_readwrite("blob_count", &ArraySpec::blob_count);
 
   py::class_<ComputeCall>(m, "ComputeCall")
       .def(py::init<>())
@@ -282,7 +284,8 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("pipeline", &ComputeCall::pipeline)
       .def_readwrite("pipeline_event", &ComputeCall::pipeline_event)
       .def_readwrite("blobs", &ComputeCall::blobs)
-      .def_readwrite("granularity", &ComputeCall::granularity);
+      .def_readwrite("granularity", &ComputeCall::granularity)
+      .def_readwrite("blob_bounds", &ComputeCall::blob_bounds);
 
   py::class_<CoresConfig>(m, "CoresConfig")
       .def(py::init<>())

@@ -1251,59 +1251,74 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
   log_op(gidx, "rec", 0, 0, 0, slot);
   for (int h = 0; h < halves; ++h) log_op(gidx, "wait", 17 + 3 * h + 1, 0, 0, slot);
   ++slot;
-  // Interleave the two half-pipelines' chunks so both read streams start early.
-  for (long long k = 0; k < per_half; ++k) {
-    for (int h = 0; h < halves; ++h) {
+  // Interleave the two half-pipelines' chunks so both read streams start
+  // early; explicit blobs (c.blob_bounds) alternate between the halves.
+  const bool explicit_blobs = !c.blob_bounds.empty();
+  const long long nblob = explicit_blobs ? static_cast<long long>(c.blob_bounds.size()) - 1 : per_half * halves;
+  const int used_halves = explicit_blobs ? (nblob >= 2 ? 2 : 1) : halves;
+  for (long long q = 0; q < nblob; ++q) {
+    {
+      const long long k = explicit_blobs ? q : q / halves;
+      const int h = explicit_blobs ? static_cast<int>(q % 2) : static_cast<int>(q % halves);
       // reads_on_main_stream: every blob's upload follows the full reads on
       // the main stream (one in-order chain of copies)
       hipStream_t rs = pipeline_reads_on_main_stream ? m : wk.pipe_stream(h, 0), ks = wk.pipe_stream(h, 1);
       // writes_on_compute_stream: a blob's D2H follows its kernel on the same
       // stream (in-stream order) instead of a write stream gated by an event
       hipStream_t ws = pipeline_writes_on_compute_stream ? ks : wk.pipe_stream(pipeline_writes_one_stream ? 0 : h, 2);
-      long long off = ref + h * (range / halves) + k * chunk;
+      const long long off = explicit_blobs ? ref + c.blob_bounds[q] : ref + h * (range / halves) + k * chunk;
+      const long long len = explicit_blobs ? c.blob_bounds[q + 1] - c.blob_bounds[q] : chunk;
       const int ksid = 17 + 3 * h + 1;
       const int wsid = pipeline_writes_on_compute_stream ? ksid : (pipeline_writes_one_stream ? 19 : ksid + 1);
       const int rsid = pipeline_reads_on_main_stream ? 0 : ksid - 1;  // as logged for the schedule checker
+      auto blob_slice = [&](const ArraySpec& a, uint64_t& b, uint64_t& n) {
+        if (explicit_blobs && a.blob_begin.size() == c.blob_bounds.size() - 1) {
+          b = a.blob_begin[q];
+          n = a.blob_count[q];
+        } else {
+          a.slice(off, len, c.local_range, b, n);
+        }
+      };
       for (auto& a : c.arrays) {
         if (a.zc || !a.partial) continue;
         uint64_t b, n;
-        a.slice(off, chunk, c.local_range, b, n);
+        blob_slice(a, b, n);
         wk.h2d(rs, a, b, n);
         *h2d += n * a.elem_size;
       }
-      log_op(gidx, "h2d", rsid, off, chunk);
+      log_op(gidx, "h2d", rsid, off, len);
       if (wk.gpu()) {
         hipEvent_t er = wk.event(slot);
         CEK_HIP(hipEventRecord(er, rs));
         CEK_HIP(hipStreamWaitEvent(ks, er, 0));
       }
-      log_op(gidx, "rec", rsid, off, chunk, slot);
-      log_op(gidx, "wait", ksid, off, chunk, slot);
+      log_op(gidx, "rec", rsid, off, len, slot);
+      log_op(gidx, "wait", ksid, off, len, slot);
       ++slot;
-      launch_kernels(wk, ks, c, off, chunk);
-      log_op(gidx, "kernel", ksid, off, chunk);
+      launch_kernels(wk, ks, c, off, len);
+      log_op(gidx, "kernel", ksid, off, len);
       if (wk.gpu() && ws != ks) {
         hipEvent_t ek = wk.event(slot);
         CEK_HIP(hipEventRecord(ek, ks));
         CEK_HIP(hipStreamWaitEvent(ws, ek, 0));
       }
-      log_op(gidx, "rec", ksid, off, chunk, slot);
-      log_op(gidx, "wait", wsid, off, chunk, slot);
+      log_op(gidx, "rec", ksid, off, len, slot);
+      log_op(gidx, "wait", wsid, off, len, slot);
       ++slot;
       for (auto& a : c.arrays) {
         if (a.zc || !a.write || a.write_all) continue;
         uint64_t b, n;
-        a.slice(off, chunk, c.local_range, b, n);
+        blob_slice(a, b, n);
         wk.d2h(ws, a, b, n);
         *d2h += n * a.elem_size;
       }
-      log_op(gidx, "d2h", wsid, off, chunk);
+      log_op(gidx, "d2h", wsid, off, len);
     }
   }
   // write-all owners download after every chunk's kernels
   bool any_all = false;
   for (auto& a : c.arrays) any_all |= (a.write && a.write_all && !a.zc);
-  for (int h = 0; h < halves; ++h) {
+  for (int h = 0; h < used_halves; ++h) {
     if (wk.gpu()) {
       hipEvent_t e = wk.event(slot);
       CEK_HIP(hipEventRecord(e, wk.pipe_stream(h, 1)));
@@ -1594,8 +1609,22 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
     throw Error("gather across ranks needs an RCCL communicator (DistributedCruncher(comm=True))");
   call_gathers_ = !gather_idx.empty() && !comm_ && nloc > 1;
   bool pipelined = pipe_req && c.repeats <= 1 && !enqueue_mode_ && !hazard && gather_idx.empty();
-  for (int i = 0; i < D && pipelined; ++i)
-    if (st.ranges[i] != 0 && (st.ranges[i] % (B * U) != 0 || st.ranges[i] < B * U)) pipelined = false;
+  if (!c.blob_bounds.empty()) {
+    // explicit blobs describe the whole range on one device
+    const auto& bb = c.blob_bounds;
+    bool ok = bb.size() >= 2 && bb.front() == 0 && bb.back() == G && c.pipeline_event;
+    for (size_t k = 1; ok && k < bb.size(); ++k) ok = bb[k] > bb[k - 1] && bb[k] % L == 0;
+    if (!ok) throw Error("blob_bounds must rise from 0 to the global range in whole work-groups (event pipeline)");
+    for (const auto& a : c.arrays)
+      if (!a.blob_begin.empty() && (a.blob_begin.size() != bb.size() - 1 || a.blob_count.size() != bb.size() - 1))
+        throw Error("an array's blob slices must have one entry per blob");
+    int holders = 0;
+    for (int i = 0; i < D; ++i) holders += st.ranges[i] > 0;
+    if (holders != 1) pipelined = false;  // split over devices: the plain path
+  } else {
+    for (int i = 0; i < D && pipelined; ++i)
+      if (st.ranges[i] != 0 && (st.ranges[i] % (B * U) != 0 || st.ranges[i] < B * U)) pipelined = false;
+  }
   if (collective(c)) pipelined = false;
 
   std::vector<double> ms(nloc, 0.0);

@@ -46,6 +46,11 @@ struct ComputeCall {
   // a multiple of it, e.g. to keep the K-split work-groups of one GEMM tile
   // on the same device.  Must be a multiple of local_range.
   long long granularity = 0;
+  // Explicit, possibly uneven pipeline blobs (event pipeline, one device
+  // holding the whole range): blob k = work items [blob_bounds[k],
+  // blob_bounds[k+1]) of the range; blobs alternate between the two
+  // half-pipelines.  Arrays may carry per-blob slices (ArraySpec::blob_begin).
+  std::vector<long long> blob_bounds;
 };
 
 struct CoresConfig {

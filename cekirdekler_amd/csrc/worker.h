@@ -44,6 +44,11 @@ struct ArraySpec {
   bool gather = false;
   int epw = 1;            // elements per work item
   int epg = 0;            // >0: elements per work-GROUP instead (per-group outputs)
+  // explicit blob slices (event pipeline with ComputeCall::blob_bounds):
+  // blob k moves elements [blob_begin[k], blob_begin[k] + blob_count[k])
+  // instead of the slice proportional to its work items — e.g. blob k of a
+  // square-shell GEMM needs row panel k of A and of B
+  std::vector<uint64_t> blob_begin, blob_count;
   // Element slice [begin, begin+count) owned by work items [ref, ref+range).
   void slice(long long ref, long long range, long long local, uint64_t& begin, uint64_t& count) const {
     if (epg > 0) {

@@ -79,9 +79,8 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   // XCD's L2 instead of re-fetched per tile.  C storage stays tile-major by
   // t, so a device's contiguous tile range is still one contiguous slice.
   const int ntn = N / BN, ntm = M / BM;
-  const int per_group = GM * ntn, grp = (int)(t / per_group), first = grp * GM;
-  const int gsz = min(ntm - first, GM), in_g = (int)(t % per_group);
-  const int tm = first + in_g % gsz, tn = in_g / gsz;
+  int tm, tn;
+  cek_tile_coords(t, ntm, ntn, GM, dims[6], tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
   // Staging: instruction `ins` of this wave fills LDS bytes [ins·1 KiB, +1 KiB)

@@ -38,9 +38,8 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
   const int wr = wave / WN, wc = wave % WN;
   const long long t = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
   const int ntn = N / BN, ntm = M / BM;
-  const int per_group = GM * ntn, grp = (int)(t / per_group), first = grp * GM;
-  const int gsz = min(ntm - first, GM), in_g = (int)(t % per_group);
-  const int tm = first + in_g % gsz, tn = in_g / gsz;
+  int tm, tn;
+  cek_tile_coords(t, ntm, ntn, GM, dims[6], tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
   // staging: lane l of a wave instruction lands at row ins·8 + l/8, physical
@@ -292,9 +291,8 @@ __device__ __forceinline__ void gemm_f32w_tile(const int* __restrict__ dims, con
   const int wr = wave / WN, wc = wave % WN;
   const long long t = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
   const int ntn = N / BN, ntm = M / BM;
-  const int per_group = GM * ntn, grp = (int)(t / per_group), first = grp * GM;
-  const int gsz = min(ntm - first, GM), in_g = (int)(t % per_group);
-  const int tm = first + in_g % gsz, tn = in_g / gsz;
+  int tm, tn;
+  cek_tile_coords(t, ntm, ntn, GM, dims[6], tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int lrow = lane >> 3, lchunk = (lane & 7) ^ (lrow & 7);

@@ -52,3 +52,46 @@ def test_pipeline_schedule_stream_layouts(layout):
     cpu = ck.ClPlatforms.all().cpus(True)
     sched = _record(cpu + cpu, ck.PIPELINE_EVENT, 4, **layout)
     assert check_pipeline_schedule(sched) == 8
+
+
+def test_explicit_uneven_blobs_with_array_slices():
+    """Explicit pipeline blobs (compute(..., pipeline_blobs=[0, b1, ..., G])):
+    uneven work-item ranges, alternating half-pipelines, and per-blob array
+    slices that are NOT proportional to the blob's work items (blob k of a
+    shell-streamed GEMM uploads row panel k of A and B).  The recorded
+    schedule keeps H2D → kernel → D2H per blob, and the result is right."""
+    src = """__global__ void k(const float* x, const float* w, float* y) {
+      long long i = get_global_id(0); y[i] = x[i] * 2.0f + w[i % 64]; }"""
+    cpu = ck.ClPlatforms.all().cpus(True)
+    cr = ck.ClNumberCruncher(cpu, src)
+    cr.cores.record_schedule = True
+    bounds = [0, 64, 256, 576, 1024]  # 1, 3, 5, 7 work-groups of 64: a shell-like progression
+    n = bounds[-1]
+    x = ck.ClArray(np.arange(n, dtype=np.float32))
+    x.partial_read = True
+    x.write = False
+    w = ck.ClArray(np.arange(256, dtype=np.float32))  # 4 panels of 64: blob k uploads panel k
+    w.partial_read = True
+    w.write = False
+    w.blob_slices = [(64 * k, 64) for k in range(4)]
+    y = ck.ClArray(np.zeros(n, np.float32))
+    y.read = False
+    x.next_param(w, y).compute(cr, 1, "k", n, 64, 0, True, ck.PIPELINE_EVENT, bounds)
+    np.testing.assert_array_equal(y.array, 2 * x.array + w.array[np.arange(n) % 64])
+    sched = cr.cores.schedule()
+    kernels = [(o[3], o[4], o[2]) for o in sched if o[1] == "kernel"]
+    assert [(b, c) for b, c, _ in kernels] == [(0, 64), (64, 192), (256, 320), (576, 448)]
+    assert [s for _, _, s in kernels] == [18, 21, 18, 21]  # halves alternate
+    assert check_pipeline_schedule(sched) == 4
+    assert cr.last_record()["pipelined"]
+    cr.dispose()
+
+
+def test_explicit_blob_bounds_validated():
+    cpu = ck.ClPlatforms.all().cpus(True)
+    cr = ck.ClNumberCruncher(cpu, SRC)
+    x = ck.ClArray(np.zeros(256, np.float32))
+    y = ck.ClArray(np.zeros(256, np.float32))
+    with pytest.raises(Exception):
+        x.next_param(y).compute(cr, 1, "k", 256, 64, 0, True, ck.PIPELINE_EVENT, [0, 100, 256])
+    cr.dispose()
