@@ -182,18 +182,22 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     ms_host = timed(ctx, host_step, host_steps, 2)
     # the streamed host-resident output: this rank's tiles of the host C
     err_host = _max_over_ranks(ctx, g.verify(compute_id=2, host=True))
-    ms_blobs, mode = ms_host, f"blob pipeline, {blobs} blobs" if blobs else "serial 3-phase"
-    ms_shells = None
+    ms_blobs, mode = ms_host, f"compute() event pipeline, {blobs} equal blobs" if blobs else "compute() serial 3-phase"
+    ms_shells = ms_native_shells = None
     panels = HOST_RESIDENT_PANELS
     if ctx.world == 1 and g.split_k == 1 and size % panels == 0 and (size // panels) % max(g.BM, g.BN) == 0:
-        # one GPU holds the whole problem: the square-shell stream
-        # (Cores::gemm_host_shells), whose first kernels need two panels
-        # instead of all of B; reported when it is the faster path
-        # (a GEMM-specific entry point outside compute(): reported on its own,
-        # never as the host-resident number)
-        ms_shells = timed(ctx, lambda: g.run_host_shells(panels), host_steps, 2)
-        err_shells = g.verify_shells(panels)
+        # one GPU holds the whole problem: the square-shell stream through
+        # compute() — the event pipeline with explicit, uneven blobs (blob s =
+        # shell s; A and B go up one row panel per blob), whose first kernels
+        # need two panels instead of all of B
+        ms_shells = timed(ctx, lambda: g.run_shells(panels, compute_id=3), host_steps, 2)
+        err_shells = g.verify(compute_id=3, host=True)
         err_host = max(err_host, err_shells)
+        if ms_shells < ms_host:
+            ms_host, mode = ms_shells, f"compute() event pipeline, {panels} shell blobs"
+        # the same schedule through its dedicated native entry point, for comparison
+        ms_native_shells = timed(ctx, lambda: g.run_host_shells(panels), host_steps, 2)
+        err_host = max(err_host, g.verify_shells(panels))
     cr.dispose()
     for a in (g.A, g.B, g.C, g.dims):
         a.dispose()  # release 0.5 GB of pinned host memory before the next config
@@ -203,6 +207,7 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
             "host_resident_blobs": blobs, "host_resident_calls_ms": [round(x, 3) for x in host_calls],
             "host_resident_pipelined": host_piped, "host_resident_mode": mode,
             "host_resident_blob_pipeline_ms": ms_blobs, "host_resident_shells_ms": ms_shells,
+            "host_resident_native_shells_ms": ms_native_shells,
             "ranges": ranges, "max_rel_err": max(err, err_host), "max_rel_err_host_resident": err_host,
             "handover_fallbacks": fallbacks, "device": "gpu"}
 
@@ -574,6 +579,7 @@ def main(argv=None) -> int:
                 "sgemm_host_resident_mode": sg.get("host_resident_mode"),
                 "sgemm_host_resident_blob_pipeline_ms": sg.get("host_resident_blob_pipeline_ms"),
                 "sgemm_host_resident_shells_ms": sg.get("host_resident_shells_ms"),
+                "sgemm_host_resident_native_shells_ms": sg.get("host_resident_native_shells_ms"),
                 "sgemm_max_rel_err": sg["max_rel_err"],
                 "sgemm_handover_fallbacks": sg["handover_fallbacks"],
                 "sgemm_balancer_setup_calls": sg["balancer_setup_calls"],

@@ -1151,12 +1151,18 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
   auto gathered = [&](const ArraySpec& a) {
     return comm_ && !a.zc && !a.write_all && (a.gather || (dist_gather_writes && (a.write || a.wo)));
   };
-  // phase 1: host → device (partial slice wins over full read)
+  // phase 1: host → device (partial slice wins over full read; an array
+  // with explicit blob slices, run without its pipeline, goes up whole)
   for (auto& a : c.arrays) {
     if (a.zc) continue;
     if (a.partial) {
       uint64_t b, n;
-      a.slice(ref, range, c.local_range, b, n);
+      if (!a.blob_begin.empty()) {
+        b = 0;
+        n = a.bytes / a.elem_size;
+      } else {
+        a.slice(ref, range, c.local_range, b, n);
+      }
       wk.h2d(s, a, b, n);
       *h2d += n * a.elem_size;
     }

@@ -112,24 +112,53 @@ def from_bf16_bits(b: np.ndarray) -> np.ndarray:
     return (b.astype(np.uint32) << 16).view(np.float32)
 
 
-def tile_coords(t: np.ndarray, M: int, N: int, BM: int, BN: int, group_m: int):
-    """Tile index → (tile row, tile col) under the kernel's grouped order."""
+def tile_coords(t: np.ndarray, M: int, N: int, BM: int, BN: int, group_m: int, panels: int = 0):
+    """Tile index → (tile row, tile col) under the kernel's order
+    (``cek_tile_coords`` in kernels/cek_kernel.h): grouped rows, or square
+    shells of ``panels`` row panels (shell s = R_s then C_s)."""
+    t = np.asarray(t)
     ntm, ntn = M // BM, N // BN
-    gm = max(1, group_m)
-    per = gm * ntn
-    first = (t // per) * gm
-    gsz = np.minimum(ntm - first, gm)
-    in_g = t % per
-    return first + in_g % gsz, in_g // gsz
+
+    def grouped(r, rows, cols):
+        gm = max(1, group_m)
+        per = gm * cols
+        first = (r // per) * gm
+        gsz = np.minimum(rows - first, gm)
+        in_g = r % per
+        return first + in_g % gsz, in_g // gsz
+
+    if panels <= 0:
+        return grouped(t, ntm, ntn)
+    pm, pn = ntm // panels, ntn // panels
+    tm = np.empty_like(t)
+    tn = np.empty_like(t)
+    s = np.floor(np.sqrt(t // (pm * pn))).astype(np.int64)
+    s = np.where((s + 1) ** 2 * pm * pn <= t, s + 1, s)
+    s = np.where(s * s * pm * pn > t, s - 1, s)
+    r = t - s * s * pm * pn
+    r_tiles = pm * (s + 1) * pn
+    for sh in np.unique(s):
+        sel = s == sh
+        rr = r[sel]
+        isr = rr < r_tiles[sel]
+        a, b = grouped(rr[isr], pm, (sh + 1) * pn)
+        c, d = grouped(rr[~isr] - pm * (sh + 1) * pn, max(sh * pm, 1), pn)
+        out_m = np.empty(rr.shape, t.dtype)
+        out_n = np.empty(rr.shape, t.dtype)
+        out_m[isr], out_n[isr] = a + sh * pm, b
+        out_m[~isr], out_n[~isr] = c, d + sh * pn
+        tm[sel], tn[sel] = out_m, out_n
+    return tm, tn
 
 
-def untile(c: np.ndarray, M: int, N: int, BM: int, BN: int, group_m: int = 1, geom=None) -> np.ndarray:
-    """Tile-major C (grouped tile order) → row-major [M][N]; ``geom``: the
-    tile's wave geometry when its elements are in fragment order (bf16
-    kernels), None for row-major tiles."""
+def untile(c: np.ndarray, M: int, N: int, BM: int, BN: int, group_m: int = 1, geom=None,
+           panels: int = 0) -> np.ndarray:
+    """Tile-major C (the kernel's tile order) → row-major [M][N]; ``geom``:
+    the tile's wave geometry when its elements are in fragment order (bf16
+    kernels), None for row-major tiles; ``panels``: shell order."""
     ntm, ntn = M // BM, N // BN
     tiles = c.reshape(ntm * ntn, BM, BN) if geom is None else tile_to_rows(c.reshape(ntm * ntn, BM * BN), geom)
-    tm, tn = tile_coords(np.arange(ntm * ntn), M, N, BM, BN, group_m)
+    tm, tn = tile_coords(np.arange(ntm * ntn), M, N, BM, BN, group_m, panels)
     out = np.empty((ntm, ntn, BM, BN), c.dtype)
     out[tm, tn] = tiles
     return out.transpose(0, 2, 1, 3).reshape(M, N)
@@ -196,6 +225,7 @@ class GemmBf16:
             self.B.array[:] = to_bf16_bits(rng.uniform(-1, 1, N * K).astype(np.float32))
         self._uploaded = False
         self.wave_granularity = wave_granularity
+        self._orders = {}  # compute id -> shell panels of its tile order (0: grouped)
 
     def granularity(self) -> int:
         """Balancer unit in work items.  One tile (all its K-splits) by
@@ -249,6 +279,7 @@ class GemmBf16:
         (``partial``) and every blob's C tiles come down while later blobs'
         panels upload and compute, on the two half-pipelines' streams."""
         first = not self._uploaded
+        self._orders[compute_id] = 0
         streamed = bool(stream_blobs) and not resident
         if streamed and not self.can_stream():
             raise ValueError("stream_blobs needs split_k == 1, whole tile groups and an integral A panel "
@@ -269,6 +300,53 @@ class GemmBf16:
             pipeline=streamed, pipeline_type=stream_event, pipeline_blobs=max(1, stream_blobs),
             granularity=gran)
         self._uploaded = True
+
+    def shell_bounds(self, panels: int):
+        """Work-item bounds of the square shells (blob s = shell s) and the
+        per-blob row panels of A and B, for :meth:`run_shells`."""
+        P = int(panels)
+        if self.split_k != 1:
+            raise ValueError("shell streaming runs single-pass tiles (split_k == 1)")
+        if P < 1 or self.M % P or self.N % P or (self.M // P) % self.BM or (self.N // P) % self.BN:
+            raise ValueError(f"M and N must split into {P} panels of whole {self.BM}x{self.BN} tiles")
+        pm, pn = self.M // P // self.BM, self.N // P // self.BN
+        bounds = [pm * pn * (s * s) * self.L for s in range(P + 1)]
+        a_rows, b_rows = self.M // P, self.N // P
+        a_sl = [(k * a_rows * self.K, a_rows * self.K) for k in range(P)]
+        b_sl = [(k * b_rows * self.K, b_rows * self.K) for k in range(P)]
+        return bounds, a_sl, b_sl
+
+    def run_shells(self, panels: int = 16, compute_id: int = 2) -> None:
+        """One host-resident call through ``compute()``: the event-driven
+        read/compute/write pipeline with explicit, uneven blobs — blob s is
+        square shell s (``R_s = A_s·B[0..s]ᵀ`` then ``C_s = A[0..s-1]·B_sᵀ``,
+        the kernels' shell tile order, ``dims[6] = panels``), A and B go up
+        one row panel per blob (``ClArray.blob_slices``) on the upload stream
+        and every shell's C comes down (one contiguous range) while later
+        panels go up.  The first kernels need two panels instead of all of
+        B.  One device holds the range (several: the plain path)."""
+        bounds, a_sl, b_sl = self.shell_bounds(panels)
+        if getattr(self, "_dims_shell", None) is None or int(self._dims_shell.array[6]) != panels:
+            d = self.dims.array.copy()
+            d[6] = panels
+            self._dims_shell = ClArray(d)
+            self._dims_shell.write = False
+        self._orders[compute_id] = int(panels)
+        saved = [(a.read, a.partial_read, a.blob_slices) for a in (self.A, self.B)]
+        try:
+            for a, sl in ((self.A, a_sl), (self.B, b_sl)):
+                a.partial_read = True
+                a.blob_slices = sl
+            self.C.write = True
+            self._dims_shell.read = True
+            self._dims_shell.next_param(self.A, self.B, self.C).compute(
+                self.cr, compute_id, self.kernel, self.global_range, self.L, pipeline=True,
+                pipeline_blobs=bounds, granularity=self.granularity())
+        finally:
+            for a, (r, pr, bs) in zip((self.A, self.B), saved):
+                a.partial_read, a.blob_slices = pr, bs
+                a.read = r
+        self._uploaded = False  # the device copies of A/B were streamed, not kept whole
 
     def run_host_shells(self, panels: int = 8, device: int = 0) -> None:
         """One host-resident call streamed in square shells
@@ -329,7 +407,8 @@ class GemmBf16:
                 g = self.cr._cores.global_base + dev
                 lo, n = refs[g] * e, rng[g] * e
                 self._download_slice(dev, lo, n)
-        return untile(self.C.array, self.M, self.N, self.BM, self.BN, self.group_m, self.geom)
+        return untile(self.C.array, self.M, self.N, self.BM, self.BN, self.group_m, self.geom,
+                      self._orders.get(self.cr._cores.last_compute_id, 0))
 
     def tile_block(self, flat: np.ndarray) -> np.ndarray:
         """One C tile as stored (``BM·BN`` floats) → row-major ``[BM][BN]``."""
@@ -381,7 +460,8 @@ class GemmBf16:
             picks = {t0, t0 + nt - 1}
             picks.update((t0 + rng.choice(nt, size=min(nt, tiles_per_device), replace=False)).tolist())
             picks = np.array(sorted(picks))
-            tm, tn = tile_coords(picks, self.M, self.N, self.BM, self.BN, self.group_m)
+            tm, tn = tile_coords(picks, self.M, self.N, self.BM, self.BN, self.group_m,
+                                 self._orders.get(compute_id, 0))
             for t, r, c in zip(picks, tm, tn):
                 got = self.tile_block(self.C.array[t * tile:(t + 1) * tile]).astype(np.float64)
                 ref = (a[r * self.BM:(r + 1) * self.BM].astype(np.float64)
@@ -442,6 +522,7 @@ class GemmF32(GemmBf16):
             self.B.array[:] = rng.uniform(-1, 1, N * K).astype(np.float32)
         self._uploaded = False
         self.wave_granularity = wave_granularity
+        self._orders = {}
 
     def reference(self, rows: slice = slice(None)) -> np.ndarray:
         a = self.A.array.reshape(self.M, self.K)[rows].astype(np.float64)

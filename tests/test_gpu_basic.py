@@ -346,3 +346,31 @@ def test_mandelbrot_two_frames_in_flight_async_enqueue():
         img = m.out.array.reshape(m.height, m.width)
         assert np.mean(img != ref) < 2e-3
     cr.dispose()
+
+
+@pytest.mark.parametrize("tile,panels", [("256x256pb", 4), ("256x256pb", 2), ("256x128pe", 4)])
+def test_gemm_shells_through_compute(tile, panels):
+    """Host-resident GEMM streamed in square shells THROUGH compute(): the
+    event pipeline with explicit uneven blobs (blob s = shell s), A and B
+    uploaded one row panel per blob, C downloaded shell by shell — the
+    kernels' shell tile order (dims[6]) untiled on the host."""
+    from cekirdekler_amd.ops.gemm import GEMM_LIBS, GemmBf16
+    from cekirdekler_amd.ops.library import library
+
+    cr = ck.ClNumberCruncher(_gpu()[0], "", prebuilt=library(*GEMM_LIBS))
+    g = GemmBf16(1024, 1024, 512, cruncher=cr, tile=tile)
+    ref = g.reference()
+    for _ in range(2):
+        g.C.array[:] = np.nan
+        g.run_shells(panels, compute_id=3)
+        rec = cr.last_record()
+        assert rec["pipelined"], rec
+        assert rec["h2d_bytes"] == g.A.array.nbytes + g.B.array.nbytes + g.dims.array.nbytes, rec
+        assert rec["d2h_bytes"] == g.C.array.nbytes, rec
+        c = g.result(download=False)
+        assert np.abs(c - ref).max() < 1e-3 * np.abs(ref).max()
+    assert g.verify(compute_id=3, host=True) < 5e-3
+    # a resident grouped-order run afterwards is unaffected by the shell dims
+    g.run(compute_id=1, resident=True)
+    assert g.verify(compute_id=1) < 5e-3
+    cr.dispose()

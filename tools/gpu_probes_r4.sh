@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-4 probes on one GPU: host fan-out cost and pool throughput (both
+# worker hand-off modes), PCIe duplex beside a CU-masked busy kernel, and
+# the N-body force-kernel variants.  Each step has its own time limit; the
+# first failing step ends the call.
+set -o pipefail
+out=${1:-gpurun_out/probes}
+mkdir -p "$out"
+CEK_SPIN_US=0 timeout -k 10 180 python tools/fanout_probe.py "$out/fanout_spin0.json" > "$out/fanout0.log" 2>&1 || exit $?
+timeout -k 10 180 python tools/fanout_probe.py "$out/fanout_spin50.json" > "$out/fanout50.log" 2>&1 || exit $?
+timeout -k 10 120 ./tools/microbench/pcie_cumask > "$out/pcie_cumask.json" 2> "$out/pcie_cumask.err" || exit $?
+timeout -k 10 240 python tools/nbody_force_variants.py 1048576 1,0.5,0.25 "$out/nbody_variants.json" > "$out/nbody_variants.log" 2>&1 || exit $?
