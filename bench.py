@@ -297,6 +297,61 @@ def bench_mandelbrot(ctx, steps, warmup):
     return out
 
 
+def _row_major_comparison(steps: int) -> dict:
+    """Like-for-like layout check: the headline kernel with a
+    row-major C epilogue (``256x256pbr``) at 8192³ through compute() in
+    enqueue mode, and hipBLASLt (torch.mm, bf16 in, fp32 out, row-major C)
+    at the same shape on the same GPU, each the median of 5 timed runs."""
+    import statistics
+
+    import torch
+
+    import cekirdekler_amd as ck
+    from cekirdekler_amd.ops.gemm import GEMM_LIBS, GemmBf16
+    from cekirdekler_amd.ops.library import library
+
+    size = 8192
+    flops = 2.0 * size ** 3
+    cr = ck.ClNumberCruncher(ck.ClPlatforms.all().gpus()[0], "", prebuilt=library(*GEMM_LIBS))
+    g = GemmBf16(size, size, size, cruncher=cr, tile="256x256pbr")
+    g.run(compute_id=1, resident=True)
+    runs = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        cr.enqueue_mode = True
+        for _ in range(steps):
+            g.run(compute_id=1, resident=True)
+        cr.enqueue_mode = False
+        torch.cuda.synchronize()
+        runs.append((time.perf_counter() - t0) / steps)
+    err = g.verify(compute_id=1, tiles_per_device=4)
+    cr.dispose()
+    for arr in (g.A, g.B, g.C, g.dims):
+        arr.dispose()
+    out = {"tile": "256x256pbr", "gflops": round(flops / statistics.median(runs) / 1e9, 1), "max_rel_err": err}
+    try:
+        a = torch.randn(size, size, device="cuda", dtype=torch.bfloat16)
+        b = torch.randn(size, size, device="cuda", dtype=torch.bfloat16).T
+        for _ in range(3):
+            c = torch.mm(a, b, out_dtype=torch.float32)
+        ts = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                c = torch.mm(a, b, out_dtype=torch.float32)
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) / steps)
+        out["hipblaslt_fp32_out_gflops"] = round(flops / statistics.median(ts) / 1e9, 1)
+        out["vs_hipblaslt"] = round(out["gflops"] / out["hipblaslt_fp32_out_gflops"], 4)
+        del a, b, c
+        torch.cuda.empty_cache()
+    except Exception as e:  # pragma: no cover
+        out["hipblaslt_error"] = repr(e)[:200]
+    return out
+
+
 def _mandelbrot_kernel_only(kernel: str = "blk8u", reps: int = 20) -> dict:
     """The fastest Mandelbrot kernel alone on this rank's GPU (image left in
     device memory, no D2H, calls enqueued back to back in enqueue mode):
@@ -539,6 +594,12 @@ def main(argv=None) -> int:
     all_ranges = _all_ranges(ctx, sg["ranges"])
     mb = {} if (args.skip_mandelbrot or not use_gpu) else bench_mandelbrot(ctx, args.steps, args.warmup)
     lb = bench_lb_iters() if (ctx.rank == 0 and use_gpu) else {}
+    rowc = {}
+    if ctx.rank == 0 and use_gpu and args.size == 8192:
+        try:  # an extra: a failure is reported in its field
+            rowc = _row_major_comparison(args.steps)
+        except Exception as e:  # pragma: no cover
+            rowc = {"error": repr(e)[:300]}
     if ctx.is_distributed:
         import torch.distributed as dist
 
@@ -585,6 +646,8 @@ def main(argv=None) -> int:
                 "sgemm_balancer_setup_calls": sg["balancer_setup_calls"],
                 "sgemm_ranges": sg["ranges"],
                 "sgemm_ranges_identical_on_all_ranks": all(r == all_ranges[0] for r in all_ranges),
+                "sgemm_row_major_c_gflops": rowc.get("gflops"),
+                "sgemm_row_major_c": rowc,
                 "mandelbrot_4k": mb,
                 "load_balance_iters": lb,
                 "nbody_pipeline": node.get("nbody_pipeline"),

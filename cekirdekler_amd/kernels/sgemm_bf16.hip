@@ -37,7 +37,7 @@
 
 namespace {
 
-template <int WM, int WN, int FM, int FN, int MODE, bool SK = false, int XCH = 0>
+template <int WM, int WN, int FM, int FN, int MODE, bool SK = false, int XCH = 0, bool ROWC = false>
 __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
                                           const uint16_t* __restrict__ A,
                                           const uint16_t* __restrict__ Bt, float* __restrict__ C,
@@ -597,11 +597,42 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   // work-group per CU the store tail is exposed).  Host side: ops/gemm.py
   // tile_to_rows.  Element (row, col) of the tile lives at
   // ((((wr·WN + wc)·FM + i)·FN + j)·64 + fq·16 + fr)·4 + r.
-  f32x4* ct = reinterpret_cast<f32x4*>(C + (size_t)t * BM * BN);
+  if constexpr (ROWC) {
+    // Row-major C ([M][N], ldc = N): a lane holds 4 consecutive ROWS of one
+    // column per fragment, so each wave turns its 16-row strips around in
+    // LDS (4 KiB + padding per wave; the main loop is done with LDS): lane
+    // (fq, fr) writes fragment j's rows fq·4 + r at column j·16 + fr, then
+    // every lane reads 16 B of one row and stores it — 16 lanes cover a
+    // 256-B row segment, one dwordx4 per lane per 4 rows.  Row stride 68
+    // floats: the two 16-lane halves of a 32-lane write group fall on
+    // different banks.
+    constexpr int RS = 16 * FN + 4;
+    __syncthreads();
+    float* strip = reinterpret_cast<float*>(smem) + wave * 16 * RS;
+    const int rrow = lane >> 4, rcol = (lane & 15) * 4;
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+    for (int i = 0; i < FM; ++i) {
 #pragma unroll
-    for (int j = 0; j < FN; ++j) ct[(((wr * WN + wc) * FM + i) * FN + j) * 64 + lane] = acc[i][j];
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) strip[(fq * 4 + r) * RS + j * 16 + fr] = acc[i][j][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's strip is written
+#pragma unroll
+      for (int q = 0; q < 16 / 4; ++q) {
+        const int row = q * 4 + rrow;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(strip + row * RS + rcol);
+        const size_t grow = (size_t)m0 + wr * 16 * FM + i * 16 + row;
+        *reinterpret_cast<f32x4*>(C + grow * N + n0 + wc * 16 * FN + rcol) = v;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the strip is rewritten
+    }
+  } else {
+    f32x4* ct = reinterpret_cast<f32x4*>(C + (size_t)t * BM * BN);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) ct[(((wr * WN + wc) * FM + i) * FN + j) * 64 + lane] = acc[i][j];
+  }
 #ifdef CEK_TS_END
   CEK_TS_END;
 #endif
@@ -654,6 +685,12 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sw(
 // Balanced-DMA ping-pong (MODE 4):
 // 160 KiB LDS at 256², 128 KiB at 256×128.
 CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x256pb, 2, 4, 8, 4, 4)
+// the same with C row-major ([M][N]) through an LDS turn-around per wave
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pbr(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
+  gemm_tile<2, 4, 8, 4, 4, false, 0, true>(dims, A, Bt, C, smem, __cek_off);
+}
 CEK_GEMM_B3_KERNEL(cek_sgemm_bf16_256x128pb, 4, 2, 4, 4, 4)
 
 // Even chunk-split DMA with three whole stages (MODE 6): 144 KiB at 256×128.

@@ -27,6 +27,11 @@ TILES = {
     # balanced-DMA ping-pong (G0 stages A, G1 stages Bt two K-tiles ahead):
     # the full-problem tile (1.47-1.50 PF at 8192³)
     "256x256pb": (256, 256, 512, "cek_sgemm_bf16_256x256pb"),
+    # the same kernel with C row-major [M][N] (an LDS turn-around per wave in
+    # the epilogue): the layout hipBLASLt writes, for like-for-like numbers;
+    # device-resident computes only (a device's slice of C is one block of
+    # rows only when its tile range is whole tile groups)
+    "256x256pbr": (256, 256, 512, "cek_sgemm_bf16_256x256pbr"),
     # uneven split-K = 2 (the helper runs `exchange_shift` K-tiles fewer and
     # hands its whole partial to the owner while the owner still multiplies):
     # the 8-GPU slice (1024 rows of 8192², 128 tiles for 256 CUs).  The
@@ -50,7 +55,7 @@ GEMM_LIBS = ("sgemm_bf16",)
 # each): the kernels store a C tile in fragment order (one dwordx4 per lane
 # per fragment), which tile_to_rows / rows_to_tile convert.
 TILE_WAVES = {
-    "256x256pb": (2, 4, 8, 4), "256x256pbw": (2, 4, 8, 4), "256x256": (2, 4, 8, 4), "256x256pp": (2, 4, 8, 4),
+    "256x256pb": (2, 4, 8, 4), "256x256pbr": (2, 4, 8, 4), "256x256pbw": (2, 4, 8, 4), "256x256": (2, 4, 8, 4), "256x256pp": (2, 4, 8, 4),
     "256x128pe": (4, 2, 4, 4), "256x128pb": (4, 2, 4, 4), "128x128": (2, 2, 4, 4),
 }
 
@@ -92,6 +97,8 @@ F32_TILES = {
     "128x128": (128, 128, 256, "cek_sgemm_f32_128x128"),
 }
 
+# tiles whose kernel stores C row-major ([M][N]) instead of tile-major
+ROW_MAJOR_TILES = {"256x256pbr"}
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
 SPLIT_K_TILES = {"256x256pp", "256x256pb"}
 # tiles whose kernel always runs two K-splits with a hand-over (flag words per tile)
@@ -190,6 +197,7 @@ class GemmBf16:
         self.exchange_shift = shift
         self.M, self.N, self.K, self.BM, self.BN, self.L, self.kernel = M, N, K, BM, BN, L, kname
         self.geom = TILE_WAVES[tile]  # C tiles in fragment order
+        self.row_major_c = tile in ROW_MAJOR_TILES
         self.split_k = max(1, int(split_k))
         self.tiles = (M // BM) * (N // BN)
         self.global_range = self.tiles * self.split_k * L
@@ -278,6 +286,8 @@ class GemmBf16:
         per device — B is a full read, A goes up one row panel per blob
         (``partial``) and every blob's C tiles come down while later blobs'
         panels upload and compute, on the two half-pipelines' streams."""
+        if self.row_major_c and not resident:
+            raise ValueError("row-major C tiles run device-resident computes only")
         first = not self._uploaded
         self._orders[compute_id] = 0
         streamed = bool(stream_blobs) and not resident
@@ -407,6 +417,8 @@ class GemmBf16:
                 g = self.cr._cores.global_base + dev
                 lo, n = refs[g] * e, rng[g] * e
                 self._download_slice(dev, lo, n)
+        if getattr(self, "row_major_c", False):
+            return self.C.array.reshape(self.M, self.N).copy()
         return untile(self.C.array, self.M, self.N, self.BM, self.BN, self.group_m, self.geom,
                       self._orders.get(self.cr._cores.last_compute_id, 0))
 
@@ -463,7 +475,11 @@ class GemmBf16:
             tm, tn = tile_coords(picks, self.M, self.N, self.BM, self.BN, self.group_m,
                                  self._orders.get(compute_id, 0))
             for t, r, c in zip(picks, tm, tn):
-                got = self.tile_block(self.C.array[t * tile:(t + 1) * tile]).astype(np.float64)
+                if getattr(self, "row_major_c", False):
+                    got = self.C.array.reshape(self.M, self.N)[r * self.BM:(r + 1) * self.BM,
+                                                               c * self.BN:(c + 1) * self.BN].astype(np.float64)
+                else:
+                    got = self.tile_block(self.C.array[t * tile:(t + 1) * tile]).astype(np.float64)
                 ref = (a[r * self.BM:(r + 1) * self.BM].astype(np.float64)
                        @ b[c * self.BN:(c + 1) * self.BN].astype(np.float64).T)
                 worst = max(worst, float(np.max(np.abs(got - ref)) / max(float(np.max(np.abs(ref))), 1e-30)))

@@ -17,6 +17,7 @@ LIBRARY = {
     # production tiles plus at most two tested alternates each (the measured
     # losers of rounds 1-2 live in git history and profiles/gemm_*.md)
     "sgemm_bf16": ["cek_sgemm_bf16_256x256", "cek_sgemm_bf16_256x256pp", "cek_sgemm_bf16_256x256pb",
+                   "cek_sgemm_bf16_256x256pbr",
                    "cek_sgemm_bf16_256x128pb", "cek_sgemm_bf16_256x128pe", "cek_sgemm_bf16_128x128",
                    "cek_sgemm_bf16_256x256pp_sk", "cek_sgemm_bf16_256x256pb_sk",
                    "cek_sgemm_bf16_256x256pb_sw"],

@@ -374,3 +374,28 @@ def test_gemm_shells_through_compute(tile, panels):
     g.run(compute_id=1, resident=True)
     assert g.verify(compute_id=1) < 5e-3
     cr.dispose()
+
+
+def test_gemm_row_major_c_variant():
+    """256x256pbr: the production kernel with a row-major C epilogue (LDS
+    turn-around per wave) — bit-identical to the fragment-order kernel's C
+    after untiling, and right against float64."""
+    from cekirdekler_amd.ops.gemm import GEMM_LIBS, GemmBf16
+    from cekirdekler_amd.ops.library import library
+
+    cr = ck.ClNumberCruncher(_gpu()[0], "", prebuilt=library(*GEMM_LIBS))
+    frag = GemmBf16(1024, 1536, 512, cruncher=cr, tile="256x256pb")
+    rowc = GemmBf16(1024, 1536, 512, cruncher=cr, tile="256x256pbr")
+    rowc.A.array[:] = frag.A.array
+    rowc.B.array[:] = frag.B.array
+    frag.run(compute_id=1, resident=True)
+    rowc.run(compute_id=2, resident=True)
+    a = frag.result()
+    b = rowc.result()
+    np.testing.assert_array_equal(a, b)
+    ref = frag.reference()
+    assert np.abs(b - ref).max() < 1e-3 * np.abs(ref).max()
+    assert rowc.verify(compute_id=2) < 5e-3
+    with pytest.raises(ValueError):
+        rowc.run(compute_id=3, resident=False)
+    cr.dispose()
