@@ -183,7 +183,7 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     # the streamed host-resident output: this rank's tiles of the host C
     err_host = _max_over_ranks(ctx, g.verify(compute_id=2, host=True))
     ms_blobs, mode = ms_host, f"compute() event pipeline, {blobs} equal blobs" if blobs else "compute() serial 3-phase"
-    ms_shells = ms_native_shells = None
+    ms_shells = ms_native_shells = ms_shells_cu = None
     panels = HOST_RESIDENT_PANELS
     if ctx.world == 1 and g.split_k == 1 and size % panels == 0 and (size // panels) % max(g.BM, g.BN) == 0:
         # one GPU holds the whole problem: the square-shell stream through
@@ -195,6 +195,18 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
         err_host = max(err_host, err_shells)
         if ms_shells < ms_host:
             ms_host, mode = ms_shells, f"compute() event pipeline, {panels} shell blobs"
+        # the same with downloads by a copy kernel on CUs reserved for it
+        # (CU-masked streams): the downloads never wait for a GEMM
+        # work-group to leave a CU, so they run beside the SDMA uploads
+        try:
+            cr.copy_cus, cr.kernel_d2h = HOST_RESIDENT_COPY_CUS, True
+            ms_shells_cu = timed(ctx, lambda: g.run_shells(panels, compute_id=4), host_steps, 2)
+            err_host = max(err_host, g.verify(compute_id=4, host=True))
+        finally:
+            cr.kernel_d2h, cr.copy_cus = False, 0
+        if ms_shells_cu < ms_host:
+            ms_host, mode = ms_shells_cu, (f"compute() event pipeline, {panels} shell blobs, downloads by a copy "
+                                           f"kernel on {HOST_RESIDENT_COPY_CUS} reserved CUs")
         # the same schedule through its dedicated native entry point, for comparison
         ms_native_shells = timed(ctx, lambda: g.run_host_shells(panels), host_steps, 2)
         err_host = max(err_host, g.verify_shells(panels))
@@ -207,7 +219,7 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
             "host_resident_blobs": blobs, "host_resident_calls_ms": [round(x, 3) for x in host_calls],
             "host_resident_pipelined": host_piped, "host_resident_mode": mode,
             "host_resident_blob_pipeline_ms": ms_blobs, "host_resident_shells_ms": ms_shells,
-            "host_resident_native_shells_ms": ms_native_shells,
+            "host_resident_native_shells_ms": ms_native_shells, "host_resident_shells_copy_cus_ms": ms_shells_cu,
             "ranges": ranges, "max_rel_err": max(err, err_host), "max_rel_err_host_resident": err_host,
             "handover_fallbacks": fallbacks, "device": "gpu"}
 
@@ -521,6 +533,7 @@ MAX_REL_ERR = 5e-3
 NODE_CONFIGS_BUDGET_S = 360  # all of bench_node_configs' child processes together
 HOST_RESIDENT_BLOBS = 8
 HOST_RESIDENT_PANELS = 16
+HOST_RESIDENT_COPY_CUS = 8
 
 
 def _peer_topology(world: int) -> dict:
@@ -641,6 +654,7 @@ def main(argv=None) -> int:
                 "sgemm_host_resident_blob_pipeline_ms": sg.get("host_resident_blob_pipeline_ms"),
                 "sgemm_host_resident_shells_ms": sg.get("host_resident_shells_ms"),
                 "sgemm_host_resident_native_shells_ms": sg.get("host_resident_native_shells_ms"),
+                "sgemm_host_resident_shells_copy_cus_ms": sg.get("host_resident_shells_copy_cus_ms"),
                 "sgemm_max_rel_err": sg["max_rel_err"],
                 "sgemm_handover_fallbacks": sg["handover_fallbacks"],
                 "sgemm_balancer_setup_calls": sg["balancer_setup_calls"],

@@ -510,6 +510,20 @@ class ClNumberCruncher:
     def kernel_d2h(self, on: bool) -> None:
         self._cores.kernel_d2h = bool(on)
 
+    @property
+    def copy_cus(self) -> int:
+        """CUs per GPU reserved for copy kernels (0: none): the pipeline's
+        write streams run on those CUs only (CU-masked HIP streams) and
+        every other stream on the rest, so downloads by copy kernel
+        (``kernel_d2h``) never wait for a compute work-group to leave a CU
+        and overlap the SDMA uploads.  Setting it drains and re-creates the
+        streams."""
+        return int(self._cores.copy_cus) if self._cores else 0
+
+    @copy_cus.setter
+    def copy_cus(self, n: int) -> None:
+        self._cores.copy_cus = int(n)
+
     # ------------------------------------------------------------ xGMI read fan-out
     @property
     def peer_reads(self) -> bool:

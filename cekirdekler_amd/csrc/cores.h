@@ -228,6 +228,14 @@ class Cores {
     for (auto& w : workers_) w->kernel_d2h = on;
   }
   bool kernel_d2h() const { return !workers_.empty() && workers_[0]->kernel_d2h.load(); }
+  // CUs reserved per GPU for copy kernels (Worker::set_cu_reserve); drains
+  // and re-creates the streams
+  void set_copy_cus(int n) {
+    std::lock_guard<std::recursive_mutex> g(call_mu_);
+    if (capturing_) throw Error("copy CUs cannot change during a graph capture");
+    for (auto& w : workers_) w->set_cu_reserve(n);
+  }
+  int copy_cus() const { return workers_.empty() ? 0 : workers_[0]->cu_reserve(); }
   uint64_t kernel_d2h_bytes() const {
     uint64_t b = 0;
     for (auto& w : workers_) b += w->kernel_d2h_bytes();

@@ -246,32 +246,68 @@ void Worker::release_all() {
   bytes_allocated_ = 0;
 }
 
+hipStream_t Worker::new_stream(bool copy_cus) {
+  set_device();
+  hipStream_t s = nullptr;
+  if (cu_reserve_ <= 0) {
+    CEK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return s;
+  }
+  const int ncu = std::max(1, dev_.compute_units);
+  const int every = std::max(1, ncu / cu_reserve_);
+  std::vector<uint32_t> mask((ncu + 31) / 32, 0);
+  for (int cu = 0; cu < ncu; ++cu) {
+    const bool reserved = (cu % every) == every - 1 && cu / every < cu_reserve_;
+    if (reserved == copy_cus) mask[cu / 32] |= 1u << (cu % 32);
+  }
+  CEK_HIP(hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask.size()), mask.data()));
+  return s;
+}
+
+void Worker::destroy_streams() {
+  if (!gpu()) return;
+  sync_all();
+  set_device();
+  for (auto& dq : dyn_queues_) (void)hipFree(dq.second);
+  dyn_queues_.clear();
+  if (main_) (void)hipStreamDestroy(main_);
+  main_ = nullptr;
+  for (auto& s : cq_) {
+    if (s) (void)hipStreamDestroy(s);
+    s = nullptr;
+  }
+  for (auto& h : pq_)
+    for (auto& s : h) {
+      if (s) (void)hipStreamDestroy(s);
+      s = nullptr;
+    }
+}
+
+void Worker::set_cu_reserve(int n) {
+  if (!gpu()) return;
+  n = std::max(0, std::min(n, std::max(0, dev_.compute_units / 2)));
+  if (n == cu_reserve_) return;
+  destroy_streams();
+  cu_reserve_ = n;
+}
+
 hipStream_t Worker::main_stream() {
   if (!gpu()) return nullptr;
-  if (!main_) {
-    set_device();
-    CEK_HIP(hipStreamCreateWithFlags(&main_, hipStreamNonBlocking));
-  }
+  if (!main_) main_ = new_stream(false);
   return main_;
 }
 
 hipStream_t Worker::compute_stream(int i) {
   if (!gpu()) return nullptr;
   i %= 16;
-  if (!cq_[i]) {
-    set_device();
-    CEK_HIP(hipStreamCreateWithFlags(&cq_[i], hipStreamNonBlocking));
-  }
+  if (!cq_[i]) cq_[i] = new_stream(false);
   return cq_[i];
 }
 
 hipStream_t Worker::pipe_stream(int half, int role) {
   if (!gpu()) return nullptr;
   hipStream_t& s = pq_[half & 1][role % 3];
-  if (!s) {
-    set_device();
-    CEK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  }
+  if (!s) s = new_stream(role % 3 == 2);
   return s;
 }
 

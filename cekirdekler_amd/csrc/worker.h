@@ -106,6 +106,14 @@ class Worker {
   hipStream_t main_stream();
   hipStream_t compute_stream(int i);        // i in [0, queue_concurrency)
   hipStream_t pipe_stream(int half, int role);  // role 0=read 1=compute 2=write
+  // Reserve `n` CUs (spread evenly over the XCDs) for copy kernels: the
+  // pipeline's write streams run on those CUs only and every other stream
+  // on the rest (hipExtStreamCreateWithCUMask).  A download by copy kernel
+  // (kernel_d2h) then never waits for a GEMM work-group to leave a CU, so
+  // it runs beside the SDMA uploads (PCIe full duplex).  0: no masks.
+  // Drains and re-creates the worker's streams.
+  void set_cu_reserve(int n);
+  int cu_reserve() const { return cu_reserve_; }
   int next_compute_queue();                 // round robin (Worker.cs:435-458)
   int queue_concurrency() const { return qconc_; }
   hipEvent_t event(int slot);               // pooled, timing disabled
@@ -210,6 +218,9 @@ class Worker {
   uint64_t bytes_allocated_ = 0;
   std::mutex buf_mu_;
 
+  int cu_reserve_ = 0;
+  hipStream_t new_stream(bool copy_cus);
+  void destroy_streams();
   hipStream_t main_ = nullptr;
   std::vector<hipStream_t> cq_;
   hipStream_t pq_[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};

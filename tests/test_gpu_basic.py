@@ -399,3 +399,30 @@ def test_gemm_row_major_c_variant():
     with pytest.raises(ValueError):
         rowc.run(compute_id=3, resident=False)
     cr.dispose()
+
+
+def test_gemm_shells_with_reserved_copy_cus():
+    """Shell-streamed GEMM with downloads by a copy kernel on 8 reserved CUs
+    (CU-masked streams): same C as the plain path, and the masks can be
+    turned on and off between calls."""
+    from cekirdekler_amd.ops.gemm import GEMM_LIBS, GemmBf16
+    from cekirdekler_amd.ops.library import library
+
+    cr = ck.ClNumberCruncher(_gpu()[0], "", prebuilt=library(*GEMM_LIBS))
+    g = GemmBf16(2048, 2048, 512, cruncher=cr, tile="256x256pb")
+    ref = g.reference()
+    cr.copy_cus = 8
+    cr.kernel_d2h = True
+    assert cr.copy_cus == 8
+    for _ in range(2):
+        g.C.array[:] = np.nan
+        g.run_shells(4, compute_id=3)
+        c = g.result(download=False)
+        assert np.abs(c - ref).max() < 1e-3 * np.abs(ref).max()
+    assert cr.cores.kernel_d2h_bytes >= g.C.array.nbytes
+    cr.kernel_d2h = False
+    cr.copy_cus = 0
+    g.C.array[:] = np.nan
+    g.run_shells(4, compute_id=3)
+    assert np.abs(g.result(download=False) - ref).max() < 1e-3 * np.abs(ref).max()
+    cr.dispose()
