@@ -8,8 +8,18 @@ namespace cek {
 
 // ----------------------------------------------------------------- CpuPool --
 
+// Pool threads alive in the process: spinning only pays while every spinner
+// has a core (two CPU devices of one host would otherwise spin 2·(N-1)
+// threads on N cores and starve each other).
+static std::atomic<int> g_pool_threads{0};
+static bool pool_may_spin() {
+  static const int cores = std::max(1u, std::thread::hardware_concurrency());
+  return Worker::spin_us > 0 && g_pool_threads.load(std::memory_order_relaxed) < cores;
+}
+
 CpuPool::CpuPool(int threads) {
   for (int i = 1; i < threads; ++i) threads_.emplace_back([this] { loop(); });
+  g_pool_threads += static_cast<int>(threads_.size());
 }
 
 CpuPool::~CpuPool() {
@@ -19,27 +29,39 @@ CpuPool::~CpuPool() {
   }
   cv_.notify_all();
   for (auto& t : threads_) t.join();
+  g_pool_threads -= static_cast<int>(threads_.size());
 }
+
+static inline void pool_relax() { __builtin_ia32_pause(); }
+
 
 void CpuPool::loop() {
   uint64_t seen = 0;
   for (;;) {
+    if (pool_may_spin()) {  // a new generation usually follows within µs
+      const double until = now_ms() + Worker::spin_us * 1e-3;
+      int k = 0;
+      while (gen_.load(std::memory_order_acquire) == seen) {
+        pool_relax();
+        if ((++k & 63) == 0 && now_ms() > until) break;
+      }
+    }
     const std::function<void(long long)>* fn;
     long long n;
     {
       std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      cv_.wait(lk, [&] { return stop_ || gen_.load(std::memory_order_relaxed) != seen; });
       if (stop_) return;
-      seen = gen_;
+      seen = gen_.load(std::memory_order_relaxed);
       fn = fn_;
       n = n_;
       if (!fn) continue;
-      ++active_;
+      active_.fetch_add(1, std::memory_order_acq_rel);
     }
     for (long long i = next_++; i < n; i = next_++) (*fn)(i);
     {
       std::lock_guard<std::mutex> g(mu_);
-      --active_;
+      active_.fetch_sub(1, std::memory_order_acq_rel);
     }
     done_cv_.notify_all();
   }
@@ -56,12 +78,21 @@ void CpuPool::parallel_for(long long n, const std::function<void(long long)>& fn
     fn_ = &fn;
     n_ = n;
     next_ = 0;
-    ++gen_;
+    gen_.fetch_add(1, std::memory_order_release);
   }
   cv_.notify_all();
   for (long long i = next_++; i < n; i = next_++) fn(i);
+  // every item is claimed; wait (spinning first) for the threads still running one
+  if (pool_may_spin()) {
+    const double until = now_ms() + Worker::spin_us * 1e-3;
+    int k = 0;
+    while (active_.load(std::memory_order_acquire) != 0) {
+      pool_relax();
+      if ((++k & 63) == 0 && now_ms() > until) break;
+    }
+  }
   std::unique_lock<std::mutex> lk(mu_);
-  done_cv_.wait(lk, [&] { return active_ == 0 && next_ >= n; });
+  done_cv_.wait(lk, [&] { return active_.load(std::memory_order_acquire) == 0 && next_ >= n; });
   fn_ = nullptr;
 }
 

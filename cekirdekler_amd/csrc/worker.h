@@ -77,8 +77,12 @@ class CpuPool {
   const std::function<void(long long)>* fn_ = nullptr;
   long long n_ = 0;
   std::atomic<long long> next_{0};
-  int active_ = 0;
-  uint64_t gen_ = 0;
+  std::atomic<int> active_{0};
+  // generation of the current parallel_for: pool threads spin on it for
+  // Worker::spin_us before sleeping on cv_ (a frame loop calls
+  // parallel_for every few tens of µs; a futex wake per thread per call
+  // was the CPU device's fixed cost)
+  std::atomic<uint64_t> gen_{0};
   bool stop_ = false;
 };
 
