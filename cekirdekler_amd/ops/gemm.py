@@ -517,6 +517,8 @@ class GemmF32(GemmBf16):
             raise ValueError(f"M%{BM}, N%{BN} and K%32 must be 0 (got {M},{N},{K})")
         self.M, self.N, self.K, self.BM, self.BN, self.L, self.kernel = M, N, K, BM, BN, L, kname
         self.geom = None  # the fp32 kernels store C tiles row-major
+        self.row_major_c = False
+        self.exchange = False
         self.split_k = 1
         self.tiles = (M // BM) * (N // BN)
         self.global_range = self.tiles * L
