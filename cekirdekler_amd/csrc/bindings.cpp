@@ -525,6 +525,27 @@ PYBIND11_MODULE(_cek, m) {
            py::arg("policy") = 0, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("policy", &DevicePool::policy)
       .def("enqueue", &DevicePool::enqueue, py::call_guard<py::gil_scoped_release>())
+      // the batch form: task i = template calls[which[i]] with its own arrays,
+      // type and id (one crossing and no per-task Python objects)
+      .def("enqueue_batch",
+           [](DevicePool& p, const std::vector<ComputeCall>& calls, const std::vector<int>& which,
+              const std::vector<std::vector<ArraySpec>>& arrays, const std::vector<uint32_t>& types,
+              const std::vector<long long>& ids) {
+             const size_t n = which.size();
+             if (arrays.size() != n || types.size() != n || ids.size() != n)
+               throw Error("enqueue_batch: which, arrays, types and ids must have one entry per task");
+             std::vector<PoolTask> ts(n);
+             for (size_t i = 0; i < n; ++i) {
+               if (which[i] < 0 || static_cast<size_t>(which[i]) >= calls.size())
+                 throw Error("enqueue_batch: template index out of range");
+               ts[i].call = calls[which[i]];
+               ts[i].call.arrays = arrays[i];
+               ts[i].type = types[i];
+               ts[i].id = ids[i];
+             }
+             py::gil_scoped_release r;
+             p.enqueue(ts);
+           })
       .def("finish", &DevicePool::finish, py::call_guard<py::gil_scoped_release>())
       .def("completions", &DevicePool::completions, py::arg("timeout_ms") = 0.0,
            py::call_guard<py::gil_scoped_release>())

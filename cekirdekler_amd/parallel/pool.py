@@ -273,34 +273,61 @@ class ClDevicePool:
 
     # ---- producer -------------------------------------------------------------
     def enqueue_task_pool(self, pool: ClTaskPool) -> None:
+        """Hand every task of ``pool`` to the native device pool, in FIFO
+        order.  Tasks that share a compute shape (compute id, kernels,
+        ranges, pipeline, repeats) share one validated template call; the
+        native side gets one batch (``DevicePool.enqueue_batch``) instead of
+        one Python-built call per task."""
         if self._native is None:
             raise RuntimeError("device pool has no devices (add_device first)")
         cr0 = self.crunchers[0]
         ndev = len(self.crunchers)
-        batch = []
-        while pool.tasks:
-            t = pool.tasks.popleft()
-            pt = cek.PoolTask()
-            pt.type = int(t.type)
-            with self._cv:
-                pt.id = self._next_id
-                self._next_id += 1
+        templates, index = [], {}
+        empty = cek.ComputeCall()  # barrier / message tasks: no kernels
+        which, arrays, types, ids, entries = [], [], [], [], []
+        expected = 0
+        tasks = list(pool.tasks)
+        pool.tasks.clear()
+        with self._cv:
+            first_id = self._next_id
+            self._next_id += len(tasks)
+        for k, t in enumerate(tasks):
+            tid = first_id + k
             if t.group is not None and t.kernels and not (t.type & ClTaskType.TASK_MESSAGE_NO_COMPUTE
                                                           and not t.kernels):
-                try:
-                    pt.call = cr0._build_call(ClParameterGroup(), t.compute_id, t.kernels, t.global_range,
-                                              t.local_range, t.global_offset, t.pipeline, t.pipeline_type,
-                                              t.pipeline_blobs, specs=t.specs)
-                    t._apply_repeats(pt.call)
-                except ClComputeError as e:
-                    raise ClComputeError(f"task {pt.id}: {e}") from None
+                bl = t.pipeline_blobs if isinstance(t.pipeline_blobs, int) else tuple(t.pipeline_blobs)
+                key = (t.compute_id, t.kernels, t.global_range, t.local_range, t.global_offset, bool(t.pipeline),
+                       bool(t.pipeline_type), bl, int(t.kernel_repeats), t.kernel_repeat_name)
+                j = index.get(key)
+                if j is None:
+                    try:
+                        call = cr0._build_call(ClParameterGroup(), t.compute_id, t.kernels, t.global_range,
+                                               t.local_range, t.global_offset, t.pipeline, t.pipeline_type,
+                                               t.pipeline_blobs, specs=[])
+                        t._apply_repeats(call)
+                    except ClComputeError as e:
+                        raise ClComputeError(f"task {tid}: {e}") from None
+                    j = index[key] = len(templates)
+                    templates.append(call)
+                which.append(j)
+                arrays.append(t.specs)
+            else:
+                if not templates or templates[0] is not empty:
+                    templates.insert(0, empty)
+                    which = [w + 1 for w in which]
+                    index = {kk: v + 1 for kk, v in index.items()}
+                which.append(0)
+                arrays.append([])
+            types.append(int(t.type))
+            ids.append(tid)
             copies = ndev if t.type & ClTaskType.TASK_MESSAGE_BROADCAST else 1
-            with self._cv:
-                self._tasks[pt.id] = [t, copies]
-                self._expected += copies
-            batch.append(pt)
-        if batch:
-            self._native.enqueue(batch)
+            entries.append((tid, [t, copies]))
+            expected += copies
+        with self._cv:
+            self._tasks.update(entries)
+            self._expected += expected
+        if ids:
+            self._native.enqueue_batch(templates, which, arrays, types, ids)
 
     enqueueTaskPool = enqueue_task_pool
 
