@@ -51,8 +51,9 @@ FORCE = r"""
 // hiprtc.  Work-group g owns bodies [512 g, 512 g + 512), so a device's range
 // of whole work-groups owns one contiguous body range.  Two bodies per item
 // (not four) keep 4+ work-groups per CU when the force stage is split over
-// 2-6 GPUs: 52 % / 50 % of FP32 peak at 1/2 and 1/4 of the bodies per GPU
-// against 51 % / 45 % with four (tools/nbody_force_probe.py).
+// 2-6 GPUs.  The next LDS tile of bodies is loaded into registers while the
+// current one is consumed (as in kernels/nbody.hip), so its global-load
+// latency hides behind 256 interactions.
 typedef float f2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void force(const float4* pos, const float4* vel, const float* prm,
                                              float4* pos_o, float4* vel_o, float4* acc_o) {
@@ -64,10 +65,12 @@ __global__ __launch_bounds__(256) void force(const float4* pos, const float4* ve
   const float4 b0 = pos[i0], b1 = pos[i0 + 256];
   const f2 px = {b0.x, b1.x}, py = {b0.y, b1.y}, pz = {b0.z, b1.z};
   f2 ax = {0.f, 0.f}, ay = ax, az = ax;
+  float4 next = pos[threadIdx.x];
   for (int j0 = 0; j0 < n; j0 += 256) {
     __syncthreads();
-    tile[threadIdx.x] = pos[j0 + threadIdx.x];
+    tile[threadIdx.x] = next;
     __syncthreads();
+    if (j0 + 256 < n) next = pos[j0 + 256 + threadIdx.x];
 #pragma unroll 8
     for (int j = 0; j < 256; ++j) {
       const float4 q = tile[j];

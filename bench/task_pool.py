@@ -18,6 +18,11 @@ plus a serial group (eight ``add`` tasks on one array, in order on one
 device: TASK_MESSAGE_SERIAL_MODE_BEGIN/END) and a global barrier task
 (TASK_MESSAGE_GLOBAL_SYNCHRONIZATION_FIRST) in the middle of the pool.
 
+Both device policies run the same pool (ClDevicePoolType.DEVICE_COMPUTE_AT_WILL
+and DEVICE_ROUND_ROBIN, ClPipeline.cs:3792-3806), and the pool's dispatch
+rate is measured on 4096 near-zero-cost tasks (``dispatch``).  With one GPU
+the pool has 8 logical devices of it, the node's width.
+
 Makespan is compared with the ideal Σ(task time) / physical GPUs, where a
 task's time is its kernel's hipEvent device time run alone on one GPU.  The
 ideal is not a strict floor: tasks that occupy a fraction of the CUs (gemm,
@@ -59,7 +64,7 @@ SERIAL = 8  # + the serial group; + 1 barrier task = 256
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--gpus", type=int, default=0)
-ap.add_argument("--logical", type=int, default=2, help="logical devices per GPU when only one GPU")
+ap.add_argument("--logical", type=int, default=8, help="logical devices per GPU when only one GPU (8: the node's width)")
 ap.add_argument("--queues", type=int, default=3)
 a = ap.parse_args()
 g = ck.ClPlatforms.all().gpus()
@@ -204,24 +209,54 @@ def build_pool() -> ClTaskPool:
     return tp
 
 
-pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, True, a.queues, prebuilt=prebuilt)
-pool.add_device(devs)
-for cr in pool.crunchers:  # every input on every device: a task may land anywhere
-    for _, grp, *_ in work:
-        for x in grp.arrays:
+def run_policy(policy):
+    pool = ClDevicePool(policy, SRC, True, a.queues, prebuilt=prebuilt)
+    pool.add_device(devs)
+    for cr in pool.crunchers:  # every input on every device: a task may land anywhere
+        for _, grp, *_ in work:
+            for x in grp.arrays:
+                cr.upload(x)
+        cr.upload(serial_v)
+    pool.enqueue_task_pool(build_pool())  # warm-up pass: untimed
+    pool.finish()
+    tp = build_pool()
+    n = len(tp.tasks)
+    sync()
+    t0 = time.perf_counter()
+    pool.enqueue_task_pool(tp)
+    pool.finish()
+    sync()
+    ms = (time.perf_counter() - t0) * 1e3
+    counts = pool.device_task_counts()
+    # dispatch rate: 4096 tasks of one work-group each (the host-side cost
+    # of the pool: native batch enqueue, consumer threads, marker retirement)
+    tiny_x = [ck.ClArray(np.zeros(256, np.float32)) for _ in range(64)]
+    for x in tiny_x:
+        x.read = x.write = False
+    for x in tiny_x:
+        for cr in pool.crunchers:
             cr.upload(x)
-    cr.upload(serial_v)
-pool.enqueue_task_pool(build_pool())  # warm-up pass: untimed
-pool.finish()
-tp = build_pool()
-ntasks = len(tp.tasks)
-sync()
-t0 = time.perf_counter()
-pool.enqueue_task_pool(tp)
-pool.finish()
-sync()
-makespan = (time.perf_counter() - t0) * 1e3
+    def tiny(k):
+        t = ClTaskPool()
+        for i in range(k):
+            t.feed(tiny_x[i % 64].next_param(serial_v).task(3, "add", 256, 256))
+        return t
+    pool.enqueue_task_pool(tiny(512))
+    pool.finish()
+    tp2 = tiny(4096)
+    sync()
+    t0 = time.perf_counter()
+    pool.enqueue_task_pool(tp2)
+    pool.finish()
+    sync()
+    dispatch = 4096 / (time.perf_counter() - t0)
+    pool.dispose()
+    return n, ms, counts, dispatch
+
+
+ntasks, makespan, counts, dispatch = run_policy(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL)
 ideal = sum(single) / max(1, ng)
+_, makespan_rr, counts_rr, dispatch_rr = run_policy(ClDevicePoolType.DEVICE_ROUND_ROBIN)
 
 # checks: serial group order (x ← 2x + 1, eight times from 0 = 255), one GEMM, one reduction
 serial_ok = bool(np.all(serial_x.array == 255.0))
@@ -241,9 +276,11 @@ emit({"config": "task_pool_256", "tasks": ntasks, "gpus": ng, "logical_devices":
                          for k, v in per_kind.items()},
       "makespan_ms": makespan, "ideal_ms_sum_over_gpus": ideal, "ideal_basis": "hipEvent device time per task, alone",
       "makespan_over_ideal": makespan / ideal, "tasks_per_s": ntasks / (makespan * 1e-3),
-      "per_device_tasks": pool.device_task_counts(), "serial_group_in_order": serial_ok,
+      "per_device_tasks": counts, "serial_group_in_order": serial_ok,
+      "round_robin": {"makespan_ms": makespan_rr, "makespan_over_ideal": makespan_rr / ideal,
+                      "per_device_tasks": counts_rr, "dispatch_tasks_per_s": round(dispatch_rr)},
+      "dispatch_tasks_per_s": round(dispatch), "pool_devices": len(devs),
       "gemm_task_max_rel_err": gemm_err, "reduce_task_rel_err": red_err})
-pool.dispose()
 ref_cr.dispose()
 if not (serial_ok and gemm_err < 5e-3 and red_err < 1e-4):
     raise SystemExit("task pool output check failed")
