@@ -554,15 +554,15 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     if (S > 1) {
       // Every split stores its partial tile; the last of the S to arrive
       // (device-scope counter) adds the others' partials to its own and
-      // writes C, then re-arms the counter for the next call.
-      float* wt = W + (size_t)u * BM * BN;
+      // writes C, then re-arms the counter for the next call.  Partials are
+      // in fragment order (one dwordx4 per lane per fragment, 1 KiB per wave
+      // instruction), so a wave needs one base address, not one per element.
+      const int frag0 = (wr * WN + wc) * FM * FN * 64 + lane;
+      f32x4* wt = reinterpret_cast<f32x4*>(W + (size_t)u * BM * BN) + frag0;
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            wt[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr] = acc[i][j][r];
+        for (int j = 0; j < FN; ++j) wt[(i * FN + j) * 64] = acc[i][j];
       // Each wave waits for its stores to reach L2; ONE release fence (an L2
       // write-back) then covers the whole block before the arrival counter —
       // a fence per wave would write the L2 back eight times.
@@ -580,14 +580,11 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       for (int s2 = 0; s2 < S; ++s2) {
         if (s2 == (int)(u % S)) continue;
-        const float* wp = W + (size_t)(t * S + s2) * BM * BN;
+        const f32x4* wp = reinterpret_cast<const f32x4*>(W + (size_t)(t * S + s2) * BM * BN) + frag0;
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              acc[i][j][r] += wp[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr];
+          for (int j = 0; j < FN; ++j) acc[i][j] += wp[(i * FN + j) * 64];
       }
     }
   }
