@@ -71,8 +71,8 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   const long long t = u / S;
   // XCH 3: the K-split of u odd (the helper) takes K/64/2 − dims[5] K-tiles
   // from the start, u even (the owner) the rest
-  const int kt_all = dims[2] / 64, shift = XCH == 3 ? dims[5] : 0;
-  int ks = XCH == 3 ? ((u & 1) ? 0 : kt_all / 2 - shift) : SK ? (int)(u % S) * (kt_all / S) : 0;
+  const int kt_all = dims[2] / 64, shift = XCH >= 3 ? dims[5] : 0;
+  int ks = XCH >= 3 ? ((u & 1) ? 0 : kt_all / 2 - shift) : SK ? (int)(u % S) * (kt_all / S) : 0;
   // Grouped tile order (dims[3] = GM row panels per group, tiles walk down
   // the group's rows first): the 32 work-groups an XCD runs at once cover a
   // GM × (32/GM) block of C, so A and B K-slices are shared through that
@@ -136,19 +136,21 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  int nk = XCH == 3 ? ((u & 1) ? kt_all / 2 - shift : kt_all / 2 + shift) : K / BK / S;
+  int nk = XCH >= 3 ? ((u & 1) ? kt_all / 2 - shift : kt_all / 2 + shift) : K / BK / S;
   unsigned my_xcc = 0;
-  // XCH 3 flags per tile: [4t] hand-over state (0 open, 1 partial ready, 2
-  // claimed by the owner), [4t + 2] owner's XCD + 1, [4t + 3] helper's XCD + 1;
-  // the word after the last tile counts owner fall-backs.
+  // XCH 3 / 4 flags per tile: [4t] hand-over state (0 open, 1 the helper's
+  // partial is ready, 2 claimed by the owner), [4t + 1] (XCH 4) the owner's
+  // hand-over back (0 open, 1 ready, 2 claimed by the helper), [4t + 2]
+  // owner's XCD + 1, [4t + 3] helper's XCD + 1; the word after the last tile
+  // counts fall-backs.
   bool claimed = false;  // owner: it will compute the helper's K-range itself
-  if constexpr (XCH == 3) {
+  if constexpr (XCH >= 3) {
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(my_xcc));
     my_xcc &= 15u;
     if (tid == 0)
       __hip_atomic_store(&tile_cnt[4 * t + 2 + (u & 1)], (int)my_xcc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!(u & 1) && dims[7] < 0) {
-      // debug (dims[7] < 0): the owner claims the hand-over before its main
+    if (!(u & 1) && dims[7] == -1) {
+      // debug (dims[7] == -1): the owner claims the hand-over before its main
       // loop, so the fall-back pass runs (tests of the co-residency-safe path)
       int* st = reinterpret_cast<int*>(smem);
       if (tid == 0) {
@@ -423,17 +425,31 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     if (!g1) bar();  // equal barrier counts for both groups
     CEK_TS(2);
   }
-  if constexpr (XCH == 3) {
+  // Epilogue: acc[i][j][r] is C(row = wr·16FM + i·16 + fq·4 + r, col = wc·16FN + j·16 + fr)
+  bool store_c = true;
+  if constexpr (XCH >= 3) {
+    // Uneven split-K = 2: the helper (u odd) ran `shift` K-tiles fewer than
+    // half, so its partial is ready while the owner (u even) still
+    // multiplies.  XCH 3: the helper hands its whole partial tile over and
+    // leaves; the owner adds it and stores all of C.  XCH 4 (halves): the
+    // helper hands over its partial of the owner's row half (waves wr == 0)
+    // and waits; the owner then hands back its partial of the helper's half
+    // (waves wr == 1), and each side adds the other's partial to its own half
+    // and stores that half of C — the owner's tail moves 384 KiB instead of
+    // 512 KiB, the helper stores the other half beside it.
+    // Every wait is bounded and co-residency-safe: a side whose partner is
+    // late CLAIMS that hand-over (one CAS against the partner's) and
+    // multiplies the partner's K-range itself; the last side to touch a
+    // state word re-arms it (0) for the next launch.
+    // Partials use the fragment order of the C tile (1 KiB per wave
+    // instruction).
+    f32x4* wt = reinterpret_cast<f32x4*>(W + (size_t)t * BM * BN) + (wr * WN + wc) * FM * FN * 64 + lane;
+    int* st = reinterpret_cast<int*>(smem);
+    int rk0 = 0, rcnt = 0;  // a K-range this work-group multiplies in the fall-back loop
+    bool read_partial = false;
+    __syncthreads();  // every wave is done with LDS before it holds the flags
     if (!(u & 1)) {
-      // Owner, main loop done: is the helper's partial there?  A helper that
-      // is not co-resident (the GPU shared with other kernels) may not even
-      // have started.  After a bounded wait the owner CLAIMS the hand-over
-      // (one CAS against the helper's) and multiplies the helper's K-range
-      // itself, so C is correct whatever the residency; a late helper finds
-      // the claim and leaves.  Exactly one side's CAS wins, and the last one
-      // to touch the state word re-arms it (0) for the next launch.
-      __syncthreads();  // every wave is done with LDS before it holds the flags
-      int* st = reinterpret_cast<int*>(smem);
+      // owner, main loop done: is the helper's partial there?
       if (tid == 0) {
         int v = claimed ? 2 : 0;
         if (!claimed) {
@@ -467,55 +483,42 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       __syncthreads();
       claimed = st[0] == 2;
       const bool same = st[1] != 0;
-      __syncthreads();  // st[] read by every wave before LDS is restaged
+      __syncthreads();  // st[] read by every wave before LDS is reused
       if (claimed) {
-        // fall-back: the helper's K-tiles [0, K/64/2 - shift), one LDS stage
-        // in flight, the first half of the waves staging (rare path: kept
-        // simple, outside the tuned loop)
-        const bool g1 = wave >= NWAVES / 2;
-        ks = 0;
-        nk = kt_all / 2 - shift;
-        if (!g1) stage(0, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        for (int kt = 0; kt < nk; ++kt) {
-          const int cur = kt & 1;
-          if (!g1 && kt + 1 < nk) stage(cur ^ 1, kt + 1);
-          const char* base = smem + cur * STAGE;
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            bf16x8 a[FM], b[FN];
-#pragma unroll
-            for (int j = 0; j < FN; ++j) b[j] = *(const bf16x8*)(base + b_off[s2] + j * 2048);
-#pragma unroll
-            for (int i = 0; i < FM; ++i) a[i] = *(const bf16x8*)(base + a_off[s2] + i * 2048);
+        rk0 = 0;
+        rcnt = kt_all / 2 - shift;
+      } else {
+        if constexpr (XCH == 4) {
+          // hand back the partial of the helper's half
+          if (wr == 1) {
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
-              for (int j = 0; j < FN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+              for (int j = 0; j < FN; ++j) wt[(i * FN + j) * 64] = acc[i][j];
           }
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __syncthreads();
+          if (tid == 0) {
+            if (!same) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            int open = 0;
+            if (!__hip_atomic_compare_exchange_strong(&tile_cnt[4 * t + 1], &open, 1, __ATOMIC_RELAXED,
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+              tile_cnt[4 * t + 1] = 0;  // the helper claimed it: we are the last to touch the word
+          }
+          store_c = wr == 0;
         }
-      } else if (!same) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (!same) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        read_partial = XCH == 3 || wr == 0;
       }
-    }
-  }
-
-  // Epilogue: acc[i][j][r] is C(row = wr·16FM + i·16 + fq·4 + r, col = wc·16FN + j·16 + fr)
-  if constexpr (XCH == 3) {
-    // Uneven split-K = 2, one-way hand-over: the helper ran `shift` K-tiles
-    // fewer than half, so it stores its whole partial tile (fragment order,
-    // 1 KiB per wave instruction) while the owner still multiplies; the owner
-    // (pass loop above) found it ready, adds it and stores the whole C tile.
-    f32x4* wt = reinterpret_cast<f32x4*>(W + (size_t)t * BM * BN);
-    if (u & 1) {  // helper: publish the partial and leave
+    } else {
+      // helper: publish the partial (XCH 4: of the owner's half only)
+      if (XCH == 3 || wr == 0) {
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) wt[(((wr * WN + wc) * FM + i) * FN + j) * 64 + lane] = acc[i][j];
+          for (int j = 0; j < FN; ++j) wt[(i * FN + j) * 64] = acc[i][j];
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       CEK_TS(3);
@@ -526,24 +529,94 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
         if (px != (int)my_xcc + 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int open = 0;
+        int abort = 0;
         if (!__hip_atomic_compare_exchange_strong(&tile_cnt[4 * t], &open, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT)) {
           // the owner claimed the hand-over and computed our K-range itself:
           // this work-group is the last to touch the tile's words
           tile_cnt[4 * t] = 0;
           tile_cnt[4 * t + 3] = 0;
+          abort = 1;
         }
+        st[0] = abort;
+        st[2] = px == (int)my_xcc + 1;
       }
-      CEK_TS(4);
-      return;
+      __syncthreads();
+      const bool abort = st[0] != 0, same_o = st[2] != 0;
+      __syncthreads();
+      if (abort || XCH == 3) return;
+      // XCH 4: wait for the owner's partial of our half
+      if (tid == 0) {
+        int v = 0;
+        const int limit = dims[7] == -2 ? 0 : (1 << 20);
+        for (int spins = 0; (v = __hip_atomic_load(&tile_cnt[4 * t + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0;) {
+          if (++spins > limit) {
+            int open = 0;
+            if (__hip_atomic_compare_exchange_strong(&tile_cnt[4 * t + 1], &open, 2, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+              v = 2;
+            else
+              v = open;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (v == 2)
+          __hip_atomic_fetch_add(&tile_cnt[(size_t)4 * ntm * ntn], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          tile_cnt[4 * t + 1] = 0;  // re-arm: the helper is the last to touch it
+        st[0] = v;
+      }
+      __syncthreads();
+      const bool fb2 = st[0] == 2;
+      __syncthreads();
+      if (fb2) {
+        rk0 = kt_all / 2 - shift;
+        rcnt = kt_all / 2 + shift;
+      } else {
+        if (!same_o) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        read_partial = wr == 1;
+      }
+      store_c = wr == 1;
+    }
+    if (rcnt > 0) {
+      // fall-back: the partner's K-tiles [rk0, rk0 + rcnt), one LDS stage in
+      // flight, the first half of the waves staging (rare path: kept simple,
+      // outside the tuned loop)
+      const bool g1 = wave >= NWAVES / 2;
+      ks = rk0;
+      nk = rcnt;
+      if (!g1) stage(0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (!g1 && kt + 1 < nk) stage(cur ^ 1, kt + 1);
+        const char* base = smem + cur * STAGE;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 a[FM], b[FN];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) b[j] = *(const bf16x8*)(base + b_off[s2] + j * 2048);
+#pragma unroll
+          for (int i = 0; i < FM; ++i) a[i] = *(const bf16x8*)(base + a_off[s2] + i * 2048);
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
     }
     CEK_TS(3);
-    if (!claimed) {
+    if (read_partial) {
       f32x4 part[FM][FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) part[i][j] = wt[(((wr * WN + wc) * FM + i) * FN + j) * 64 + lane];
+        for (int j = 0; j < FN; ++j) part[i][j] = wt[(i * FN + j) * 64];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -623,7 +696,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the strip is rewritten
     }
-  } else {
+  } else if (store_c) {
     f32x4* ct = reinterpret_cast<f32x4*>(C + (size_t)t * BM * BN);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -670,6 +743,14 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sw(
     const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
   __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
   gemm_tile<2, 4, 8, 4, 4, true, 3>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
+}
+
+// the same with the row halves exchanged at the end (XCH 4): the owner's
+// tail carries 384 KiB instead of 512, the helper stores half of C
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sh(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
+  gemm_tile<2, 4, 8, 4, 4, true, 4>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
 }
 
 #define CEK_GEMM_B3_KERNEL(NAME, WM, WN, FM, FN, MODE)                                              \

@@ -38,6 +38,11 @@ TILES = {
     # hand-over is co-residency-safe: an owner whose helper is late claims
     # the hand-over and multiplies the helper's K-range itself.
     "256x256pbw": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sw"),
+    # the same, row halves exchanged at the end: the helper hands over its
+    # partial of the owner's half, the owner hands back its partial of the
+    # helper's half, each stores one half of C (384 KiB of tail traffic on
+    # the owner instead of 512)
+    "256x256pbh": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sh"),
     # 256×128 fallbacks (twice the tiles): even chunk-split DMA, three stages / balanced DMA
     "256x128pe": (256, 128, 512, "cek_sgemm_bf16_256x128pe"),
     "256x128pb": (256, 128, 512, "cek_sgemm_bf16_256x128pb"),
@@ -55,7 +60,7 @@ GEMM_LIBS = ("sgemm_bf16",)
 # each): the kernels store a C tile in fragment order (one dwordx4 per lane
 # per fragment), which tile_to_rows / rows_to_tile convert.
 TILE_WAVES = {
-    "256x256pb": (2, 4, 8, 4), "256x256pbr": (2, 4, 8, 4), "256x256pbw": (2, 4, 8, 4), "256x256": (2, 4, 8, 4), "256x256pp": (2, 4, 8, 4),
+    "256x256pb": (2, 4, 8, 4), "256x256pbr": (2, 4, 8, 4), "256x256pbw": (2, 4, 8, 4), "256x256pbh": (2, 4, 8, 4), "256x256": (2, 4, 8, 4), "256x256pp": (2, 4, 8, 4),
     "256x128pe": (4, 2, 4, 4), "256x128pb": (4, 2, 4, 4), "128x128": (2, 2, 4, 4),
 }
 
@@ -102,10 +107,10 @@ ROW_MAJOR_TILES = {"256x256pbr"}
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
 SPLIT_K_TILES = {"256x256pp", "256x256pb"}
 # tiles whose kernel always runs two K-splits with a hand-over (flag words per tile)
-EXCHANGE_TILES = {"256x256pbw": 4}
+EXCHANGE_TILES = {"256x256pbw": 4, "256x256pbh": 4}
 # K-tile deficit of the helper split (dims[5]): it hands its whole partial
 # over and leaves while the owner still multiplies
-EXCHANGE_SHIFT = {"256x256pbw": 4}
+EXCHANGE_SHIFT = {"256x256pbw": 4, "256x256pbh": 4}
 
 
 def to_bf16_bits(x: np.ndarray) -> np.ndarray:
@@ -204,7 +209,8 @@ class GemmBf16:
         self.cr = cruncher or ClNumberCruncher(devices, "", prebuilt=library(*GEMM_LIBS))
         self.group_m = group_m
         # dims[7]: the owner's wait for the helper's partial, in polls (0: the
-        # kernel default, 65536; < 0: claim at once — forces the fall-back)
+        # kernel default, 65536; -1: the owner claims at once, -2 (halves
+        # tile): the helper claims the hand-back at once — forced fall-backs)
         self.dims = ClArray(np.array([M, N, K, group_m, self.split_k, shift, 0, int(handover_spin_limit)], np.int32))
         self.dims.write = False
         self.A = ClArray(M * K, "bfloat16")

@@ -108,8 +108,9 @@ def test_gemm_split_k(tile, split):
     cr.dispose()
 
 
-@pytest.mark.parametrize("limit", [0, -1, 1])
-def test_gemm_split_k_handover(limit):
+@pytest.mark.parametrize("tile,limit", [("256x256pbw", 0), ("256x256pbw", -1), ("256x256pbw", 1),
+                                        ("256x256pbh", 0), ("256x256pbh", -1), ("256x256pbh", -2), ("256x256pbh", 1)])
+def test_gemm_split_k_handover(tile, limit):
     """Uneven split-K = 2 with a one-way hand-over: flags re-armed across
     calls (4 calls), the pair of K-splits kept on one device (two logical
     devices, one slower).  limit -1: every owner claims the hand-over before
@@ -122,7 +123,7 @@ def test_gemm_split_k_handover(limit):
     g0 = _gpu()[0]
     cr = ck.ClNumberCruncher(g0 + g0, "", prebuilt=library("sgemm_bf16"))
     cr.set_time_scale(1, 2.0)
-    g = GemmBf16(1024, 768, 1024, cruncher=cr, tile="256x256pbw", group_m=2, handover_spin_limit=limit)
+    g = GemmBf16(1024, 768, 1024, cruncher=cr, tile=tile, group_m=2, handover_spin_limit=limit)
     assert g.split_k == 2
     ref = g.reference()
     for _ in range(4):
@@ -133,8 +134,10 @@ def test_gemm_split_k_handover(limit):
     fb = g.handover_fallbacks()
     if limit == 0:
         assert fb == 0
-    if limit < 0:
+    if limit == -1:
         assert fb == 4 * g.tiles, fb  # every owner of every call fell back
+    if limit == -2:
+        assert fb > 0, fb  # helpers claimed the hand-back (race with the owner: not every tile)
     # the state words are re-armed: only the fall-back counter is nonzero
     for dev in range(2):
         cr.download(g.counters, dev)
@@ -267,7 +270,7 @@ def test_gemm_f32_matches_fp64(tile, shape):
     assert np.abs(c - ref).max() < 1e-4 * np.sqrt(K) * max(1.0, np.abs(ref).max())
 
 
-@pytest.mark.parametrize("tile,rows", [("256x256pb", 8192), ("256x256pbw", 1024)])
+@pytest.mark.parametrize("tile,rows", [("256x256pb", 8192), ("256x256pbw", 1024), ("256x256pbh", 1024)])
 def test_gemm_benchmarked_size_verify(tile, rows):
     """The headline kernels at the benchmarked size: the full 8192³ problem
     (N = 1) and the 1024-row slice one GPU of eight computes, device-resident
