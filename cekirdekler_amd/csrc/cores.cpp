@@ -1673,8 +1673,16 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
       }
     }
   } else {
+    // One participant runs on the calling thread: a hand-off fewer per call
+    // (the wave frame's GPU+CPU split pays one wake-up instead of two).  A
+    // CPU device is preferred there — its work is the calling thread plus
+    // the CPU pool either way, and the GPU workers are posted first so
+    // their launches go out while the CPU computes.
+    int inline_w = -1;
+    for (int w = 0; w < nloc; ++w)
+      if (part[w] && (inline_w < 0 || !workers_[w]->gpu())) inline_w = w;
     for (int w = 0; w < nloc; ++w) {
-      if (!part[w]) continue;
+      if (!part[w] || w == inline_w) continue;
       int g = global_base_ + w;
       long long ref = st.references[g], rng = st.ranges[g];
       workers_[w]->post([=, &c, &ms, &h2d, &d2h] {
@@ -1682,15 +1690,16 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
       });
     }
     for (int w = 0; w < nloc; ++w) {
-      if (part[w]) continue;
+      if (part[w] && w != inline_w) continue;
       try {
-        run_device(w, c, st.references[global_base_ + w], 0, pipelined, &ms[w], &h2d[w], &d2h[w]);
+        run_device(w, c, st.references[global_base_ + w], part[w] ? st.ranges[global_base_ + w] : 0,
+                   pipelined, &ms[w], &h2d[w], &d2h[w]);
       } catch (const std::exception& e) {
         failure.add(w, e.what());
       }
     }
     for (int w = 0; w < nloc; ++w) {
-      if (!part[w]) continue;
+      if (!part[w] || w == inline_w) continue;
       try {
         workers_[w]->wait();
       } catch (const std::exception& e) {
