@@ -149,7 +149,11 @@ void RcclComm::allgatherv(void* dptr, const std::vector<uint64_t>& offsets,
   if (world_ == 1) return;
   auto* base = static_cast<char*>(dptr);
   // Equal slices at contiguous offsets: one ring all-gather.
-  bool equal = true;
+  static const bool direct_always = [] {
+    const char* e = std::getenv("CEK_ALLGATHERV");
+    return e && std::string(e) == "direct";
+  }();
+  bool equal = !direct_always;
   for (int r = 0; r < world_; ++r)
     if (sizes[r] != sizes[0] || offsets[r] != offsets[0] + sizes[0] * r) equal = false;
   if (equal && sizes[0] > 0) {
@@ -157,11 +161,19 @@ void RcclComm::allgatherv(void* dptr, const std::vector<uint64_t>& offsets,
                            static_cast<ncclComm_t>(comm_), s));
     return;
   }
+  // Uneven slices (the balancer moved work): every rank sends its slice
+  // straight to each peer.  The MI355X node is a full xGMI mesh — one link
+  // per GPU pair — so the N−1 sends of a rank leave on N−1 different links
+  // at once and each link carries one slice, where a ring (or a group of
+  // ring broadcasts) pushes every slice over every link it passes.  Sizes
+  // are identical on all ranks, so zero-byte pairs are skipped on both
+  // sides.
+  auto* comm = static_cast<ncclComm_t>(comm_);
   CEK_NCCL(ncclGroupStart());
-  for (int r = 0; r < world_; ++r) {
-    if (sizes[r] == 0) continue;
-    CEK_NCCL(ncclBroadcast(base + offsets[r], base + offsets[r], sizes[r], ncclChar, r,
-                           static_cast<ncclComm_t>(comm_), s));
+  for (int k = 1; k < world_; ++k) {
+    const int to = (rank_ + k) % world_, from = (rank_ - k + world_) % world_;
+    if (sizes[rank_] > 0) CEK_NCCL(ncclSend(base + offsets[rank_], sizes[rank_], ncclChar, to, comm, s));
+    if (sizes[from] > 0) CEK_NCCL(ncclRecv(base + offsets[from], sizes[from], ncclChar, from, comm, s));
   }
   CEK_NCCL(ncclGroupEnd());
 }

@@ -70,9 +70,10 @@ class RcclComm : public Comm {
   int rank() const override { return rank_; }
   int world() const override { return world_; }
   void broadcast(void* dptr, uint64_t bytes, int root, hipStream_t s) override;
-  // Equal contiguous slices: one ring all-gather.  Uneven slices (after the
-  // balancer moved work): one grouped broadcast per owner; with W of them in
-  // flight each link carries about (W-1)/W of the array, as a ring would.
+  // Equal contiguous slices: one RCCL all-gather.  Uneven slices (after the
+  // balancer moved work): grouped point-to-point sends, each rank's slice
+  // straight to every peer over that pair's own xGMI link.
+  // CEK_ALLGATHERV=direct uses the sends for equal slices too.
   void allgatherv(void* dptr, const std::vector<uint64_t>& offsets,
                   const std::vector<uint64_t>& sizes, hipStream_t s) override;
   void allreduce_sum_f32(void* dptr, uint64_t count, hipStream_t s) override;
