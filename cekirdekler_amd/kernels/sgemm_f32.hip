@@ -385,7 +385,134 @@ __device__ __forceinline__ void gemm_f32w_tile(const int* __restrict__ dims, con
             acc[i][j][r];
 }
 
+// Register-direct tiles: fragments loaded global → VGPR, no LDS, no barrier.
+//
+// Every LDS-staged form above shares each K-tile between the waves of a
+// work-group, so every K-tile ends in a barrier; with one wave per SIMD
+// nothing covers the wait after it (the q tiles, 134–140 TF/s), and with
+// two waves per SIMD both waves of a SIMD stall at the same barrier (89 %
+// MFMA-busy).  Here a wave loads its own fragments, 16 B per lane straight
+// into the register image ds_read_b128 would have produced: lane l holds
+// A[row = 16i + l%16][16kb + 4(l/16) .. +3], element t feeding the t-th of
+// four MFMAs.  The next 16-deep block's loads go out before the current
+// block's MFMAs (4·FM·FN of them, 32 cycles each), so even an HBM miss lands
+// in time, and the waves never wait for each other.  Waves that share A
+// rows (or B rows) read the same lines through the CU's L1; the L2 sees at
+// most a few times the LDS form's traffic, a few TB/s against its ~30.
+//
+// Buffer loads: one descriptor per operand over the work-group's rows
+// (built from work-group-uniform values only), the lane's row and k chunk in
+// the voffset VGPR and fragment i / block kb as a scalar soffset: two
+// address VGPRs for all loads.
+// VAR 0: sched_barrier between the phases and a memory clobber after each
+//        load group;
+// VAR 1: each MFMA phase starts with an empty asm that takes its fragments
+//        in and out ("+v", with a memory clobber), so the phase cannot start
+//        before the loads issued ahead of it, and nothing else is pinned.
+template <int N>
+__device__ __forceinline__ void cek_tie(f32x4 (&x)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(x[i])::"memory");
+}
+
+template <int WM, int WN, int FM, int FN, int VAR>
+__device__ __forceinline__ void gemm_f32_direct(const int* __restrict__ dims, const float* __restrict__ A,
+                                                const float* __restrict__ Bt, float* __restrict__ C,
+                                                long long off) {
+  constexpr int BM = WM * 16 * FM, BN = WN * 16 * FN, NT = 64 * WM * WN;
+  const int M = dims[0], N = dims[1], K = dims[2], GM = dims[3] > 0 ? dims[3] : 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave / WN, wc = wave % WN;
+  const long long t = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
+  const int ntn = N / BN, ntm = M / BM;
+  int tm, tn;
+  cek_tile_coords(t, ntm, ntn, GM, dims[6], tm, tn);
+  const int fr = lane & 15, fq = lane >> 4;
+  const float* a_base = A + (size_t)tm * BM * K;
+  const float* b_base = Bt + (size_t)tn * BN * K;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)a_base, 0, (unsigned)(BM * K * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)b_base, 0, (unsigned)(BN * K * 4), 0x00020000);
+  const int va = ((wr * 16 * FM + fr) * K + fq * 4) * 4;
+  const int vb = ((wc * 16 * FN + fr) * K + fq * 4) * 4;
+  const int frag_stride = 16 * K * 4;  // bytes between fragment rows i and i+1
+
+  auto load = [&](f32x4(&a)[FM], f32x4(&b)[FN], int kb) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+      a[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, va, i * frag_stride + kb * 64, 0));
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      b[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, vb, j * frag_stride + kb * 64, 0));
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const f32x4(&a)[FM], const f32x4(&b)[FN]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
+  };
+  const int nkb = K / 16;  // even: K % 32 == 0
+  f32x4 a0[FM], b0[FN], a1[FM], b1[FN];
+  load(a0, b0, 0);
+  __builtin_amdgcn_s_setprio(1);
+  // The last iteration reloads block 0 (in bounds, unused): no branch.
+  for (int kb = 0; kb < nkb; kb += 2) {
+    if constexpr (VAR == 0) {
+      load(a1, b1, kb + 1);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      load(a0, b0, kb + 2 < nkb ? kb + 2 : 0);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      load(a1, b1, kb + 1);
+      cek_tie(a0);
+      cek_tie(b0);
+      mma(a0, b0);
+      load(a0, b0, kb + 2 < nkb ? kb + 2 : 0);
+      cek_tie(a1);
+      cek_tie(b1);
+      mma(a1, b1);
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+
+  // acc[i][j][r] is C(row = wr·16FM + 16i + 4fq + r, col = wc·16FN + 16j + fr)
+  float* ct = C + (size_t)t * BM * BN;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        ct[(size_t)(wr * 16 * FM + i * 16 + fq * 4 + r) * BN + wc * 16 * FN + j * 16 + fr] = acc[i][j][r];
+}
+
 }  // namespace
+
+#define CEK_GEMM_F32G_KERNEL(NAME, WM, WN, FM, FN, VAR)                                            \
+  extern "C" __global__ __launch_bounds__(64 * WM * WN) void NAME(                                  \
+      const int* dims, const float* A, const float* Bt, float* C, CEK_HIDDEN) {                      \
+    gemm_f32_direct<WM, WN, FM, FN, VAR>(dims, A, Bt, C, __cek_off);                                 \
+  }
+// 256×256: 4 waves of 128×128 (one per SIMD, accumulators in AGPRs: 512
+// registers per lane) and 8 waves of 128×64 (two per SIMD)
+CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g, 2, 2, 8, 8, 0)
+CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256gt, 2, 2, 8, 8, 1)
+CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g8, 2, 4, 8, 4, 0)
+CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g8t, 2, 4, 8, 4, 1)
 
 #define CEK_GEMM_F32_KERNEL(NAME, WM, WN, FM, FN, PIPE)                                           \
   extern "C" __global__ __launch_bounds__(64 * WM * WN) void NAME(                                 \

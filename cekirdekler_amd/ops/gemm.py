@@ -99,6 +99,13 @@ F32_TILES = {
     # plain one-stage-in-flight structures
     "256x256": (256, 256, 512, "cek_sgemm_f32_256x256"),
     "256x128": (256, 128, 512, "cek_sgemm_f32_256x128"),
+    # register-direct: fragments global → VGPR, no LDS, no barrier; 4 waves
+    # of 128×128 (one per SIMD) or 8 of 128×64; t = phases ordered by
+    # fragment ties instead of scheduling barriers
+    "256x256g": (256, 256, 256, "cek_sgemm_f32_256x256g"),
+    "256x256gt": (256, 256, 256, "cek_sgemm_f32_256x256gt"),
+    "256x256g8": (256, 256, 512, "cek_sgemm_f32_256x256g8"),
+    "256x256g8t": (256, 256, 512, "cek_sgemm_f32_256x256g8t"),
     "128x128": (128, 128, 256, "cek_sgemm_f32_128x128"),
 }
 

@@ -1,11 +1,12 @@
 #!/bin/bash
 # Round-4 probes on one GPU: host fan-out cost and pool throughput (both
 # worker hand-off modes), PCIe duplex beside a CU-masked busy kernel, and
-# the N-body force-kernel variants.  Each step has its own time limit; the
+# the N-body force-kernel variants, register-direct fp32 GEMM tiles.  Each step has its own time limit; the
 # first failing step ends the call.
 set -o pipefail
 out=${1:-gpurun_out/probes}
 mkdir -p "$out"
+timeout -k 10 240 python tools/gemm_f32_probe.py 8192 256x256ir,256x256gt,256x256g8t,256x256g,256x256g8 3 5 > "$out/f32_probe.json" 2> "$out/f32_probe.err" || exit $?
 CEK_SPIN_US=0 timeout -k 10 180 python tools/fanout_probe.py "$out/fanout_spin0.json" > "$out/fanout0.log" 2>&1 || exit $?
 timeout -k 10 180 python tools/fanout_probe.py "$out/fanout_spin50.json" > "$out/fanout50.log" 2>&1 || exit $?
 timeout -k 10 120 ./tools/microbench/pcie_cumask > "$out/pcie_cumask.json" 2> "$out/pcie_cumask.err" || exit $?
