@@ -1689,6 +1689,17 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
         run_device(w, c, ref, rng, pipelined, &ms[w], &h2d[w], &d2h[w]);
       });
     }
+    // the calling thread's current device is the caller's (torch allocates
+    // on it): restored after a GPU participant ran here
+    struct RestoreDevice {
+      int dev = -1;
+      explicit RestoreDevice(bool gpu) {
+        if (gpu && hipGetDevice(&dev) != hipSuccess) dev = -1;
+      }
+      ~RestoreDevice() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+      }
+    } restore(inline_w >= 0 && workers_[inline_w]->gpu());
     for (int w = 0; w < nloc; ++w) {
       if (part[w] && w != inline_w) continue;
       try {
