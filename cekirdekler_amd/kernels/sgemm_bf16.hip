@@ -449,6 +449,33 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
     bool read_partial = false;
     __syncthreads();  // every wave is done with LDS before it holds the flags
     if (!(u & 1)) {
+      if constexpr (XCH == 5) {
+        // XCH 5: hand back the partial of the helper's half FIRST, so the
+        // two sides' partial stores overlap instead of the owner's waiting
+        // for the helper's before starting its own (with no K-tile shift
+        // both sides end their loops together)
+        if (!claimed) {
+          if (wr == 1) {
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+              for (int j = 0; j < FN; ++j) wt[(i * FN + j) * 64] = acc[i][j];
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          if (tid == 0) {
+            // the helper published its XCD at its start (0: not started
+            // yet, then release through the L2 write-back to be safe)
+            const int hx = __hip_atomic_load(&tile_cnt[4 * t + 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (hx != (int)my_xcc + 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            int open = 0;
+            if (!__hip_atomic_compare_exchange_strong(&tile_cnt[4 * t + 1], &open, 1, __ATOMIC_RELAXED,
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+              tile_cnt[4 * t + 1] = 0;  // the helper claimed it: we are the last to touch the word
+          }
+        }
+      }
       // owner, main loop done: is the helper's partial there?
       if (tid == 0) {
         int v = claimed ? 2 : 0;
@@ -470,6 +497,9 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
         int same = 0;
         if (v == 2) {
           __hip_atomic_fetch_add(&tile_cnt[(size_t)4 * ntm * ntn], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // XCH 5: the hand-back published above has no reader now (the
+          // helper aborts at its own CAS): re-arm the word
+          if constexpr (XCH == 5) tile_cnt[4 * t + 1] = 0;
         } else {  // ready: the helper published its XCD before its partial
           const int hx = __hip_atomic_load(&tile_cnt[4 * t + 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           tile_cnt[4 * t + 3] = 0;
@@ -508,6 +538,7 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
           }
           store_c = wr == 0;
         }
+        if constexpr (XCH == 5) store_c = wr == 0;
         if (!same) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         read_partial = XCH == 3 || wr == 0;
       }
@@ -751,6 +782,14 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sh(
     const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
   __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
   gemm_tile<2, 4, 8, 4, 4, true, 4>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
+}
+
+// halves exchanged with both partial stores in flight at once (XCH 5):
+// meant for an even split (dims[5] = 0), both sides ending together
+extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_ss(
+    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
+  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
+  gemm_tile<2, 4, 8, 4, 4, true, 5>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
 }
 
 #define CEK_GEMM_B3_KERNEL(NAME, WM, WN, FM, FN, MODE)                                              \

@@ -43,6 +43,10 @@ TILES = {
     # helper's half, each stores one half of C (384 KiB of tail traffic on
     # the owner instead of 512)
     "256x256pbh": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sh"),
+    # halves exchanged with an even split: the owner hands its partial back
+    # before it waits for the helper's, so both partial stores are in flight
+    # together and both sides end their loops together
+    "256x256pbs": (256, 256, 512, "cek_sgemm_bf16_256x256pb_ss"),
     # 256×128 fallbacks (twice the tiles): even chunk-split DMA, three stages / balanced DMA
     "256x128pe": (256, 128, 512, "cek_sgemm_bf16_256x128pe"),
     "256x128pb": (256, 128, 512, "cek_sgemm_bf16_256x128pb"),
@@ -60,7 +64,7 @@ GEMM_LIBS = ("sgemm_bf16",)
 # each): the kernels store a C tile in fragment order (one dwordx4 per lane
 # per fragment), which tile_to_rows / rows_to_tile convert.
 TILE_WAVES = {
-    "256x256pb": (2, 4, 8, 4), "256x256pbr": (2, 4, 8, 4), "256x256pbw": (2, 4, 8, 4), "256x256pbh": (2, 4, 8, 4), "256x256": (2, 4, 8, 4), "256x256pp": (2, 4, 8, 4),
+    "256x256pb": (2, 4, 8, 4), "256x256pbr": (2, 4, 8, 4), "256x256pbw": (2, 4, 8, 4), "256x256pbh": (2, 4, 8, 4), "256x256pbs": (2, 4, 8, 4), "256x256": (2, 4, 8, 4), "256x256pp": (2, 4, 8, 4),
     "256x128pe": (4, 2, 4, 4), "256x128pb": (4, 2, 4, 4), "128x128": (2, 2, 4, 4),
 }
 
@@ -114,10 +118,10 @@ ROW_MAJOR_TILES = {"256x256pbr"}
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
 SPLIT_K_TILES = {"256x256pp", "256x256pb"}
 # tiles whose kernel always runs two K-splits with a hand-over (flag words per tile)
-EXCHANGE_TILES = {"256x256pbw": 4, "256x256pbh": 4}
+EXCHANGE_TILES = {"256x256pbw": 4, "256x256pbh": 4, "256x256pbs": 4}
 # K-tile deficit of the helper split (dims[5]): it hands its whole partial
 # over and leaves while the owner still multiplies
-EXCHANGE_SHIFT = {"256x256pbw": 4, "256x256pbh": 4}
+EXCHANGE_SHIFT = {"256x256pbw": 4, "256x256pbh": 4, "256x256pbs": 0}
 
 
 def to_bf16_bits(x: np.ndarray) -> np.ndarray:

@@ -109,7 +109,8 @@ def test_gemm_split_k(tile, split):
 
 
 @pytest.mark.parametrize("tile,limit", [("256x256pbw", 0), ("256x256pbw", -1), ("256x256pbw", 1),
-                                        ("256x256pbh", 0), ("256x256pbh", -1), ("256x256pbh", -2), ("256x256pbh", 1)])
+                                        ("256x256pbh", 0), ("256x256pbh", -1), ("256x256pbh", -2), ("256x256pbh", 1),
+                                        ("256x256pbs", 0), ("256x256pbs", -1), ("256x256pbs", -2), ("256x256pbs", 1)])
 def test_gemm_split_k_handover(tile, limit):
     """Uneven split-K = 2 with a one-way hand-over: flags re-armed across
     calls (4 calls), the pair of K-splits kept on one device (two logical
@@ -136,8 +137,10 @@ def test_gemm_split_k_handover(tile, limit):
         assert fb == 0
     if limit == -1:
         assert fb == 4 * g.tiles, fb  # every owner of every call fell back
-    if limit == -2:
-        assert fb > 0, fb  # helpers claimed the hand-back (race with the owner: not every tile)
+    if limit == -2 and tile != "256x256pbs":
+        # helpers claimed the hand-back (race with the owner: not every
+        # tile; pbs owners hand back before they wait, so it may be none)
+        assert fb > 0, fb
     # the state words are re-armed: only the fall-back counter is nonzero
     for dev in range(2):
         cr.download(g.counters, dev)
@@ -271,7 +274,8 @@ def test_gemm_f32_matches_fp64(tile, shape):
     assert np.abs(c - ref).max() < 1e-4 * np.sqrt(K) * max(1.0, np.abs(ref).max())
 
 
-@pytest.mark.parametrize("tile,rows", [("256x256pb", 8192), ("256x256pbw", 1024), ("256x256pbh", 1024)])
+@pytest.mark.parametrize("tile,rows", [("256x256pb", 8192), ("256x256pbw", 1024), ("256x256pbh", 1024),
+                                      ("256x256pbs", 1024)])
 def test_gemm_benchmarked_size_verify(tile, rows):
     """The headline kernels at the benchmarked size: the full 8192³ problem
     (N = 1) and the 1024-row slice one GPU of eight computes, device-resident
