@@ -11,10 +11,20 @@ namespace cek {
 // Pool threads alive in the process: spinning only pays while every spinner
 // has a core (two CPU devices of one host would otherwise spin 2·(N-1)
 // threads on N cores and starve each other).
+// Off by default (CEK_POOL_SPIN_US): measured on an 8-vCPU VM, spinning pool
+// threads made a tiny CPU-device compute 1.5-3x slower (20 -> 33-60 µs; two
+// CPU devices 42-51 -> 130-141 µs), and under a cgroup CPU quota (the GPU
+// boxes give a process a 16-CPU share of a much larger machine) every
+// spinning thread burns the share the computing threads need.
 static std::atomic<int> g_pool_threads{0};
+static double env_pool_spin_us() {
+  const char* e = std::getenv("CEK_POOL_SPIN_US");
+  return e ? std::max(0.0, std::atof(e)) : 0.0;
+}
+static const double g_pool_spin_us = env_pool_spin_us();
 static bool pool_may_spin() {
   static const int cores = std::max(1u, std::thread::hardware_concurrency());
-  return Worker::spin_us > 0 && g_pool_threads.load(std::memory_order_relaxed) < cores;
+  return g_pool_spin_us > 0 && g_pool_threads.load(std::memory_order_relaxed) < cores;
 }
 
 CpuPool::CpuPool(int threads) {
@@ -39,7 +49,7 @@ void CpuPool::loop() {
   uint64_t seen = 0;
   for (;;) {
     if (pool_may_spin()) {  // a new generation usually follows within µs
-      const double until = now_ms() + Worker::spin_us * 1e-3;
+      const double until = now_ms() + g_pool_spin_us * 1e-3;
       int k = 0;
       while (gen_.load(std::memory_order_acquire) == seen) {
         pool_relax();
@@ -84,7 +94,7 @@ void CpuPool::parallel_for(long long n, const std::function<void(long long)>& fn
   for (long long i = next_++; i < n; i = next_++) fn(i);
   // every item is claimed; wait (spinning first) for the threads still running one
   if (pool_may_spin()) {
-    const double until = now_ms() + Worker::spin_us * 1e-3;
+    const double until = now_ms() + g_pool_spin_us * 1e-3;
     int k = 0;
     while (active_.load(std::memory_order_acquire) != 0) {
       pool_relax();
@@ -661,7 +671,9 @@ void Worker::post(std::function<void()> fn) {
 
 void Worker::wait() {
   const uint64_t target = posted_.load(std::memory_order_acquire);
-  if (finished_.load(std::memory_order_acquire) < target && spin_us > 0) {
+  // spin only on a GPU worker: a CPU device's job runs on the CPU pool,
+  // which needs every core the caller would spin on
+  if (finished_.load(std::memory_order_acquire) < target && spin_us > 0 && gpu()) {
     const double until = now_ms() + spin_us * 1e-3;
     int n = 0;
     while (finished_.load(std::memory_order_acquire) < target) {
@@ -686,8 +698,9 @@ void Worker::thread_loop() {
   bool device_set = false;
   for (;;) {
     std::function<void()> job;
-    // spin for new work first (a hot loop of computes posts every few µs)
-    if (spin_us > 0 && !stop_) {
+    // spin for new work first (a hot loop of computes posts every few µs);
+    // GPU workers only (a CPU worker's spin competes with its own pool)
+    if (spin_us > 0 && !stop_ && gpu()) {
       const uint64_t seen = finished_.load(std::memory_order_acquire);
       const double until = now_ms() + spin_us * 1e-3;
       int n = 0;

@@ -78,8 +78,8 @@ class CpuPool {
   long long n_ = 0;
   std::atomic<long long> next_{0};
   std::atomic<int> active_{0};
-  // generation of the current parallel_for: pool threads spin on it for
-  // Worker::spin_us before sleeping on cv_ (a frame loop calls
+  // generation of the current parallel_for: pool threads may spin on it for
+  // CEK_POOL_SPIN_US (default 0) before sleeping on cv_ (a frame loop calls
   // parallel_for every few tens of µs; a futex wake per thread per call
   // was the CPU device's fixed cost)
   std::atomic<uint64_t> gen_{0};
@@ -181,8 +181,8 @@ class Worker {
   size_t graphs_cached() const { return graphs_.size(); }
 
   // --- job thread --------------------------------------------------------
-  // Hand-off to the worker thread.  Both sides spin (with pause) for up to
-  // spin_us before blocking on a condition variable: back-to-back computes
+  // Hand-off to a GPU worker's thread.  Both sides spin (with pause) for up
+  // to spin_us before blocking on a condition variable: back-to-back computes
   // (a loop of enqueue-mode calls, ~10-20 µs apart) then cost an atomic
   // store and a cache-line transfer per device instead of a futex wake-up
   // (tens of µs on a busy host).  CEK_SPIN_US sets it (0: block at once).
