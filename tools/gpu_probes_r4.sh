@@ -7,6 +7,12 @@ set -o pipefail
 out=${1:-gpurun_out/probes}
 mkdir -p "$out"
 timeout -k 10 240 python tools/gemm_f32_probe.py 8192 256x256ir,256x256gt,256x256g8t,256x256g,256x256g8 3 5 > "$out/f32_probe.json" 2> "$out/f32_probe.err" || exit $?
+for v in "4 sw" "4 sh" "0 ss" "1 ss" "2 ss"; do
+  timeout -k 10 60 ./tools/microbench/gemm_loop 30 $v >> "$out/gemm_loop.json" 2>> "$out/gemm_loop.err" || exit $?
+done
+for v in "4 sw" "4 sh" "0 ss"; do
+  timeout -k 10 60 ./tools/microbench/gemm_loop_ts 10 $v >> "$out/gemm_loop_ts.json" 2>> "$out/gemm_loop.err" || exit $?
+done
 CEK_SPIN_US=0 timeout -k 10 180 python tools/fanout_probe.py "$out/fanout_spin0.json" > "$out/fanout0.log" 2>&1 || exit $?
 timeout -k 10 180 python tools/fanout_probe.py "$out/fanout_spin50.json" > "$out/fanout50.log" 2>&1 || exit $?
 timeout -k 10 120 ./tools/microbench/pcie_cumask > "$out/pcie_cumask.json" 2> "$out/pcie_cumask.err" || exit $?

@@ -1,6 +1,7 @@
 // Main-loop probe of the production bf16 GEMM kernels, outside the runtime:
-// times cek_sgemm_bf16_256x256pb (8192³) and the 8-GPU slice kernel
-// cek_sgemm_bf16_256x256pb_sw (1024 × 8192 × 8192) with hipEvents.
+// times cek_sgemm_bf16_256x256pb (8192³) and an 8-GPU slice kernel
+// (1024 × 8192 × 8192) with hipEvents: argv[3] = sw (256x256pbw, default),
+// sh (256x256pbh) or ss (256x256pbs).
 // Built twice by tools/microbench/build_gemm_loop.sh:
 //   gemm_loop      the kernels as shipped
 //   gemm_loop_l2   -DCEK_KTILE: every stage load re-reads K-tiles 0/1 of its
@@ -78,10 +79,18 @@ static void launch_full(hipStream_t s) {
                      0LL, (long long)(N / 256) * (N / 256) * 512);
 }
 
+static char g_slice = 'w';  // w: pb_sw, h: pb_sh, s: pb_ss
 static void launch_slice(hipStream_t s) {
   const int tiles = (SLICE / 256) * (N / 256);
-  hipLaunchKernelGGL(cek_sgemm_bf16_256x256pb_sw, dim3(2 * tiles), dim3(512), 0, s, g_dims_slice, g_A, g_B, g_C, g_W,
-                     g_cnt, 0LL, (long long)2 * tiles * 512);
+  if (g_slice == 'h')
+    hipLaunchKernelGGL(cek_sgemm_bf16_256x256pb_sh, dim3(2 * tiles), dim3(512), 0, s, g_dims_slice, g_A, g_B, g_C, g_W,
+                       g_cnt, 0LL, (long long)2 * tiles * 512);
+  else if (g_slice == 's')
+    hipLaunchKernelGGL(cek_sgemm_bf16_256x256pb_ss, dim3(2 * tiles), dim3(512), 0, s, g_dims_slice, g_A, g_B, g_C, g_W,
+                       g_cnt, 0LL, (long long)2 * tiles * 512);
+  else
+    hipLaunchKernelGGL(cek_sgemm_bf16_256x256pb_sw, dim3(2 * tiles), dim3(512), 0, s, g_dims_slice, g_A, g_B, g_C, g_W,
+                       g_cnt, 0LL, (long long)2 * tiles * 512);
 }
 
 #ifdef CEK_PROBE_TS
@@ -150,6 +159,8 @@ static void timeline(const char* name, void (*launch)(hipStream_t), int grid) {
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 20;
   const int shift = argc > 2 ? atoi(argv[2]) : 4;  // the slice helper's K-tile deficit (dims[5])
+  if (argc > 3) g_slice = argv[3][1];  // "sw" / "sh" / "ss"
+  const char* slice_name = g_slice == 'h' ? "256x256pbh" : g_slice == 's' ? "256x256pbs" : "256x256pbw";
   const size_t nab = (size_t)N * N;
   CK(hipMalloc(&g_A, nab * 2));
   CK(hipMalloc(&g_B, nab * 2));
@@ -183,12 +194,14 @@ int main(int argc, char** argv) {
     printf("{\"variant\": \"%s\", \"kernel\": \"256x256pb\", \"shape\": \"8192^3\", \"ms\": %.4f, \"tflops\": %.1f}\n",
            variant, ms, 2.0 * N * N * (double)N / ms / 1e9);
     ms = time_kernel(launch_slice, reps);
-    printf("{\"variant\": \"%s\", \"kernel\": \"256x256pbw\", \"shift\": %d, \"shape\": \"1024x8192x8192\", \"ms\": %.4f, \"tflops\": %.1f}\n",
-           variant, shift, ms, 2.0 * SLICE * N * (double)N / ms / 1e9);
+    printf("{\"variant\": \"%s\", \"kernel\": \"%s\", \"shift\": %d, \"shape\": \"1024x8192x8192\", \"ms\": %.4f, \"tflops\": %.1f}\n",
+           variant, slice_name, shift, ms, 2.0 * SLICE * N * (double)N / ms / 1e9);
   }
 #ifdef CEK_PROBE_TS
   timeline("256x256pb 8192^3", launch_full, (N / 256) * (N / 256));
-  timeline("256x256pbw 1024x8192x8192", launch_slice, 2 * tiles_slice);
+  char tl[64];
+  snprintf(tl, sizeof tl, "%s 1024x8192x8192", slice_name);
+  timeline(tl, launch_slice, 2 * tiles_slice);
 #endif
   int err = 0;
   CK(hipMemcpy(&err, g_cnt + 4 * tiles_slice, sizeof(int), hipMemcpyDeviceToHost));
