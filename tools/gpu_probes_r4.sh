@@ -13,6 +13,8 @@ done
 for v in "4 sw" "4 sh" "0 ss"; do
   timeout -k 10 60 ./tools/microbench/gemm_loop_ts 10 $v >> "$out/gemm_loop_ts.json" 2>> "$out/gemm_loop.err" || exit $?
 done
+CEK_POOL_SPIN_US=0 timeout -k 10 120 python tools/cpu_spin_probe.py "$out/cpu_spin0.json" > /dev/null 2>> "$out/cpu_spin.err" || exit $?
+CEK_POOL_SPIN_US=50 timeout -k 10 120 python tools/cpu_spin_probe.py "$out/cpu_spin50.json" > /dev/null 2>> "$out/cpu_spin.err" || exit $?
 CEK_SPIN_US=0 timeout -k 10 180 python tools/fanout_probe.py "$out/fanout_spin0.json" > "$out/fanout0.log" 2>&1 || exit $?
 timeout -k 10 180 python tools/fanout_probe.py "$out/fanout_spin50.json" > "$out/fanout50.log" 2>&1 || exit $?
 timeout -k 10 120 ./tools/microbench/pcie_cumask > "$out/pcie_cumask.json" 2> "$out/pcie_cumask.err" || exit $?
