@@ -17,7 +17,7 @@ from __future__ import annotations
 import numpy as np
 
 from ..arrays import ClArray
-from ..cruncher import ClNumberCruncher
+from ..cruncher import ClComputeError, ClNumberCruncher
 from .library import library
 
 # tile name -> (BM, BN, work-group size, kernel).  The production tiles and
@@ -193,6 +193,7 @@ class GemmBf16:
                  group_m: int = 4, split_k: int = 1, wave_granularity: bool | None = None,
                  exchange_shift: int | None = None, handover_spin_limit: int = 0):
         BM, BN, L, kname = TILES[tile]
+        self.tile = tile
         if M % BM or N % BN or K % 64:
             raise ValueError(f"M%{BM}, N%{BN} and K%64 must be 0 (got {M},{N},{K})")
         if split_k > 1:
@@ -305,6 +306,12 @@ class GemmBf16:
         panels upload and compute, on the two half-pipelines' streams."""
         if self.row_major_c and not resident:
             raise ValueError("row-major C tiles run device-resident computes only")
+        if self.split_k > 1 and self.cr.enqueue_mode and self.cr.enqueue_mode_async_enable:
+            # computes on async queues run concurrently; two launches of one
+            # split-K GEMM would share its partial tiles and hand-over words
+            raise ClComputeError("split-K / exchange GEMM tiles cannot run on async enqueue queues "
+                                 "(concurrent launches would share the partial-tile workspace); "
+                                 "use a single-pass tile such as 256x256pb")
         first = not self._uploaded
         self._orders[compute_id] = 0
         streamed = bool(stream_blobs) and not resident
@@ -530,6 +537,7 @@ class GemmF32(GemmBf16):
                  group_m: int = 4, wave_granularity: bool | None = None):
         # 256x256: 140 TF/s at 8192³, 91 % of hipBLASLt fp32 (profiles/gemm_f32_findings.md)
         BM, BN, L, kname = F32_TILES[tile]
+        self.tile = tile
         if M % BM or N % BN or K % 32:
             raise ValueError(f"M%{BM}, N%{BN} and K%32 must be 0 (got {M},{N},{K})")
         self.M, self.N, self.K, self.BM, self.BN, self.L, self.kernel = M, N, K, BM, BN, L, kname

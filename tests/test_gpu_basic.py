@@ -299,6 +299,37 @@ def test_gemm_benchmarked_size_verify(tile, rows):
         a.dispose()
 
 
+def test_gemm_async_queues_overlap_verified():
+    """The bench's async-queue schedule: consecutive single-pass GEMMs on
+    async enqueue queues (they overlap on the GPU) leave a correct C; a
+    split-K tile refuses that mode (its partial-tile workspace is per GEMM)."""
+    from cekirdekler_amd.cruncher import ClComputeError
+    from cekirdekler_amd.ops.gemm import GEMM_LIBS, GemmBf16
+    from cekirdekler_amd.ops.library import library
+
+    cr = ck.ClNumberCruncher(_gpu()[0], "", prebuilt=library(*GEMM_LIBS))
+    g = GemmBf16(1024, 8192, 2048, cruncher=cr, tile="256x256pb")
+    g.run(compute_id=1, resident=True)
+    cr.enqueue_mode = True
+    cr.enqueue_mode_async_enable = True
+    for _ in range(6):
+        g.run(compute_id=1, resident=True)
+    cr.enqueue_mode = False
+    cr.enqueue_mode_async_enable = False
+    assert g.verify(compute_id=1, tiles_per_device=6) < 5e-3
+    w = GemmBf16(1024, 1024, 1024, cruncher=cr, tile="256x256pbw")
+    w.run(compute_id=2, resident=True)
+    cr.enqueue_mode = True
+    cr.enqueue_mode_async_enable = True
+    try:
+        with pytest.raises(ClComputeError):
+            w.run(compute_id=2, resident=True)
+    finally:
+        cr.enqueue_mode = False
+        cr.enqueue_mode_async_enable = False
+    cr.dispose()
+
+
 @pytest.mark.parametrize("tile,panels", [("256x256pb", 4), ("256x256pb", 2), ("256x128pe", 4), ("256x256", 1)])
 def test_gemm_host_shells_matches_fp64(tile, panels):
     """Host-resident GEMM streamed in square shells (Cores::gemm_host_shells)

@@ -8,7 +8,9 @@ and reporting median / min TF/s.
 
     python tools/scale_probe.py [rows,...] [tile[:sS][:wD],...] [rounds] [steps]
 
-(``:sS`` split-K S, ``:wD`` the helper's K-tile deficit of an uneven-split tile)
+(``:sS`` split-K S, ``:wD`` the helper's K-tile deficit of an uneven-split
+tile, ``:a`` the computes on async enqueue queues — consecutive GEMMs overlap,
+as the bench's async schedule runs them)
 """
 import json
 import os
@@ -37,6 +39,7 @@ for m in rows:
         name, *opts = t.split(":")
         sk = next((int(o[1:]) for o in opts if o.startswith("s")), 1)
         wd = next((int(o[1:]) for o in opts if o.startswith("w")), None)
+        asy = "a" in opts
         try:
             g = GemmBf16(m, n, k, devices=dev, tile=name, group_m=gm, split_k=sk, exchange_shift=wd)
         except ValueError as e:
@@ -44,6 +47,7 @@ for m in rows:
             continue
         for _ in range(3):
             g.run(resident=True)
+        g.async_queues = asy
         runs[(m, t)] = g
 torch.cuda.synchronize()
 
@@ -53,9 +57,11 @@ for r in range(rounds):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         g.cr.enqueue_mode = True
+        g.cr.enqueue_mode_async_enable = g.async_queues
         for _ in range(steps):
             g.run(resident=True)
         g.cr.enqueue_mode = False
+        g.cr.enqueue_mode_async_enable = False
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / steps
         res[key].append(g.flops / ms / 1e9)
