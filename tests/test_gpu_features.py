@@ -572,10 +572,12 @@ def test_checkpoint_partitioned_device_state(gpu, tmp_path, ndev):
     it = ck.ClArray(np.zeros(1, np.int32))
     y = ck.ClArray(np.full(n, -1.0, np.float32))
     it.write = False
-    y.read = False
     y.write = False
     for k in range(5):
         it.array[0] = k
+        # the first call uploads -1 into every replica (fresh device memory
+        # may hold anything, even this array's values from an earlier test)
+        y.read = k == 0
         it.next_param(y).compute(cr, 7, "fill", n, 256)
     ranges = cr.ranges(7)
     assert len(set(ranges)) > 1, ranges
