@@ -181,7 +181,13 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
         cr.enqueue_mode = False
         cr.enqueue_mode_async_enable = False
 
-    ms_async = timed(ctx, step_a, steps, 1, enter=enter_async, leave=leave_async)
+    # untimed: one pass over every async queue, so the queues' HIP streams
+    # exist before the timed loop (creating one costs ~1 ms)
+    enter_async()
+    for _ in range(cr.compute_queue_concurrency + 1):
+        step_a()
+    leave_async()
+    ms_async = timed(ctx, step_a, steps, 0, enter=enter_async, leave=leave_async)
     err_async = _max_over_ranks(ctx, ga.verify(compute_id=cid_a))
     if ga is not g:
         for a in (ga.A, ga.B, ga.C, ga.dims):

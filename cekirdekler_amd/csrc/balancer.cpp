@@ -121,6 +121,7 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
     if (active >= 2) {
       const double ov = std::max(0.0, wall_ms - tmax);
       fs.o_multi = fs.o_multi < 0 ? ov : 0.7 * fs.o_multi + 0.3 * ov;
+      fs.multi_wall = fs.multi_wall < 0 ? wall_ms : 0.5 * fs.multi_wall + 0.5 * wall_ms;
     } else if (fs.recording_probe && alone == fs.probe_dev) {
       fs.probe_walls.push_back(wall_ms);
     } else {
@@ -212,7 +213,7 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
         single = true;
       }
     } else {
-      single = fs.single_wall[best] <= pred_multi;
+      single = fs.single_wall[best] <= std::max(pred_multi, fs.multi_wall);
     }
   }
   std::vector<double> target(n, 0.0);

@@ -23,9 +23,12 @@ namespace cek {
 // wall time as T + the measured multi-device overhead (wall − slowest
 // device).  The best single device is then run alone for a few calls, once,
 // when its predicted time is within 25 % of that, and from then on the
-// configuration with the lower wall time — measured for the single device,
-// predicted for the split — is used.  Until every device has a fit it defers
-// to the law.
+// configuration with the lower wall time is used: measured for the single
+// device; for the split the larger of the prediction and the measured wall
+// of recent split calls (a fit that misses a cost of co-execution — a CPU
+// pool's wake-ups, contention on shared hardware — cannot keep choosing a
+// split that is slower in fact).  Until every device has a fit it defers to
+// the law.
 struct FitState {
   std::vector<std::vector<std::pair<double, double>>> samples;  // per device: (range, ms), distinct ranges
   double o_multi = -1;                 // EWMA of wall − max device ms over multi-device calls
@@ -38,6 +41,7 @@ struct FitState {
   std::string decision = "law";        // law | multi | single | probe
   std::vector<double> a, b;            // last fits (ms, ms per work item)
   double predicted_multi_ms = 0;
+  double multi_wall = -1;              // EWMA wall ms of recent multi-device calls (−1: none yet)
 };
 
 constexpr int kFitSamples = 8;

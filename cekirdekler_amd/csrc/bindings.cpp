@@ -219,7 +219,8 @@ PYBIND11_MODULE(_cek, m) {
       .def_readonly("b", &FitState::b)
       .def_readonly("o_multi", &FitState::o_multi)
       .def_readonly("single_wall", &FitState::single_wall)
-      .def_readonly("predicted_multi_ms", &FitState::predicted_multi_ms);
+      .def_readonly("predicted_multi_ms", &FitState::predicted_multi_ms)
+      .def_readonly("multi_wall", &FitState::multi_wall);
   m.def("initial_split", [](int devices, bool smooth, std::vector<std::vector<double>> history,
                             long long total, long long step) {
     std::vector<long long> ranges;
@@ -453,6 +454,7 @@ PYBIND11_MODULE(_cek, m) {
         d["o_multi_ms"] = f->o_multi;
         d["single_wall_ms"] = f->single_wall;
         d["predicted_multi_ms"] = f->predicted_multi_ms;
+        d["measured_multi_ms"] = f->multi_wall;
         return d;
       })
       .def("set_dynamic_lds", &Cores::set_dynamic_lds)

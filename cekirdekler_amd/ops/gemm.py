@@ -92,8 +92,12 @@ def rows_to_tile(b: np.ndarray, geom) -> np.ndarray:
 
 # fp32 tiles (kernels/sgemm_f32.hip): v_mfma_f32_16x16x4_f32, BK = 32
 F32_TILES = {
-    # production: k block 1's fragment reads between block 0's MFMA groups
-    # (146-147 TF at 8192³, profiles/gemm_f32_findings.md)
+    # production: register-direct, 8 waves of 128×64 — fragments loaded
+    # global → VGPR, no LDS, no barrier (151.4 TF at 8192³ vs hipBLASLt 153.4
+    # and 256x256ir 138.6 on one box, profiles/gemm_f32_findings.md)
+    "256x256g8": (256, 256, 512, "cek_sgemm_f32_256x256g8"),
+    # LDS-staged: k block 1's fragment reads between block 0's MFMA groups
+    # (146-147 TF at 8192³ on earlier boxes)
     "256x256ir": (256, 256, 512, "cek_sgemm_f32_256x256ir"),
     # alternates: the barrier ahead of the last MFMA groups; v_mfma_f32_32x32x2_f32
     "256x256ib7": (256, 256, 512, "cek_sgemm_f32_256x256ib7"),
@@ -108,7 +112,6 @@ F32_TILES = {
     # fragment ties instead of scheduling barriers
     "256x256g": (256, 256, 256, "cek_sgemm_f32_256x256g"),
     "256x256gt": (256, 256, 256, "cek_sgemm_f32_256x256gt"),
-    "256x256g8": (256, 256, 512, "cek_sgemm_f32_256x256g8"),
     "256x256g8t": (256, 256, 512, "cek_sgemm_f32_256x256g8t"),
     "128x128": (128, 128, 256, "cek_sgemm_f32_128x128"),
 }
@@ -532,10 +535,9 @@ class GemmF32(GemmBf16):
     (same grouped tile order, so the same range partitioning and
     wave-quantized balancing apply)."""
 
-    def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256ir",
+    def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256g8",
                  cruncher: ClNumberCruncher | None = None, fill: str = "random", seed: int = 0,
                  group_m: int = 4, wave_granularity: bool | None = None):
-        # 256x256: 140 TF/s at 8192³, 91 % of hipBLASLt fp32 (profiles/gemm_f32_findings.md)
         BM, BN, L, kname = F32_TILES[tile]
         self.tile = tile
         if M % BM or N % BN or K % 32:

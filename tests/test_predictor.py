@@ -12,7 +12,7 @@ from cekirdekler_amd._native import cek
 
 
 def _simulate(a, b, o_multi, o_single, G=102_400, step=256, calls=40, predictor=True, noise=0.0, seed=0,
-              cold_ms=0.0, switch_ms=0.0):
+              cold_ms=0.0, switch_ms=0.0, quad=None):
     """Run the balancer against devices whose time is a_i + b_i·r_i (ms) and a
     compute whose wall time adds o_multi (≥ 2 devices) or o_single (1)."""
     rng = np.random.default_rng(seed)
@@ -23,7 +23,8 @@ def _simulate(a, b, o_multi, o_single, G=102_400, step=256, calls=40, predictor=
     walls, decisions = [], []
     prev_active = None
     for call in range(calls):
-        t = [(a[i] + b[i] * r) * (1 + noise * rng.standard_normal()) if r > 0 else 0.0 for i, r in enumerate(ranges)]
+        t = [(a[i] + b[i] * r + (quad[i] * r * r if quad else 0.0)) * (1 + noise * rng.standard_normal())
+             if r > 0 else 0.0 for i, r in enumerate(ranges)]
         if call < 2:  # the first computes of an id allocate and upload
             t = [x + cold_ms if x else 0.0 for x in t]
         active = tuple(r > 0 for r in ranges)
@@ -134,3 +135,19 @@ def test_probe_ignores_the_switch_call():
     ranges, walls, dec, fs = _simulate(a, b, o_multi=0.035, o_single=0.005, G=57_344, step=64, switch_ms=1.0)
     assert ranges == [57_344, 0] and dec[-1] == "single", (ranges, dec[-6:])
     assert fs.single_wall[0] == pytest.approx(0.05 + 5e-8 * 57_344 + 0.005, rel=1e-6)
+
+
+def test_measured_split_wall_overrides_an_optimistic_fit():
+    """The GPU+CPU wave on the GPU box (bench wave_cpu_gpu, round 4): the
+    linear fits predicted a split 10 % faster than the GPU alone, and the
+    split ran 9 % slower.  Here the second device's time grows faster than
+    linearly, so the fit from the ranges the law visited under-predicts the
+    water-filling split; the measured wall of the split calls must send the
+    compute back to the best single device."""
+    a, b = [0.03, 0.003], [1.2e-7, 2.0e-6]
+    quad = [0.0, 2.5e-10]
+    ranges, walls, dec, fs = _simulate(a, b, o_multi=0.002, o_single=0.002, G=57_344, step=64, calls=60, quad=quad)
+    single = a[0] + b[0] * 57_344 + 0.002
+    assert dec[-1] == "single" and ranges == [57_344, 0], (ranges, dec[-8:])
+    assert walls[-1] == pytest.approx(single, rel=1e-6)
+    assert fs.multi_wall > single

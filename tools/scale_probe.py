@@ -47,6 +47,13 @@ for m in rows:
             continue
         for _ in range(3):
             g.run(resident=True)
+        if asy:  # create the async queues' streams before timing
+            g.cr.enqueue_mode = True
+            g.cr.enqueue_mode_async_enable = True
+            for _ in range(g.cr.compute_queue_concurrency + 1):
+                g.run(resident=True)
+            g.cr.enqueue_mode = False
+            g.cr.enqueue_mode_async_enable = False
         g.async_queues = asy
         runs[(m, t)] = g
 torch.cuda.synchronize()
