@@ -1,14 +1,19 @@
 #!/bin/bash
-# Second GPU session of the round: a kernel trace of the headline bench, then
-# multi-rank rehearsals of the bench on the one GPU (ranks share GPU 0; the
-# 8-GPU run is the driver's).  Every step has its own time limit; a failing
-# step ends the call.
+# Second GPU session of the round: the headline bench, its kernel trace, one
+# counter pass over the fp32 GEMM tiles, then multi-rank rehearsals of the
+# bench on the one GPU (ranks share GPU 0; the 8-GPU run is the driver's).
+# Every step has its own time limit; a failing step ends the call.
 set -o pipefail
 out=${1:-gpurun_out/runb}
 mkdir -p "$out"
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$out/prof" -o bench -- python3 bench.py --steps 10 --warmup 2 \
+export TMPDIR=/tmp
+timeout -k 10 400 python bench.py > "$out/bench.json" 2> "$out/bench.err" || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof" -o bench -- python3 bench.py --steps 10 --warmup 2 \
   --skip-node-configs > "$out/prof_bench.json" 2> "$out/prof_bench.err" || exit $?
+timeout -k 10 200 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
+  -d "$out/f32_pmc" -o run --output-format csv -- python3 tools/gemm_f32_pmc.py 256x256g8,256x256ir torch \
+  > "$out/f32_pmc.log" 2>&1 || exit $?
+[ -n "$CEK_SKIP_RANKS" ] && exit 0
 timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 2 --skip-node-configs --skip-mandelbrot \
   > "$out/bench_2r.json" 2> "$out/bench_2r.err" || exit $?
 timeout -k 10 400 python bench.py --gpus 4 --size 4096 --steps 5 --warmup 2 --skip-node-configs --skip-mandelbrot \
