@@ -72,6 +72,75 @@ def variant(name, B, prefetch, tile, unroll):
     return "\n".join(s) + "\n"
 
 
+def variant_js(name, B, S):
+    """j-split: a work-group's 256 threads form S groups that take the same
+    256·B/S bodies (B per thread, packed pairs) against S different 256-body
+    tiles of each LDS load, and add their partial accelerations through LDS
+    at the end: S times the waves for the same body share (more latency
+    hiding when one GPU holds a quarter of the bodies).  A work item owns
+    B/S bodies of each output."""
+    NP, T = B // 2, 256 // S
+    s = [f"__global__ __launch_bounds__(256) void {name}(const float4* pos, const float4* vel, const float* prm,",
+         "    float4* pos_o, float4* vel_o, float4* acc_o) {",
+         f"  __shared__ float4 t[{256 * S}];",
+         "  const int n = (int)prm[2];",
+         "  const f2 e2 = {prm[0], prm[0]};",
+         "  const int l = threadIdx.x;",
+         f"  const int grp = l / {T}, m = l % {T};",
+         f"  const long long i0 = (get_global_id(0) / 256) * {T * B} + m;  // pair p: bodies i0 + 2p·{T}, i0 + (2p+1)·{T}",
+         f"  f2 px[{NP}], py[{NP}], pz[{NP}], ax[{NP}], ay[{NP}], az[{NP}];",
+         f"  for (int p = 0; p < {NP}; ++p) {{",
+         f"    const float4 b0 = pos[i0 + (2 * p) * {T}], b1 = pos[i0 + (2 * p + 1) * {T}];",
+         "    px[p] = f2{b0.x, b1.x}; py[p] = f2{b0.y, b1.y}; pz[p] = f2{b0.z, b1.z};",
+         "    ax[p] = ay[p] = az[p] = f2{0.f, 0.f};",
+         "  }",
+         f"  float4 nx[{S}];",
+         f"  for (int k = 0; k < {S}; ++k) nx[k] = pos[k * 256 + l];",
+         f"  for (int j0 = 0; j0 < n; j0 += {256 * S}) {{",
+         "    __syncthreads();",
+         f"    for (int k = 0; k < {S}; ++k) t[k * 256 + l] = nx[k];",
+         "    __syncthreads();",
+         f"    if (j0 + {256 * S} < n) for (int k = 0; k < {S}; ++k) nx[k] = pos[j0 + {256 * S} + k * 256 + l];",
+         "    const float4* tg = t + grp * 256;",
+         "#pragma unroll 8",
+         "    for (int j = 0; j < 256; ++j) {",
+         "      const float4 q = tg[j];",
+         "      const f2 qx = {q.x, q.x}, qy = {q.y, q.y}, qz = {q.z, q.z}, qm = {q.w, q.w};",
+         "#pragma unroll",
+         f"      for (int p = 0; p < {NP}; ++p) {{",
+         "        const f2 dx = qx - px[p], dy = qy - py[p], dz = qz - pz[p];",
+         "        const f2 r2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, __builtin_elementwise_fma(dz, dz, e2)));",
+         "        const f2 inv = {__builtin_amdgcn_rsqf(r2.x), __builtin_amdgcn_rsqf(r2.y)};",
+         "        const f2 sc = (qm * inv) * (inv * inv);",
+         "        ax[p] = __builtin_elementwise_fma(dx, sc, ax[p]);",
+         "        ay[p] = __builtin_elementwise_fma(dy, sc, ay[p]);",
+         "        az[p] = __builtin_elementwise_fma(dz, sc, az[p]);",
+         "      }", "    }", "  }",
+         "  // groups 1..S-1 hand their partial sums to group 0 through LDS",
+         "  __syncthreads();",
+         "  float* red = (float*)t;",
+         f"  if (grp > 0) for (int p = 0; p < {NP}; ++p) {{",
+         f"    float* r = red + (((grp - 1) * {NP} + p) * {T} + m) * 6;",
+         "    r[0] = ax[p].x; r[1] = ax[p].y; r[2] = ay[p].x; r[3] = ay[p].y; r[4] = az[p].x; r[5] = az[p].y;",
+         "  }",
+         "  __syncthreads();",
+         "  if (grp == 0) {",
+         f"    for (int g = 1; g < {S}; ++g) for (int p = 0; p < {NP}; ++p) {{",
+         f"      const float* r = red + (((g - 1) * {NP} + p) * {T} + m) * 6;",
+         "      ax[p] += f2{r[0], r[1]}; ay[p] += f2{r[2], r[3]}; az[p] += f2{r[4], r[5]};",
+         "    }",
+         f"    for (int p = 0; p < {NP}; ++p) {{",
+         f"      const long long a = i0 + (2 * p) * {T}, b = a + {T};",
+         "      acc_o[a] = make_float4(ax[p].x, ay[p].x, az[p].x, 0.f);",
+         "      acc_o[b] = make_float4(ax[p].y, ay[p].y, az[p].y, 0.f);",
+         "      pos_o[a] = pos[a]; pos_o[b] = pos[b]; vel_o[a] = vel[a]; vel_o[b] = vel[b];",
+         "    }",
+         "  }", "}"]
+    return "\n".join(s) + "\n"
+
+
+JS_VARIANTS = {"b2_js2": (2, 2), "b4_js2": (4, 2), "b2_js4": (2, 4)}  # name: (B, S)
+
 VARIANTS = {  # name: (B, prefetch, tile, unroll)
     "b2_plain": (2, False, 256, 8),
     "b2_pf": (2, True, 256, 8),
@@ -84,7 +153,11 @@ VARIANTS = {  # name: (B, prefetch, tile, unroll)
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
     fracs = [float(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,0.5,0.25").split(",")]
-    src = HEAD + "".join(variant(k, *v) for k, v in VARIANTS.items())
+    src = HEAD + "".join(variant(k, *v) for k, v in VARIANTS.items()) + "".join(
+        variant_js(k, *v) for k, v in JS_VARIANTS.items())
+    # work items per body: B bodies per item, S items per body group for j-split
+    per_item = {k: (v[0], 1) for k, v in VARIANTS.items()}
+    per_item.update({k: (v[0], v[1]) for k, v in JS_VARIANTS.items()})
     g0 = ck.ClPlatforms.all().gpus()[0]
     cr = ck.ClNumberCruncher(g0, src)
     if cr.error_code():
@@ -106,8 +179,8 @@ def main():
     cid = 1
     ref_acc = None
     for f in fracs:
-        for name, (B, *_rest) in VARIANTS.items():
-            g = int(n // B * f) // 256 * 256
+        for name, (B, S) in per_item.items():
+            g = int(n * S // B * f) // 256 * 256
             call = lambda: arrs[0].next_param(*arrs[1:]).compute(cr, cid, name, g, 256)  # noqa: E731
             call()
             torch.cuda.synchronize()
@@ -117,9 +190,10 @@ def main():
                 call()
                 torch.cuda.synchronize()
                 best = min(best, (time.perf_counter() - t) * 1e3)
-            inter = g * B * n
+            bodies = g * B // S
+            inter = bodies * n
             cr.download(arrs[5], 0)
-            acc = arrs[5].array[: 4 * g * B].copy()
+            acc = arrs[5].array[: 4 * bodies].copy()
             if ref_acc is None or len(ref_acc) != len(acc):
                 ref_acc = acc
             err = float(np.abs(acc - ref_acc).max() / max(np.abs(ref_acc).max(), 1e-30))
