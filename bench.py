@@ -586,10 +586,11 @@ def _peer_topology(world: int) -> dict:
     from cekirdekler_amd.utils.multigpu import peer_bandwidth_report
 
     full = cek.can_access_peer_matrix()
-    m = [row[:world] for row in full[:world]]
+    ngpu = min(world, len(full))  # ranks may share a GPU (one-GPU rehearsals)
+    m = [row[:ngpu] for row in full[:ngpu]]
     out = {"gpus_visible": len(full), "job_gpus": world, "can_access_peer": m, "path": cek.peer_path(m)}
     try:  # an extra: a failure is reported in its field
-        out["bandwidth"] = peer_bandwidth_report(list(range(world)))
+        out["bandwidth"] = peer_bandwidth_report(list(range(ngpu)))
     except Exception as e:  # pragma: no cover
         out["bandwidth"] = {"error": repr(e)[:300]}
     return out

@@ -48,32 +48,40 @@ from cekirdekler_amd.parallel.pipeline import ClPipelineStage, _intersection
 FORCE = r"""
 // 2 bodies per work item as one packed f32x2 pair (v_pk_* issue: see
 // kernels/nbody.hip), written as a user kernel string and JIT-compiled by
-// hiprtc.  Work-group g owns bodies [512 g, 512 g + 512), so a device's range
-// of whole work-groups owns one contiguous body range.  Two bodies per item
-// (not four) keep 4+ work-groups per CU when the force stage is split over
-// 2-6 GPUs.  The next LDS tile of bodies is loaded into registers while the
-// current one is consumed (as in kernels/nbody.hip), so its global-load
-// latency hides behind 256 interactions.
+// hiprtc.  j-split: the work-group's 256 threads are two groups of 128 that
+// hold the same 256 bodies (work-group g owns bodies [256 g, 256 g + 256),
+// so a device's range of whole work-groups owns one contiguous body range)
+// and take the two halves of every 512-body LDS load; the halves' partial
+// accelerations are added through LDS at the end.  Twice the waves of a
+// 2-bodies-per-item kernel for the same body share: with a quarter of the
+// bodies per GPU (the force stage on four GPUs) that is 51.0 % of the FP32
+// peak against 48.9 % (tools/nbody_force_variants.py, profiles/round4_session2.md).
+// The next LDS load is held in registers while the current one is consumed.
 typedef float f2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void force(const float4* pos, const float4* vel, const float* prm,
                                              float4* pos_o, float4* vel_o, float4* acc_o) {
-  __shared__ float4 tile[256];
+  __shared__ float4 tile[512];
   const int n = (int)prm[2];
   const f2 e2 = {prm[0], prm[0]};
-  const long long w = get_global_id(0);
-  const long long i0 = (w / 256) * 512 + (w % 256);
-  const float4 b0 = pos[i0], b1 = pos[i0 + 256];
+  const int l = threadIdx.x, grp = l >> 7, m = l & 127;
+  const long long i0 = (get_global_id(0) / 256) * 256 + m;  // bodies i0 and i0 + 128
+  const float4 b0 = pos[i0], b1 = pos[i0 + 128];
   const f2 px = {b0.x, b1.x}, py = {b0.y, b1.y}, pz = {b0.z, b1.z};
   f2 ax = {0.f, 0.f}, ay = ax, az = ax;
-  float4 next = pos[threadIdx.x];
-  for (int j0 = 0; j0 < n; j0 += 256) {
+  float4 nx0 = pos[l], nx1 = pos[256 + l];
+  for (int j0 = 0; j0 < n; j0 += 512) {
     __syncthreads();
-    tile[threadIdx.x] = next;
+    tile[l] = nx0;
+    tile[256 + l] = nx1;
     __syncthreads();
-    if (j0 + 256 < n) next = pos[j0 + 256 + threadIdx.x];
+    if (j0 + 512 < n) {
+      nx0 = pos[j0 + 512 + l];
+      nx1 = pos[j0 + 768 + l];
+    }
+    const float4* tg = tile + grp * 256;
 #pragma unroll 8
     for (int j = 0; j < 256; ++j) {
-      const float4 q = tile[j];
+      const float4 q = tg[j];
       const f2 qx = {q.x, q.x}, qy = {q.y, q.y}, qz = {q.z, q.z}, qm = {q.w, q.w};
       const f2 dx = qx - px, dy = qy - py, dz = qz - pz;
       const f2 r2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, __builtin_elementwise_fma(dz, dz, e2)));
@@ -84,10 +92,21 @@ __global__ __launch_bounds__(256) void force(const float4* pos, const float4* ve
       az = __builtin_elementwise_fma(dz, sc, az);
     }
   }
-  acc_o[i0] = make_float4(ax.x, ay.x, az.x, 0.f);
-  acc_o[i0 + 256] = make_float4(ax.y, ay.y, az.y, 0.f);
-  pos_o[i0] = b0; pos_o[i0 + 256] = b1;
-  vel_o[i0] = vel[i0]; vel_o[i0 + 256] = vel[i0 + 256];
+  __syncthreads();
+  float* red = (float*)tile;
+  if (grp == 1) {
+    float* r = red + m * 6;
+    r[0] = ax.x; r[1] = ax.y; r[2] = ay.x; r[3] = ay.y; r[4] = az.x; r[5] = az.y;
+  }
+  __syncthreads();
+  if (grp == 0) {
+    const float* r = red + m * 6;
+    ax += f2{r[0], r[1]}; ay += f2{r[2], r[3]}; az += f2{r[4], r[5]};
+    acc_o[i0] = make_float4(ax.x, ay.x, az.x, 0.f);
+    acc_o[i0 + 128] = make_float4(ax.y, ay.y, az.y, 0.f);
+    pos_o[i0] = b0; pos_o[i0 + 128] = b1;
+    vel_o[i0] = vel[i0]; vel_o[i0 + 128] = vel[i0 + 128];
+  }
 }
 """
 KICK = r"""
@@ -164,18 +183,16 @@ else:
 f4 = lambda: np.zeros(4 * n, np.float32)  # noqa: E731
 prm = np.array([1e-4, 1.0, float(n), 1e-3], np.float32)
 s1, s2, s3 = ClPipelineStage(), ClPipelineStage(), ClPipelineStage()
-s1.add_devices(devs[0]); s1.add_kernels(FORCE, "force", [n // 2], [256])
+s1.add_devices(devs[0]); s1.add_kernels(FORCE, "force", [n], [256])
 s1.add_input_buffers(f4(), f4()); s1.add_hidden_buffers(prm.copy()); s1.add_output_buffers(f4(), f4(), f4())
 s2.add_devices(devs[1]); s2.add_kernels(KICK, "kick", [n], [256])
 s2.add_input_buffers(f4(), f4(), f4()); s2.add_hidden_buffers(prm.copy()); s2.add_output_buffers(f4(), f4())
 s3.add_devices(devs[2]); s3.add_kernels(ENERGY, "energy", [n], [256])
 s3.add_input_buffers(f4(), f4()); s3.add_output_buffers(f4(), f4(), np.zeros(n // 256, np.float32))
-# slice ownership in multi-device stages: a force work item owns 2 bodies
-# (8 floats) of each output, a kick / energy work item one body (4 floats),
-# an energy work-group one partial sum
-for arr in s1.outputs:
-    arr.elements_per_work_item = 8
-for arr in s2.outputs + s3.outputs[:2]:
+# slice ownership in multi-device stages: a force, kick or energy work item
+# owns one body (4 floats) of each output (a force work-group of 256 items
+# holds 256 bodies), an energy work-group one partial sum
+for arr in s1.outputs + s2.outputs + s3.outputs[:2]:
     arr.elements_per_work_item = 4
 s3.outputs[2].elements_per_group = 1
 s1.prepend_to_stage(s2)
