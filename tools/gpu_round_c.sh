@@ -1,0 +1,16 @@
+#!/bin/bash
+# Third GPU session: the GPU tier on the current tree, the j-split N-body
+# pipeline (four logical devices), PCIe issue-pattern and host-resident
+# panel-count probes, the headline bench.  Each step has its own time limit;
+# a failing step ends the call.
+set -o pipefail
+out=${1:-gpurun_out/runc}
+mkdir -p "$out"
+export TMPDIR=/tmp
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+  > "$out/gputests.log" 2>&1 || exit $?
+timeout -k 10 240 python bench/nbody_pipeline.py --gpus 4 --logical 4 --pushes 12 > "$out/nbody_shared.json" \
+  2> "$out/nbody_shared.err" || exit $?
+timeout -k 10 120 python tools/h2d_chunks_probe.py "$out/h2d_chunks.json" > /dev/null 2> "$out/h2d_chunks.err" || exit $?
+timeout -k 10 240 python tools/hostres_probe.py 8,16,32 4 > "$out/hostres_panels.json" 2> "$out/hostres_panels.err" || exit $?
+timeout -k 10 400 python bench.py > "$out/bench.json" 2> "$out/bench.err" || exit $?

@@ -4,7 +4,7 @@ shell entry point, a few calls each, with wall times.  Run it under
 ``rocprofv3 --kernel-trace --memory-copy-trace`` to see when every upload,
 kernel and download of a call ran.
 
-    python tools/hostres_probe.py [panels] [calls]
+    python tools/hostres_probe.py [panels,...] [calls]
 """
 import json
 import os
@@ -18,13 +18,15 @@ import cekirdekler_amd as ck  # noqa: E402
 from cekirdekler_amd.ops.gemm import GEMM_LIBS, GemmBf16  # noqa: E402
 from cekirdekler_amd.ops.library import library  # noqa: E402
 
-panels = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+panel_list = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "16").split(",")]
 calls = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 cr = ck.ClNumberCruncher(ck.ClPlatforms.all().gpus()[0], "", prebuilt=library(*GEMM_LIBS))
 g = GemmBf16(8192, 8192, 8192, cruncher=cr, tile="256x256pb")
-out = {"panels": panels}
-for name, fn in (("compute_shells", lambda: g.run_shells(panels, compute_id=3)),
-                 ("native_shells", lambda: g.run_host_shells(panels))):
+out = {"panels": panel_list}
+runs = [(f"compute_shells_p{p}", (lambda p=p, i=i: g.run_shells(p, compute_id=3 + i)))
+        for i, p in enumerate(panel_list)]
+runs.append((f"native_shells_p{panel_list[0]}", lambda: g.run_host_shells(panel_list[0])))
+for name, fn in runs:
     fn()
     torch.cuda.synchronize()
     ms = []
