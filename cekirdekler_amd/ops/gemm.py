@@ -338,22 +338,35 @@ class GemmBf16:
             granularity=gran)
         self._uploaded = True
 
-    def shell_bounds(self, panels: int):
+    def shell_bounds(self, panels: int, split_last: int = 0):
         """Work-item bounds of the square shells (blob s = shell s) and the
-        per-blob row panels of A and B, for :meth:`run_shells`."""
+        per-blob row panels of A and B, for :meth:`run_shells`.  The last
+        ``split_last`` shells become two blobs each, ``R_s`` (which uploads
+        panels A_s and B_s) and ``C_s`` (no upload), so ``R_s``'s C tiles
+        come down while ``C_s`` multiplies: the call's tail after the last
+        upload is ``C_s`` alone."""
         P = int(panels)
         if self.split_k != 1:
             raise ValueError("shell streaming runs single-pass tiles (split_k == 1)")
         if P < 1 or self.M % P or self.N % P or (self.M // P) % self.BM or (self.N // P) % self.BN:
             raise ValueError(f"M and N must split into {P} panels of whole {self.BM}x{self.BN} tiles")
         pm, pn = self.M // P // self.BM, self.N // P // self.BN
-        bounds = [pm * pn * (s * s) * self.L for s in range(P + 1)]
         a_rows, b_rows = self.M // P, self.N // P
-        a_sl = [(k * a_rows * self.K, a_rows * self.K) for k in range(P)]
-        b_sl = [(k * b_rows * self.K, b_rows * self.K) for k in range(P)]
+        unit = pm * pn * self.L  # work items of one panel × panel block
+        bounds, a_sl, b_sl = [0], [], []
+        for k in range(P):
+            a_panel, b_panel = (k * a_rows * self.K, a_rows * self.K), (k * b_rows * self.K, b_rows * self.K)
+            if k >= P - int(split_last) and k > 0:
+                bounds += [(k * k + k + 1) * unit, (k + 1) * (k + 1) * unit]  # R_k, then C_k
+                a_sl += [a_panel, (0, 0)]
+                b_sl += [b_panel, (0, 0)]
+            else:
+                bounds.append((k + 1) * (k + 1) * unit)
+                a_sl.append(a_panel)
+                b_sl.append(b_panel)
         return bounds, a_sl, b_sl
 
-    def run_shells(self, panels: int = 16, compute_id: int = 2) -> None:
+    def run_shells(self, panels: int = 16, compute_id: int = 2, split_last: int = 0) -> None:
         """One host-resident call through ``compute()``: the event-driven
         read/compute/write pipeline with explicit, uneven blobs — blob s is
         square shell s (``R_s = A_s·B[0..s]ᵀ`` then ``C_s = A[0..s-1]·B_sᵀ``,
@@ -362,7 +375,7 @@ class GemmBf16:
         and every shell's C comes down (one contiguous range) while later
         panels go up.  The first kernels need two panels instead of all of
         B.  One device holds the range (several: the plain path)."""
-        bounds, a_sl, b_sl = self.shell_bounds(panels)
+        bounds, a_sl, b_sl = self.shell_bounds(panels, split_last)
         if getattr(self, "_dims_shell", None) is None or int(self._dims_shell.array[6]) != panels:
             d = self.dims.array.copy()
             d[6] = panels

@@ -47,3 +47,33 @@ def test_shell_bounds_cover_every_tile(cpu_cr):
         assert ((tm[lo:hi] // 2 == s) | (tn[lo:hi] // 2 == s)).all()
     with pytest.raises(ValueError):
         g.shell_bounds(3)
+
+
+@pytest.mark.parametrize("split_last", [1, 2, 4])
+def test_shell_bounds_split_last_shells(cpu_cr, split_last):
+    """The last shells split into R_s (row panel s, which uploads A_s and B_s)
+    and C_s (column panel s above it, no upload); every blob holds exactly
+    its part's tiles and only R_s blobs upload."""
+    g = GemmBf16(2048, 2048, 256, cruncher=cpu_cr, tile="256x256pb")
+    P, pt = 4, 2  # 4 panels of 2 tiles each way
+    bounds, a_sl, b_sl = g.shell_bounds(P, split_last)
+    nsplit = min(split_last, P - 1)
+    assert len(bounds) == P + 1 + nsplit and bounds[-1] == g.global_range
+    assert sum(n for _, n in a_sl) == g.A.N and sum(n for _, n in b_sl) == g.B.N
+    t = np.arange(g.tiles)
+    tm, tn = tile_coords(t, 2048, 2048, 256, 256, g.group_m, P)
+    q = 0
+    for s in range(P):
+        parts = ("R", "C") if s >= P - split_last and s > 0 else ("RC",)
+        for part in parts:
+            lo, hi = bounds[q] // g.L, bounds[q + 1] // g.L
+            rows, cols = tm[lo:hi] // pt, tn[lo:hi] // pt
+            if part == "R":
+                assert (rows == s).all() and (cols <= s).all() and hi - lo == (s + 1) * pt * pt
+                assert a_sl[q][1] > 0 and b_sl[q][1] > 0
+            elif part == "C":
+                assert (cols == s).all() and (rows < s).all() and hi - lo == s * pt * pt
+                assert a_sl[q][1] == 0 and b_sl[q][1] == 0
+            else:
+                assert ((rows == s) | (cols == s)).all()
+            q += 1

@@ -387,8 +387,9 @@ def test_mandelbrot_two_frames_in_flight_async_enqueue():
     cr.dispose()
 
 
-@pytest.mark.parametrize("tile,panels", [("256x256pb", 4), ("256x256pb", 2), ("256x128pe", 4)])
-def test_gemm_shells_through_compute(tile, panels):
+@pytest.mark.parametrize("tile,panels,split", [("256x256pb", 4, 0), ("256x256pb", 2, 0), ("256x128pe", 4, 0),
+                                               ("256x256pb", 4, 2), ("256x256pb", 4, 4)])
+def test_gemm_shells_through_compute(tile, panels, split):
     """Host-resident GEMM streamed in square shells THROUGH compute(): the
     event pipeline with explicit uneven blobs (blob s = shell s), A and B
     uploaded one row panel per blob, C downloaded shell by shell — the
@@ -401,7 +402,7 @@ def test_gemm_shells_through_compute(tile, panels):
     ref = g.reference()
     for _ in range(2):
         g.C.array[:] = np.nan
-        g.run_shells(panels, compute_id=3)
+        g.run_shells(panels, compute_id=3, split_last=split)
         rec = cr.last_record()
         assert rec["pipelined"], rec
         assert rec["h2d_bytes"] == g.A.array.nbytes + g.B.array.nbytes + g.dims.array.nbytes, rec

@@ -25,6 +25,9 @@ g = GemmBf16(8192, 8192, 8192, cruncher=cr, tile="256x256pb")
 out = {"panels": panel_list}
 runs = [(f"compute_shells_p{p}", (lambda p=p, i=i: g.run_shells(p, compute_id=3 + i)))
         for i, p in enumerate(panel_list)]
+# the last shells split into R_s / C_s blobs (16 panels)
+runs += [(f"compute_shells_p16_split{k}", (lambda k=k: g.run_shells(16, compute_id=20 + k, split_last=k)))
+         for k in (2, 4, 8)]
 runs.append((f"native_shells_p{panel_list[0]}", lambda: g.run_host_shells(panel_list[0])))
 for name, fn in runs:
     fn()
