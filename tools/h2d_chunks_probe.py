@@ -10,6 +10,7 @@ Cases (256 MiB up, optionally 256 MiB down at the same time):
   chunks_32_ev    the same with an event recorded after every second copy
                   (the event pipeline records one per blob)
   chunks_16x16    16 MiB chunks
+  two_streams_32  the 32 chunks alternating between two streams (two SDMA queues)
   duplex_32       chunks_32 up while 32 x 8 MiB go down on another stream
 """
 import json
@@ -49,6 +50,14 @@ def main():
                 if ev and i % 2 == 1:
                     evs[i // 2].record(up)
 
+    up2 = torch.cuda.Stream()
+
+    def two_streams(size):
+        k = N // size
+        for i in range(k):
+            with torch.cuda.stream(up if i % 2 == 0 else up2):
+                dev[i * size:(i + 1) * size].copy_(host[i * size:(i + 1) * size], non_blocking=True)
+
     def duplex():
         with torch.cuda.stream(dn):
             for i in range(32):
@@ -59,6 +68,7 @@ def main():
            "chunks_32_ms": timed(lambda: chunks(8 * MB)),
            "chunks_32_ev_ms": timed(lambda: chunks(8 * MB, True)),
            "chunks_16x16_ms": timed(lambda: chunks(16 * MB)),
+           "two_streams_32_ms": timed(lambda: two_streams(8 * MB)),
            "duplex_32_ms": timed(duplex),
            "down_alone_32_ms": timed(lambda: [host_dn[i * 8 * MB:(i + 1) * 8 * MB].copy_(
                dev_dn[i * 8 * MB:(i + 1) * 8 * MB], non_blocking=True) for i in range(32)])}
