@@ -13,4 +13,5 @@ timeout -k 10 240 python bench/nbody_pipeline.py --gpus 4 --logical 4 --pushes 1
   2> "$out/nbody_shared.err" || exit $?
 timeout -k 10 120 python tools/h2d_chunks_probe.py "$out/h2d_chunks.json" > /dev/null 2> "$out/h2d_chunks.err" || exit $?
 timeout -k 10 240 python tools/hostres_probe.py 8,16,32 4 > "$out/hostres_panels.json" 2> "$out/hostres_panels.err" || exit $?
+CEK_DEVICE_SPANS=0 timeout -k 10 180 python tools/fanout_probe.py "$out/fanout_nospans.json" > "$out/fanout_nospans.log" 2>&1 || exit $?
 timeout -k 10 400 python bench.py > "$out/bench.json" 2> "$out/bench.err" || exit $?
