@@ -869,16 +869,30 @@ void Cores::launch_kernels_body(Worker& wk, hipStream_t s, const ComputeCall& c,
 // enqueued batch when the mode is left).
 bool Cores::spans_on() const { return device_spans && !(enqueue_mode_ && global_devices_ == 1); }
 
+// An enqueued batch gets one span per device (opened by its first compute,
+// closed when the mode is left) when no two local devices share a GPU: one
+// local device (a rank of a distributed job) or distinct GPUs in one
+// process.  Logical devices of one GPU keep a span per compute — their
+// batches overlap on shared hardware, and only per-compute spans separate
+// their busy time.
+bool Cores::one_span_per_batch() const {
+  if (!enqueue_mode_ || async_enqueue) return false;
+  std::vector<int> ords;
+  for (int w = 0; w < num_devices(); ++w) {
+    if (!workers_[w]->gpu()) continue;
+    const int o = workers_[w]->dev().ordinal;
+    if (std::find(ords.begin(), ords.end(), o) != ords.end()) return false;
+    ords.push_back(o);
+  }
+  return true;
+}
+
 void Cores::span_begin(Worker& wk, hipStream_t s) {
   if (!wk.gpu() || !spans_on()) return;
   const int w = worker_index(wk);
   DevSpans& d = spans_[w];
-  if (enqueue_mode_ && !async_enqueue && num_devices() == 1) {
-    // one local device on one stream (a rank of a distributed job): one span
-    // for the whole enqueued batch, opened by its first compute and closed
-    // when the mode is left (close_batch_spans), so no event marker sits
-    // between two back-to-back computes; several local devices keep a span
-    // per compute (their batches overlap on shared hardware)
+  if (one_span_per_batch()) {
+    // no event marker sits between two back-to-back computes of the batch
     if (d.used > 0) return;
     if (d.pool.empty()) {
       hipEvent_t a, b;
@@ -910,7 +924,7 @@ void Cores::span_begin(Worker& wk, hipStream_t s) {
 void Cores::span_end(Worker& wk, hipStream_t s) {
   if (!wk.gpu() || !spans_on()) return;
   DevSpans& d = spans_[worker_index(wk)];
-  if (enqueue_mode_ && !async_enqueue && num_devices() == 1) return;  // closed at the mode's end
+  if (one_span_per_batch()) return;  // closed at the mode's end
   const int i = enqueue_mode_ ? d.used - 1 : 0;
   if (i < 0) return;
   CEK_HIP(hipEventRecord(d.pool[i].second, s));

@@ -479,6 +479,7 @@ class Cores {
   bool zc_release = true;
  private:
   bool spans_on() const;
+  bool one_span_per_batch() const;
   void close_batch_spans();
   void span_begin(Worker& wk, hipStream_t s);
   void span_end(Worker& wk, hipStream_t s);
