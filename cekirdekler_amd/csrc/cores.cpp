@@ -1562,7 +1562,11 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
   }
   const int D = global_devices_;
   const int nloc = num_devices();
-  const long long B = std::max(1, c.blobs);
+  // equal blobs split every device's range, so ranges move in steps of
+  // blobs × unit; explicit blob bounds describe the whole range of the one
+  // holding device and put no constraint on the step (their count need not
+  // divide the range: 16 square shells plus split ones)
+  const long long B = c.blob_bounds.empty() ? std::max(1, c.blobs) : 1;
   const bool pipe_req = c.pipeline && !cfg_.no_pipelining;
   const long long U = c.granularity > 0 ? c.granularity : L;  // balancer unit
   if (U % L != 0) throw Error("granularity must be a multiple of the local range");

@@ -80,6 +80,9 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   // t, so a device's contiguous tile range is still one contiguous slice.
   const int ntn = N / BN, ntm = M / BM;
   int tm, tn;
+  // a launch wider than the tile grid (a host-side range error) must not
+  // read or write past A, B or C: surplus work-groups leave at once
+  if (t >= (long long)ntm * ntn) return;
   cek_tile_coords(t, ntm, ntn, GM, dims[6], tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 

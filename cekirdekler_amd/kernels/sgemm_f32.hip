@@ -39,6 +39,9 @@ __device__ __forceinline__ void gemm_f32_tile(const int* __restrict__ dims, cons
   const long long t = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
   const int ntn = N / BN, ntm = M / BM;
   int tm, tn;
+  // a launch wider than the tile grid (a host-side range error) must not
+  // read or write past A, B or C: surplus work-groups leave at once
+  if (t >= (long long)ntm * ntn) return;
   cek_tile_coords(t, ntm, ntn, GM, dims[6], tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
@@ -292,6 +295,9 @@ __device__ __forceinline__ void gemm_f32w_tile(const int* __restrict__ dims, con
   const long long t = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
   const int ntn = N / BN, ntm = M / BM;
   int tm, tn;
+  // a launch wider than the tile grid (a host-side range error) must not
+  // read or write past A, B or C: surplus work-groups leave at once
+  if (t >= (long long)ntm * ntn) return;
   cek_tile_coords(t, ntm, ntn, GM, dims[6], tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
@@ -427,6 +433,9 @@ __device__ __forceinline__ void gemm_f32_direct(const int* __restrict__ dims, co
   const long long t = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
   const int ntn = N / BN, ntm = M / BM;
   int tm, tn;
+  // a launch wider than the tile grid (a host-side range error) must not
+  // read or write past A, B or C: surplus work-groups leave at once
+  if (t >= (long long)ntm * ntn) return;
   cek_tile_coords(t, ntm, ntn, GM, dims[6], tm, tn);
   const int fr = lane & 15, fq = lane >> 4;
   const float* a_base = A + (size_t)tm * BM * K;

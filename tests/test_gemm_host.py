@@ -77,3 +77,18 @@ def test_shell_bounds_split_last_shells(cpu_cr, split_last):
             else:
                 assert ((rows == s) | (cols == s)).all()
             q += 1
+
+
+def test_explicit_blob_count_does_not_stretch_the_range():
+    """Explicit blob bounds whose count does not divide the range (split
+    shells: 6 blobs over 16 tiles) leave the one device's range at exactly the
+    global range; the equal-blob step (blobs × unit) once rounded it up to
+    18 tiles, launching two work-groups past C."""
+    src = ("__global__ void cek_sgemm_bf16_256x256pb(const int* d, const unsigned short* a, "
+           "const unsigned short* b, float* c) {}")
+    cr = ck.ClNumberCruncher(ck.ClPlatforms.all().cpus(True), src)
+    g = GemmBf16(1024, 1024, 512, cruncher=cr, tile="256x256pb")
+    for split in (0, 2, 3):
+        g.run_shells(4, compute_id=3 + split, split_last=split)
+        assert cr.ranges(3 + split) == [g.global_range]
+    cr.dispose()
