@@ -10,7 +10,7 @@ and reporting median / min TF/s.
 
 (``:sS`` split-K S, ``:wD`` the helper's K-tile deficit of an uneven-split
 tile, ``:a`` the computes on async enqueue queues — consecutive GEMMs overlap,
-as the bench's async schedule runs them)
+as the bench's async schedule runs them; ``:qN`` N async queues per device)
 """
 import json
 import os
@@ -40,8 +40,14 @@ for m in rows:
         sk = next((int(o[1:]) for o in opts if o.startswith("s")), 1)
         wd = next((int(o[1:]) for o in opts if o.startswith("w")), None)
         asy = "a" in opts
+        qc = next((int(o[1:]) for o in opts if o.startswith("q")), 0)  # async queues per device
         try:
-            g = GemmBf16(m, n, k, devices=dev, tile=name, group_m=gm, split_k=sk, exchange_shift=wd)
+            cr = None
+            if qc:
+                from cekirdekler_amd.ops.gemm import GEMM_LIBS
+                from cekirdekler_amd.ops.library import library
+                cr = ck.ClNumberCruncher(dev, "", prebuilt=library(*GEMM_LIBS), queue_concurrency=qc)
+            g = GemmBf16(m, n, k, devices=dev, tile=name, group_m=gm, split_k=sk, exchange_shift=wd, cruncher=cr)
         except ValueError as e:
             print(f"skip {m}/{t}: {e}", flush=True)
             continue
