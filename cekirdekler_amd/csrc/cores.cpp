@@ -1276,6 +1276,21 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
   const bool explicit_blobs = !c.blob_bounds.empty();
   const long long nblob = explicit_blobs ? static_cast<long long>(c.blob_bounds.size()) - 1 : per_half * halves;
   const int used_halves = explicit_blobs ? (nblob >= 2 ? 2 : 1) : halves;
+  // Explicit blobs with uploads on the main stream: the partial arrays of a
+  // blob alternate between the main stream and a second upload stream (two
+  // SDMA queues), and each blob's kernels wait for both.  One stream of
+  // 8 MiB copies pays ~11 µs per copy (32 copies of 256 MiB: 5.04 ms against
+  // 4.68 for one copy); two streams take 4.72 ms (profiles/round4_session3.md).
+  const bool two_reads = explicit_blobs && pipeline_reads_on_main_stream && pipeline_reads_two_streams;
+  hipStream_t rs2 = nullptr;
+  const int rs2id = 17;  // pipe_stream(0, 0), as logged for the schedule checker
+  if (two_reads) {
+    if (wk.gpu()) {
+      rs2 = wk.pipe_stream(0, 0);
+      CEK_HIP(hipStreamWaitEvent(rs2, ev_full, 0));
+    }
+    log_op(gidx, "wait", rs2id, 0, 0, 0);
+  }
   for (long long q = 0; q < nblob; ++q) {
     {
       const long long k = explicit_blobs ? q : q / halves;
@@ -1299,11 +1314,13 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
           a.slice(off, len, c.local_range, b, n);
         }
       };
+      int pi = 0;
       for (auto& a : c.arrays) {
         if (a.zc || !a.partial) continue;
         uint64_t b, n;
         blob_slice(a, b, n);
-        wk.h2d(rs, a, b, n);
+        const bool on2 = two_reads && (pi++ % 2 == 1);
+        wk.h2d(on2 ? rs2 : rs, a, b, n);
         *h2d += n * a.elem_size;
       }
       log_op(gidx, "h2d", rsid, off, len);
@@ -1315,6 +1332,20 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
       log_op(gidx, "rec", rsid, off, len, slot);
       log_op(gidx, "wait", ksid, off, len, slot);
       ++slot;
+      if (two_reads) {
+        // every blob's kernels wait for the second stream too, also a blob
+        // that uploads nothing there (its kernels may need an earlier blob's
+        // panel, and consecutive blobs' kernels run on different streams)
+        log_op(gidx, "h2d", rs2id, off, len);
+        if (wk.gpu()) {
+          hipEvent_t er2 = wk.event(slot);
+          CEK_HIP(hipEventRecord(er2, rs2));
+          CEK_HIP(hipStreamWaitEvent(ks, er2, 0));
+        }
+        log_op(gidx, "rec", rs2id, off, len, slot);
+        log_op(gidx, "wait", ksid, off, len, slot);
+        ++slot;
+      }
       launch_kernels(wk, ks, c, off, len);
       log_op(gidx, "kernel", ksid, off, len);
       if (wk.gpu() && ws != ks) {

@@ -56,7 +56,10 @@ def check_pipeline_schedule(schedule: Sequence[Op]) -> int:
     for dev, ops in by_dev.items():
         reach = happens_before(ops)
         full = [i for i, o in enumerate(ops) if o[1] == "h2d" and o[3] < 0]
-        h2d = {(o[3], o[4]): i for i, o in enumerate(ops) if o[1] == "h2d" and o[3] >= 0}
+        h2d: Dict[Tuple[int, int], List[int]] = defaultdict(list)  # a chunk may upload on two streams
+        for i, o in enumerate(ops):
+            if o[1] == "h2d" and o[3] >= 0:
+                h2d[(o[3], o[4])].append(i)
         kern = {(o[3], o[4]): i for i, o in enumerate(ops) if o[1] == "kernel"}
         d2h = {(o[3], o[4]): i for i, o in enumerate(ops) if o[1] == "d2h"}
         main_ops = [i for i, o in enumerate(ops) if o[2] == 0]
@@ -65,8 +68,9 @@ def check_pipeline_schedule(schedule: Sequence[Op]) -> int:
             for f in full:
                 if k not in reach[f]:
                     raise AssertionError(f"device {dev}: kernel {chunk} may start before the full reads")
-            if chunk in h2d and k not in reach[h2d[chunk]]:
-                raise AssertionError(f"device {dev}: kernel {chunk} may start before its H2D")
+            for u in h2d.get(chunk, []):
+                if k not in reach[u]:
+                    raise AssertionError(f"device {dev}: kernel {chunk} may start before its H2D")
             if chunk in d2h and d2h[chunk] not in reach[k]:
                 raise AssertionError(f"device {dev}: D2H {chunk} may start before its kernels")
             checked += 1

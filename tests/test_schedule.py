@@ -82,7 +82,15 @@ def test_explicit_uneven_blobs_with_array_slices():
     kernels = [(o[3], o[4], o[2]) for o in sched if o[1] == "kernel"]
     assert [(b, c) for b, c, _ in kernels] == [(0, 64), (64, 192), (256, 320), (576, 448)]
     assert [s for _, _, s in kernels] == [18, 21, 18, 21]  # halves alternate
+    # the two partial arrays go up on two streams (main, and upload stream 17)
+    assert {o[2] for o in sched if o[1] == "h2d" and o[3] >= 0} == {0, 17}
     assert check_pipeline_schedule(sched) == 4
+    # a kernel that does not wait for the second upload stream is caught
+    k1 = [o for o in sched if o[1] == "kernel"][1]
+    ev = [o[5] for o in sched if o[1] == "rec" and o[2] == 17 and o[3] == k1[3]][0]
+    broken = [o for o in sched if not (o[1] == "wait" and o[5] == ev and o[2] == k1[2])]
+    with pytest.raises(AssertionError):
+        check_pipeline_schedule(broken)
     assert cr.last_record()["pipelined"]
     cr.dispose()
 
