@@ -468,6 +468,36 @@ __device__ __forceinline__ void gemm_f32_direct(const int* __restrict__ dims, co
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
   };
+  // VAR 2: the next block's FM+FN loads spread evenly over the current
+  // block's 4·FM groups of FN MFMAs (one load every few groups), each group
+  // pinned by a scheduling barrier, instead of one burst of loads
+  auto mma_ld = [&](const f32x4(&a)[FM], const f32x4(&b)[FN], f32x4(&na)[FM], f32x4(&nb)[FN], int kb_next) {
+    // VAR 2: over all 4·FM groups; VAR 3: over the first half, so the last
+    // load has half a block of MFMAs more to land
+    constexpr int NL = FM + FN, NG = VAR == 3 ? 2 * FM : 4 * FM;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int g = q * FM + i;
+#pragma unroll
+        for (int l = 0; l < NL; ++l)
+          if (l * NG / NL == g) {
+            // B fragments first: the next block's first MFMA group needs
+            // every b and only a[0], and waits count loads in issue order
+            if (l < FN)
+              nb[l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, vb, l * frag_stride + kb_next * 64, 0));
+            else
+              na[l - FN] = __builtin_bit_cast(
+                  f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, va, (l - FN) * frag_stride + kb_next * 64, 0));
+            asm volatile("" ::: "memory");
+          }
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+  };
   const int nkb = K / 16;  // even: K % 32 == 0
   f32x4 a0[FM], b0[FN], a1[FM], b1[FN];
   load(a0, b0, 0);
@@ -485,7 +515,7 @@ __device__ __forceinline__ void gemm_f32_direct(const int* __restrict__ dims, co
       __builtin_amdgcn_sched_barrier(0);
       mma(a1, b1);
       __builtin_amdgcn_sched_barrier(0);
-    } else {
+    } else if constexpr (VAR == 1) {
       load(a1, b1, kb + 1);
       cek_tie(a0);
       cek_tie(b0);
@@ -494,6 +524,10 @@ __device__ __forceinline__ void gemm_f32_direct(const int* __restrict__ dims, co
       cek_tie(a1);
       cek_tie(b1);
       mma(a1, b1);
+    } else {
+      static_assert(VAR == 2 || VAR == 3, "VAR is 0, 1, 2 or 3");
+      mma_ld(a0, b0, a1, b1, kb + 1);
+      mma_ld(a1, b1, a0, b0, kb + 2 < nkb ? kb + 2 : 0);
     }
   }
   __builtin_amdgcn_s_setprio(0);
@@ -522,6 +556,8 @@ CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g, 2, 2, 8, 8, 0)
 CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256gt, 2, 2, 8, 8, 1)
 CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g8, 2, 4, 8, 4, 0)
 CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g8t, 2, 4, 8, 4, 1)
+CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g8i, 2, 4, 8, 4, 2)  // loads spread between MFMA groups
+CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g8h, 2, 4, 8, 4, 3)  // spread over the first half
 
 #define CEK_GEMM_F32_KERNEL(NAME, WM, WN, FM, FN, PIPE)                                           \
   extern "C" __global__ __launch_bounds__(64 * WM * WN) void NAME(                                 \

@@ -113,6 +113,9 @@ F32_TILES = {
     "256x256g": (256, 256, 256, "cek_sgemm_f32_256x256g"),
     "256x256gt": (256, 256, 256, "cek_sgemm_f32_256x256gt"),
     "256x256g8t": (256, 256, 512, "cek_sgemm_f32_256x256g8t"),
+    # the next block's loads spread between MFMA groups (over all / the first half)
+    "256x256g8i": (256, 256, 512, "cek_sgemm_f32_256x256g8i"),
+    "256x256g8h": (256, 256, 512, "cek_sgemm_f32_256x256g8h"),
     "128x128": (128, 128, 256, "cek_sgemm_f32_128x128"),
 }
 
