@@ -1276,11 +1276,13 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
   const bool explicit_blobs = !c.blob_bounds.empty();
   const long long nblob = explicit_blobs ? static_cast<long long>(c.blob_bounds.size()) - 1 : per_half * halves;
   const int used_halves = explicit_blobs ? (nblob >= 2 ? 2 : 1) : halves;
-  // Explicit blobs with uploads on the main stream: the partial arrays of a
-  // blob alternate between the main stream and a second upload stream (two
-  // SDMA queues), and each blob's kernels wait for both.  One stream of
-  // 8 MiB copies pays ~11 µs per copy (32 copies of 256 MiB: 5.04 ms against
-  // 4.68 for one copy); two streams take 4.72 ms (profiles/round4_session3.md).
+  // Optional (pipeline_reads_two_streams, off): the partial arrays of an
+  // explicit blob alternate between the main stream and a second upload
+  // stream, and each blob's kernels wait for both.  Alone, one stream of
+  // 8 MiB copies pays ~11 µs per copy that two streams hide (5.04 vs
+  // 4.72 ms for 256 MiB); inside the shell pipeline the extra stream shares
+  // a hardware queue with kernel and download streams and the call slows
+  // from 7.1 to 12.7 ms (profiles/round4_session4.md), so it stays off.
   const bool two_reads = explicit_blobs && pipeline_reads_on_main_stream && pipeline_reads_two_streams;
   hipStream_t rs2 = nullptr;
   const int rs2id = 17;  // pipe_stream(0, 0), as logged for the schedule checker

@@ -65,6 +65,7 @@ def test_explicit_uneven_blobs_with_array_slices():
     cpu = ck.ClPlatforms.all().cpus(True)
     cr = ck.ClNumberCruncher(cpu, src)
     cr.cores.record_schedule = True
+    cr.cores.pipeline_reads_two_streams = True  # the optional second upload stream, checked below
     bounds = [0, 64, 256, 576, 1024]  # 1, 3, 5, 7 work-groups of 64: a shell-like progression
     n = bounds[-1]
     x = ck.ClArray(np.arange(n, dtype=np.float32))
