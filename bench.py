@@ -137,7 +137,10 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
             "256x256pbw" if (size // 64) % 2 == 0 else "256x128pe")
     from cekirdekler_amd.ops.gemm import GEMM_LIBS
 
-    cr = DistributedCruncher("", ctx=ctx, prebuilt=library(*GEMM_LIBS))
+    # 4 async enqueue queues per device, one per hardware queue
+    # (GPU_MAX_HW_QUEUES=4): 1399 TF/s at 1024 rows against 1376 with 2 and
+    # 1329 with 16 on one box (profiles/round4_session4.md)
+    cr = DistributedCruncher("", ctx=ctx, prebuilt=library(*GEMM_LIBS), queue_concurrency=4)
     g = GemmBf16(size, size, size, cruncher=cr, tile=tile)
     step = lambda: g.run(compute_id=1, resident=True)  # noqa: E731
     # Setup (untimed): run the iterative load balancer to convergence — the
