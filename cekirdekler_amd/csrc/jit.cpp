@@ -478,7 +478,12 @@ std::string cpu_rewrite(const std::string& src) {
     std::string c = "__cek_call(&" + n + ", args)";
     if (!barriers) {
       // whole work-groups per outer iteration (the pool hands out multiples
-      // of L), so the inner loop only advances threadIdx.x
+      // of L), so the inner loop only advances threadIdx.x.  "omp simd"
+      // (-fopenmp-simd: the pragma only, no OpenMP runtime) states what the
+      // kernel model already guarantees — work-items without barriers are
+      // independent — so the compiler vectorizes across work-items also
+      // when the kernel body has loops of its own (it refuses "multiple
+      // nested loops" otherwise and runs such kernels one item at a time)
       os << "extern \"C\" void __cek_run_" << n
          << "(void** args, long long off, long long gsize, long long first, long long count, int L) {\n"
          << "  __cek_off = off; __cek_gsize = gsize; blockDim.x = (unsigned)L;\n"
@@ -486,6 +491,7 @@ std::string cpu_rewrite(const std::string& src) {
          << "  for (long long g0 = first; g0 < first + count; g0 += L) {\n"
          << "    blockIdx.x = (unsigned)((g0 - off) / L);\n"
          << "    const int n_items = (int)std::min<long long>(L, first + count - g0);\n"
+         << "    _Pragma(\"omp simd\")\n"
          << "    for (int t = 0; t < n_items; ++t) { threadIdx.x = (unsigned)t; " << c << "; }\n"
          << "  }\n}\n";
     } else {
@@ -601,7 +607,7 @@ bool compile_cpu(const std::string& rsrc, const std::vector<std::string>& option
   // instead of one per work item.
   std::string flags =
       "-O3 -march=native -ffp-contract=off -fPIC -shared -std=c++17 -w -fno-semantic-interposition "
-      "-ftls-model=local-dynamic";
+      "-ftls-model=local-dynamic -fopenmp-simd";
   for (auto& o : options) flags += " " + o;
   std::string key = hash_hex(rsrc + "\x01" + cxx + "\x01" + flags);
   std::string dir = cache_dir();

@@ -554,6 +554,7 @@ __device__ __forceinline__ void gemm_f32_direct(const int* __restrict__ dims, co
 // registers per lane) and 8 waves of 128×64 (two per SIMD)
 CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g, 2, 2, 8, 8, 0)
 CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256gt, 2, 2, 8, 8, 1)
+CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256gh, 2, 2, 8, 8, 3)
 CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g8, 2, 4, 8, 4, 0)
 CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g8t, 2, 4, 8, 4, 1)
 CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g8i, 2, 4, 8, 4, 2)  // loads spread between MFMA groups

@@ -93,8 +93,13 @@ def rows_to_tile(b: np.ndarray, geom) -> np.ndarray:
 # fp32 tiles (kernels/sgemm_f32.hip): v_mfma_f32_16x16x4_f32, BK = 32
 F32_TILES = {
     # production: register-direct, 8 waves of 128×64 — fragments loaded
-    # global → VGPR, no LDS, no barrier (151.4 TF at 8192³ vs hipBLASLt 153.4
-    # and 256x256ir 138.6 on one box, profiles/gemm_f32_findings.md)
+    # global → VGPR, no LDS, no barrier — with the next block's loads spread
+    # over the first half of the current block's MFMA groups (152.9 TF at
+    # 8192³ vs hipBLASLt 152.8 and the burst-load g8 149.5 in one process,
+    # profiles/round4_session5.md)
+    "256x256g8h": (256, 256, 512, "cek_sgemm_f32_256x256g8h"),
+    # burst loads ahead of each block's MFMAs (151.4 TF vs hipBLASLt 153.4 on
+    # another box, 256x256ir 138.6 there)
     "256x256g8": (256, 256, 512, "cek_sgemm_f32_256x256g8"),
     # LDS-staged: k block 1's fragment reads between block 0's MFMA groups
     # (146-147 TF at 8192³ on earlier boxes)
@@ -112,10 +117,10 @@ F32_TILES = {
     # fragment ties instead of scheduling barriers
     "256x256g": (256, 256, 256, "cek_sgemm_f32_256x256g"),
     "256x256gt": (256, 256, 256, "cek_sgemm_f32_256x256gt"),
+    "256x256gh": (256, 256, 256, "cek_sgemm_f32_256x256gh"),  # 4-wave form of g8h
     "256x256g8t": (256, 256, 512, "cek_sgemm_f32_256x256g8t"),
-    # the next block's loads spread between MFMA groups (over all / the first half)
+    # the next block's loads spread over all MFMA groups
     "256x256g8i": (256, 256, 512, "cek_sgemm_f32_256x256g8i"),
-    "256x256g8h": (256, 256, 512, "cek_sgemm_f32_256x256g8h"),
     "128x128": (128, 128, 256, "cek_sgemm_f32_128x128"),
 }
 
@@ -551,7 +556,7 @@ class GemmF32(GemmBf16):
     (same grouped tile order, so the same range partitioning and
     wave-quantized balancing apply)."""
 
-    def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256g8",
+    def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256g8h",
                  cruncher: ClNumberCruncher | None = None, fill: str = "random", seed: int = 0,
                  group_m: int = 4, wave_granularity: bool | None = None):
         BM, BN, L, kname = F32_TILES[tile]

@@ -23,7 +23,7 @@ LIBRARY = {
                    "cek_sgemm_bf16_256x256pb_sw", "cek_sgemm_bf16_256x256pb_sh", "cek_sgemm_bf16_256x256pb_ss"],
     "sgemm_f32": ["cek_sgemm_f32_128x128", "cek_sgemm_f32_256x128", "cek_sgemm_f32_256x256",
                   "cek_sgemm_f32_256x256ir", "cek_sgemm_f32_256x256ib7", "cek_sgemm_f32_256x128ie",
-                  "cek_sgemm_f32_256x256w", "cek_sgemm_f32_256x256g", "cek_sgemm_f32_256x256gt",
+                  "cek_sgemm_f32_256x256w", "cek_sgemm_f32_256x256g", "cek_sgemm_f32_256x256gt", "cek_sgemm_f32_256x256gh",
                   "cek_sgemm_f32_256x256g8", "cek_sgemm_f32_256x256g8t",
                   "cek_sgemm_f32_256x256g8i", "cek_sgemm_f32_256x256g8h"],
     "mandelbrot": ["cek_mandelbrot_f32", "cek_mandelbrot_blk8_f32", "cek_mandelbrot_blk8h_f32",

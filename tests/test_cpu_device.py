@@ -54,6 +54,32 @@ def test_saxpy_1m_bit_exact(cr):
     np.testing.assert_array_equal(y.array, np.float32(1.7) * x.array + y0)
 
 
+def test_kernel_with_inner_loop_vectorized_runner_exact(cpu):
+    """The CPU runner vectorizes across work-items ("omp simd") also when the
+    kernel body has a loop of its own; every item must still follow its own
+    scalar fp32 chain (fmaf per step, no contraction or reassociation)."""
+    src = """__global__ void poly(const float* x, float* y) {
+      long long i = get_global_id(0);
+      float v = x[i], acc = y[i];
+      for (int k = 0; k < 24; ++k) acc = fmaf(acc, v, 0.25f);
+      if (i % 7 == 3) acc = -acc;
+      y[i] = acc;
+    }"""
+    c = ck.ClNumberCruncher(cpu + cpu, src)
+    n = 256 * 40
+    rng = np.random.default_rng(5)
+    x = ck.ClArray(rng.uniform(-0.9, 0.9, n).astype(np.float32))
+    y0 = rng.uniform(-1, 1, n).astype(np.float32)
+    y = ck.ClArray(y0.copy())
+    x.partial_read = y.partial_read = True
+    x.next_param(y).compute(c, 1, "poly", n, 256)
+    acc = y0.copy()
+    for _ in range(24):  # fmaf: one rounding of the exact a·b + c
+        acc = (acc.astype(np.float64) * x.array + 0.25).astype(np.float32)
+    acc[np.arange(n) % 7 == 3] *= -1
+    np.testing.assert_array_equal(y.array, acc)
+
+
 def test_elements_per_work_item_and_partial(cpu):
     devs = cpu + cpu + cpu
     cr = ck.ClNumberCruncher(devs, SRC)
