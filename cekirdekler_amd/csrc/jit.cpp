@@ -233,7 +233,14 @@ static const char* kCpuPrelude = R"CEK(
 struct dim3 { unsigned x = 1, y = 1, z = 1; };
 static thread_local dim3 threadIdx, blockIdx, blockDim, gridDim;
 static thread_local long long __cek_off = 0, __cek_gsize = 0;
+// kernels are inlined into their runner's work-item loop (which the
+// compiler then vectorizes across work-items); CEK_NO_FORCE_INLINE is the
+// retry for a kernel that cannot be inlined
+#ifndef CEK_NO_FORCE_INLINE
+#define __global__ __attribute__((always_inline))
+#else
 #define __global__
+#endif
 #define __device__
 #define __host__
 #define __forceinline__ inline
@@ -600,6 +607,9 @@ bool compile_cpu(const std::string& rsrc, const std::vector<std::string>& option
   const char* cxx_env = getenv("CEK_CXX");
   std::string cxx = cxx_env && *cxx_env ? cxx_env : "g++";
   // -ffp-contract=off: results match the host reference (numpy) bit-for-bit.
+  // -fno-math-errno: sqrtf & co. need no errno branch (kernels have no
+  // errno), which would otherwise keep any loop calling them scalar; the
+  // results stay the correctly rounded IEEE ones.
   // -fno-semantic-interposition: the runner's call of an extern "C" kernel
   // in the same .so is a direct, inlinable call (not through the PLT), so
   // the work-item loop vectorizes; -ftls-model=local-dynamic: the work-item
@@ -607,7 +617,7 @@ bool compile_cpu(const std::string& rsrc, const std::vector<std::string>& option
   // instead of one per work item.
   std::string flags =
       "-O3 -march=native -ffp-contract=off -fPIC -shared -std=c++17 -w -fno-semantic-interposition "
-      "-ftls-model=local-dynamic -fopenmp-simd";
+      "-ftls-model=local-dynamic -fopenmp-simd -fno-math-errno";
   for (auto& o : options) flags += " " + o;
   std::string key = hash_hex(rsrc + "\x01" + cxx + "\x01" + flags);
   std::string dir = cache_dir();
@@ -621,6 +631,11 @@ bool compile_cpu(const std::string& rsrc, const std::vector<std::string>& option
   write_file_atomic(src_path, rsrc);
   std::string cmd = cxx + " " + flags + " -o " + tmp_so + " " + src_path + " > " + log_path + " 2>&1";
   int rc = std::system(cmd.c_str());
+  if (rc != 0) {  // a kernel the compiler cannot inline: build it as a call
+    const std::string retry = cxx + " " + flags + " -DCEK_NO_FORCE_INLINE -o " + tmp_so + " " + src_path + " > " +
+                              log_path + " 2>&1";
+    rc = std::system(retry.c_str());
+  }
   read_file(log_path, log);
   unlink(log_path.c_str());
   unlink(src_path.c_str());

@@ -80,6 +80,22 @@ def test_kernel_with_inner_loop_vectorized_runner_exact(cpu):
     np.testing.assert_array_equal(y.array, acc)
 
 
+def test_kernel_that_cannot_be_inlined_still_builds(cpu):
+    """Kernels are force-inlined into their runner; one the compiler cannot
+    inline (here: recursive) is rebuilt as a plain call."""
+    src = """__global__ void rec(float* x) {
+      long long i = get_global_id(0);
+      if (x[i] >= 5.0f) return;
+      x[i] += 1.0f;
+      rec(x);
+    }"""
+    c = ck.ClNumberCruncher(cpu, src)
+    assert c.error_code() == 0, c.error_message()
+    x = ck.ClArray(np.arange(256, dtype=np.float32) % 4)
+    x.compute(c, 1, "rec", 256, 64)
+    np.testing.assert_array_equal(x.array, np.full(256, 5.0, np.float32))
+
+
 def test_elements_per_work_item_and_partial(cpu):
     devs = cpu + cpu + cpu
     cr = ck.ClNumberCruncher(devs, SRC)
