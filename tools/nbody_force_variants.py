@@ -72,17 +72,21 @@ def variant(name, B, prefetch, tile, unroll):
     return "\n".join(s) + "\n"
 
 
-def variant_js(name, B, S):
+def variant_js(name, B, S, mass_lds=False):
     """j-split: a work-group's 256 threads form S groups that take the same
     256·B/S bodies (B per thread, packed pairs) against S different 256-body
     tiles of each LDS load, and add their partial accelerations through LDS
     at the end: S times the waves for the same body share (more latency
     hiding when one GPU holds a quarter of the bodies).  A work item owns
-    B/S bodies of each output."""
+    B/S bodies of each output.  ``mass_lds``: the masses also go to an LDS
+    array of their own, so the body loop reads x, y, z (one 12-B read) and
+    the masses of 4 bodies per 16-B read, and no VALU copy saves q.w from
+    the register pair the z difference is written into."""
     NP, T = B // 2, 256 // S
     s = [f"__global__ __launch_bounds__(256) void {name}(const float4* pos, const float4* vel, const float* prm,",
          "    float4* pos_o, float4* vel_o, float4* acc_o) {",
          f"  __shared__ float4 t[{256 * S}];",
+         f"  __shared__ float mt[{256 * S}];" if mass_lds else "",
          "  const int n = (int)prm[2];",
          "  const f2 e2 = {prm[0], prm[0]};",
          "  const int l = threadIdx.x;",
@@ -99,13 +103,16 @@ def variant_js(name, B, S):
          f"  for (int j0 = 0; j0 < n; j0 += {256 * S}) {{",
          "    __syncthreads();",
          f"    for (int k = 0; k < {S}; ++k) t[k * 256 + l] = nx[k];",
+         f"    for (int k = 0; k < {S}; ++k) mt[k * 256 + l] = nx[k].w;" if mass_lds else "",
          "    __syncthreads();",
          f"    if (j0 + {256 * S} < n) for (int k = 0; k < {S}; ++k) nx[k] = pos[j0 + {256 * S} + k * 256 + l];",
          "    const float4* tg = t + grp * 256;",
+         "    const float* mg = mt + grp * 256;" if mass_lds else "",
          "#pragma unroll 8",
          "    for (int j = 0; j < 256; ++j) {",
          "      const float4 q = tg[j];",
-         "      const f2 qx = {q.x, q.x}, qy = {q.y, q.y}, qz = {q.z, q.z}, qm = {q.w, q.w};",
+         "      const float qw = mg[j];" if mass_lds else "      const float qw = q.w;",
+         "      const f2 qx = {q.x, q.x}, qy = {q.y, q.y}, qz = {q.z, q.z}, qm = {qw, qw};",
          "#pragma unroll",
          f"      for (int p = 0; p < {NP}; ++p) {{",
          "        const f2 dx = qx - px[p], dy = qy - py[p], dz = qz - pz[p];",
@@ -139,7 +146,8 @@ def variant_js(name, B, S):
     return "\n".join(s) + "\n"
 
 
-JS_VARIANTS = {"b2_js2": (2, 2), "b4_js2": (4, 2), "b2_js4": (2, 4)}  # name: (B, S)
+JS_VARIANTS = {"b2_js2": (2, 2), "b4_js2": (4, 2), "b2_js4": (2, 4),  # name: (B, S[, mass_lds])
+               "b2_js2m": (2, 2, True), "b4_js2m": (4, 2, True), "b2_js4m": (2, 4, True)}
 
 VARIANTS = {  # name: (B, prefetch, tile, unroll)
     "b2_plain": (2, False, 256, 8),
@@ -158,6 +166,9 @@ def main():
     # work items per body: B bodies per item, S items per body group for j-split
     per_item = {k: (v[0], 1) for k, v in VARIANTS.items()}
     per_item.update({k: (v[0], v[1]) for k, v in JS_VARIANTS.items()})
+    if len(sys.argv) > 4:  # only the named variants
+        keep = set(sys.argv[4].split(","))
+        per_item = {k: v for k, v in per_item.items() if k in keep}
     g0 = ck.ClPlatforms.all().gpus()[0]
     cr = ck.ClNumberCruncher(g0, src)
     if cr.error_code():
