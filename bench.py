@@ -521,9 +521,11 @@ def bench_node_configs(world: int) -> dict:
     """BASELINE configs 4 and 5 on this job's GPUs (0 .. world-1), run by
     rank 0 after every other rank has left: the N-body 3-stage
     device→device pipeline (stage transitions over xGMI) and the 256-task
-    pool over a device pool; plus config 1, SAXPY 1M on the CPU device.  Both are single-process multi-GPU programs (the
-    reference's model), so each runs as a child process with its own time
-    limit; a failure is reported in its field and cannot stop the headline."""
+    pool over a device pool; plus config 1, SAXPY 1M on the CPU device, the
+    wave example and CPU + GPU co-execution on host-resident data.  They are
+    single-process programs (the reference's model), so each runs as a child
+    process with its own time limit; a failure is reported in its field and
+    cannot stop the headline."""
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                         "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
@@ -539,7 +541,8 @@ def bench_node_configs(world: int) -> dict:
     configs = [("nbody_pipeline", [sys.executable, "nbody_pipeline.py", *nb_args, "--pushes", "14"]),
                ("task_pool", [sys.executable, "task_pool.py", "--gpus", str(world)]),
                ("saxpy_1m_cpu", [sys.executable, "saxpy_cpu.py"]),
-               ("wave_cpu_gpu", [sys.executable, "wave_cpu_gpu.py"])]
+               ("wave_cpu_gpu", [sys.executable, "wave_cpu_gpu.py"]),
+               ("hetero_stream", [sys.executable, "hetero_stream.py"])]
     if world <= torch.cuda.device_count():
         configs.append(("sgemm_host_resident_rccl", rccl))
     else:
