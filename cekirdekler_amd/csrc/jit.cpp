@@ -619,7 +619,9 @@ bool compile_cpu(const std::string& rsrc, const std::vector<std::string>& option
       "-O3 -march=native -ffp-contract=off -fPIC -shared -std=c++17 -w -fno-semantic-interposition "
       "-ftls-model=local-dynamic -fopenmp-simd -fno-math-errno";
   for (auto& o : options) flags += " " + o;
-  std::string key = hash_hex(rsrc + "\x01" + cxx + "\x01" + flags);
+  // "vplan": the build may fall back to clang (below); part of the key so a
+  // cache entry from before that fallback existed is not reused
+  std::string key = hash_hex(rsrc + "\x01" + cxx + "\x01" + flags + "\x01vplan");
   std::string dir = cache_dir();
   so_path = dir + "/cpu_" + key + ".so";
   struct stat st;
@@ -629,13 +631,37 @@ bool compile_cpu(const std::string& rsrc, const std::vector<std::string>& option
   std::string tmp_so = so_path + ".tmp." + std::to_string(getpid());
   std::string log_path = src_path + ".log";
   write_file_atomic(src_path, rsrc);
-  std::string cmd = cxx + " " + flags + " -o " + tmp_so + " " + src_path + " > " + log_path + " 2>&1";
+  // With the default g++ the vectorizer's report says whether any loop was
+  // vectorized.  g++ vectorizes the work-item loop around a kernel with a
+  // loop of its own only when the body has no other control flow ("if (i >=
+  // n) return;" keeps it scalar); when it vectorized nothing, the kernel is
+  // rebuilt with clang's outer-loop vectorizer (VPlan native path), which
+  // handles those bodies (a 24-step FMA loop plus a branch: 79 -> 17 ms per
+  // 4 M items, bit-identical results).  g++ stays first: on kernels it does
+  // vectorize it is faster (all-pairs n-body 1.97 vs 2.93 ms).
+  const bool auto_cxx = !(cxx_env && *cxx_env);
+  const std::string vec_path = src_path + ".vec";
+  std::string cmd = cxx + " " + flags + (auto_cxx ? " -fopt-info-vec-optimized=" + vec_path : std::string()) +
+                    " -o " + tmp_so + " " + src_path + " > " + log_path + " 2>&1";
   int rc = std::system(cmd.c_str());
   if (rc != 0) {  // a kernel the compiler cannot inline: build it as a call
     const std::string retry = cxx + " " + flags + " -DCEK_NO_FORCE_INLINE -o " + tmp_so + " " + src_path + " > " +
                               log_path + " 2>&1";
     rc = std::system(retry.c_str());
+  } else if (auto_cxx && rsrc.find("__cek_fib = &fib") == std::string::npos) {
+    std::string report;
+    read_file(vec_path, report);
+    const char* rocm = getenv("ROCM_PATH");
+    const std::string clang = std::string(rocm && *rocm ? rocm : "/opt/rocm") + "/llvm/bin/clang++";
+    if (report.find("vectorized") == std::string::npos && stat(clang.c_str(), &st) == 0) {
+      const std::string tmp2 = tmp_so + ".vplan";
+      const std::string alt = clang + " " + flags + " -mllvm -enable-vplan-native-path -o " + tmp2 + " " + src_path +
+                              " > /dev/null 2>&1";
+      if (std::system(alt.c_str()) == 0) rename(tmp2.c_str(), tmp_so.c_str());
+      else unlink(tmp2.c_str());
+    }
   }
+  unlink(vec_path.c_str());
   read_file(log_path, log);
   unlink(log_path.c_str());
   unlink(src_path.c_str());
