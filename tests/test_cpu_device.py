@@ -80,6 +80,33 @@ def test_kernel_with_inner_loop_vectorized_runner_exact(cpu):
     np.testing.assert_array_equal(y.array, acc)
 
 
+def test_guarded_loop_kernel_exact_and_bounded(cpu):
+    """A guard ("if (i >= n) return;") ahead of a loop: the vectorized
+    runner must leave the items past the guard untouched and match the
+    scalar fp32 chain on the others."""
+    src = """__global__ void gpoly(const float* x, float* y, const int* n) {
+      long long i = get_global_id(0);
+      if (i >= n[0]) return;
+      float v = x[i], acc = y[i];
+      for (int k = 0; k < 16; ++k) acc = fmaf(acc, v, 0.25f);
+      y[i] = acc;
+    }"""
+    c = ck.ClNumberCruncher(cpu + cpu, src)
+    g, lim = 256 * 24, 256 * 24 - 77
+    rng = np.random.default_rng(9)
+    x = ck.ClArray(rng.uniform(-0.9, 0.9, g).astype(np.float32))
+    y0 = rng.uniform(-1, 1, g).astype(np.float32)
+    y = ck.ClArray(y0.copy())
+    nn = ck.ClArray(np.array([lim], np.int32))
+    nn.write = False
+    x.next_param(y, nn).compute(c, 1, "gpoly", g, 256)
+    acc = y0[:lim].copy()
+    for _ in range(16):
+        acc = (acc.astype(np.float64) * x.array[:lim] + 0.25).astype(np.float32)
+    np.testing.assert_array_equal(y.array[:lim], acc)
+    np.testing.assert_array_equal(y.array[lim:], y0[lim:])
+
+
 def test_kernel_that_cannot_be_inlined_still_builds(cpu):
     """Kernels are force-inlined into their runner; one the compiler cannot
     inline (here: recursive) is rebuilt as a plain call."""
