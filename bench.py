@@ -541,8 +541,7 @@ def bench_node_configs(world: int) -> dict:
     configs = [("nbody_pipeline", [sys.executable, "nbody_pipeline.py", *nb_args, "--pushes", "14"]),
                ("task_pool", [sys.executable, "task_pool.py", "--gpus", str(world)]),
                ("saxpy_1m_cpu", [sys.executable, "saxpy_cpu.py"]),
-               ("wave_cpu_gpu", [sys.executable, "wave_cpu_gpu.py"]),
-               ("hetero_stream", [sys.executable, "hetero_stream.py"])]
+               ("wave_cpu_gpu", [sys.executable, "wave_cpu_gpu.py"])]
     if world <= torch.cuda.device_count():
         configs.append(("sgemm_host_resident_rccl", rccl))
     else:
@@ -550,6 +549,7 @@ def bench_node_configs(world: int) -> dict:
         # ranks on one device
         out["sgemm_host_resident_rccl"] = {"skipped": f"{world} ranks on {torch.cuda.device_count()} GPU(s); "
                                                       "RCCL needs one GPU per rank"}
+    configs.append(("hetero_stream", [sys.executable, "hetero_stream.py"]))
     t_start = time.monotonic()
     for name, cmd in configs:
         # the extras share one time budget, so a hung config cannot push the
