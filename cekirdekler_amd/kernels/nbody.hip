@@ -37,13 +37,7 @@ __device__ __forceinline__ void nbody_force(const float4* __restrict__ pos, floa
                                             const float* __restrict__ params, long long off) {
   static_assert(B % 2 == 0, "bodies are processed in packed pairs");
   constexpr int NP = B / 2;  // packed pairs per work item
-  // B = 2: masses in an LDS array of their own — the j loop reads x, y, z as
-  // one 12-B read and four masses per 16-B read, and no VALU copy saves q.w
-  // from the register pair the z difference is written into (59 instead of
-  // 62 VALU per 4 bodies); B = 4 keeps q.w (its allocation gains nothing)
-  constexpr bool kMassLds = B == 2;
   __shared__ float4 tile[256];
-  __shared__ float mtile[kMassLds ? 256 : 1];
   if (blockDim.x != 256) return;  // body mapping assumes 256-item groups
   const float eps2 = params[0], gconst = params[1];
   const int n = (int)params[2];
@@ -64,14 +58,12 @@ __device__ __forceinline__ void nbody_force(const float4* __restrict__ pos, floa
   for (int j0 = 0; j0 < n; j0 += 256) {
     __syncthreads();
     tile[l] = next;
-    if (kMassLds) mtile[l] = next.w;
     __syncthreads();
     if (j0 + 256 < n) next = pos[j0 + 256 + l];
 #pragma unroll 4
     for (int j = 0; j < 256; ++j) {
       const float4 q = tile[j];
-      const float qw = kMassLds ? mtile[j] : q.w;
-      const f32x2 qx = {q.x, q.x}, qy = {q.y, q.y}, qz = {q.z, q.z}, qm = {qw, qw};
+      const f32x2 qx = {q.x, q.x}, qy = {q.y, q.y}, qz = {q.z, q.z}, qm = {q.w, q.w};
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
         const f32x2 dx = qx - px[p], dy = qy - py[p], dz = qz - pz[p];
