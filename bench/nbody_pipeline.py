@@ -57,15 +57,10 @@ FORCE = r"""
 // bodies per GPU (the force stage on four GPUs) that is 51.0 % of the FP32
 // peak against 48.9 % (tools/nbody_force_variants.py, profiles/round4_session2.md).
 // The next LDS load is held in registers while the current one is consumed.
-// The masses also go to an LDS array of their own: the body loop reads x, y, z
-// as one 12-B read and four masses per 16-B read, and no VALU copy has to
-// save q.w from the register pair the z difference is written into (116
-// instead of 121 VALU instructions per 8 bodies of the j loop).
 typedef float f2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void force(const float4* pos, const float4* vel, const float* prm,
                                              float4* pos_o, float4* vel_o, float4* acc_o) {
   __shared__ float4 tile[512];
-  __shared__ float mass[512];
   const int n = (int)prm[2];
   const f2 e2 = {prm[0], prm[0]};
   const int l = threadIdx.x, grp = l >> 7, m = l & 127;
@@ -78,20 +73,16 @@ __global__ __launch_bounds__(256) void force(const float4* pos, const float4* ve
     __syncthreads();
     tile[l] = nx0;
     tile[256 + l] = nx1;
-    mass[l] = nx0.w;
-    mass[256 + l] = nx1.w;
     __syncthreads();
     if (j0 + 512 < n) {
       nx0 = pos[j0 + 512 + l];
       nx1 = pos[j0 + 768 + l];
     }
     const float4* tg = tile + grp * 256;
-    const float* mg = mass + grp * 256;
 #pragma unroll 8
     for (int j = 0; j < 256; ++j) {
       const float4 q = tg[j];
-      const float qw = mg[j];
-      const f2 qx = {q.x, q.x}, qy = {q.y, q.y}, qz = {q.z, q.z}, qm = {qw, qw};
+      const f2 qx = {q.x, q.x}, qy = {q.y, q.y}, qz = {q.z, q.z}, qm = {q.w, q.w};
       const f2 dx = qx - px, dy = qy - py, dz = qz - pz;
       const f2 r2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, __builtin_elementwise_fma(dz, dz, e2)));
       const f2 inv = {__builtin_amdgcn_rsqf(r2.x), __builtin_amdgcn_rsqf(r2.y)};
