@@ -72,7 +72,7 @@ def variant(name, B, prefetch, tile, unroll):
     return "\n".join(s) + "\n"
 
 
-def variant_js(name, B, S, mass_lds=False):
+def variant_js(name, B, S, mass_lds=False, unroll=8):
     """j-split: a work-group's 256 threads form S groups that take the same
     256·B/S bodies (B per thread, packed pairs) against S different 256-body
     tiles of each LDS load, and add their partial accelerations through LDS
@@ -108,7 +108,7 @@ def variant_js(name, B, S, mass_lds=False):
          f"    if (j0 + {256 * S} < n) for (int k = 0; k < {S}; ++k) nx[k] = pos[j0 + {256 * S} + k * 256 + l];",
          "    const float4* tg = t + grp * 256;",
          "    const float* mg = mt + grp * 256;" if mass_lds else "",
-         "#pragma unroll 8",
+         f"#pragma unroll {unroll}",
          "    for (int j = 0; j < 256; ++j) {",
          "      const float4 q = tg[j];",
          "      const float qw = mg[j];" if mass_lds else "      const float qw = q.w;",
@@ -147,7 +147,8 @@ def variant_js(name, B, S, mass_lds=False):
 
 
 JS_VARIANTS = {"b2_js2": (2, 2), "b4_js2": (4, 2), "b2_js4": (2, 4),  # name: (B, S[, mass_lds])
-               "b2_js2m": (2, 2, True), "b4_js2m": (4, 2, True), "b2_js4m": (2, 4, True)}
+               "b2_js2m": (2, 2, True), "b4_js2m": (4, 2, True), "b2_js4m": (2, 4, True),
+               "b2_js2u4": (2, 2, False, 4), "b2_js2u16": (2, 2, False, 16), "b2_js2u32": (2, 2, False, 32)}
 
 VARIANTS = {  # name: (B, prefetch, tile, unroll)
     "b2_plain": (2, False, 256, 8),
