@@ -720,6 +720,7 @@ def main(argv=None) -> int:
                 "saxpy_1m_cpu": node.get("saxpy_1m_cpu"),
                 "wave_cpu_gpu": node.get("wave_cpu_gpu"),
                 "sgemm_host_resident_rccl": node.get("sgemm_host_resident_rccl"),
+                "hetero_stream": node.get("hetero_stream"),
                 "peer_topology": peers,
             },
         }
