@@ -12,6 +12,8 @@ Cases (256 MiB up, optionally 256 MiB down at the same time):
   chunks_16x16    16 MiB chunks
   two_streams_32  the 32 chunks alternating between two streams (two SDMA queues)
   duplex_32       chunks_32 up while 32 x 8 MiB go down on another stream
+  down_*          downloads: one copy, chunks on one stream, chunks alternating
+                  over two streams (256 MiB, and the Mandelbrot image's 64 MiB)
 """
 import json
 import sys
@@ -72,6 +74,22 @@ def main():
            "duplex_32_ms": timed(duplex),
            "down_alone_32_ms": timed(lambda: [host_dn[i * 8 * MB:(i + 1) * 8 * MB].copy_(
                dev_dn[i * 8 * MB:(i + 1) * 8 * MB], non_blocking=True) for i in range(32)])}
+    # downloads: the whole 256 MiB, and the Mandelbrot image's 64 MiB in one
+    # copy, 8 chunks on one stream, 8 chunks alternating over two streams
+    dn2 = torch.cuda.Stream()
+
+    def down(total, size, streams):
+        k = total // size
+        for i in range(k):
+            with torch.cuda.stream(streams[i % len(streams)]):
+                host_dn[i * size:(i + 1) * size].copy_(dev_dn[i * size:(i + 1) * size], non_blocking=True)
+
+    res["down_one_copy_ms"] = timed(lambda: down(N, N, [dn]))
+    res["down_two_streams_32_ms"] = timed(lambda: down(N, 8 * MB, [dn, dn2]))
+    res["down64_one_copy_ms"] = timed(lambda: down(64 * MB, 64 * MB, [dn]))
+    res["down64_8_chunks_ms"] = timed(lambda: down(64 * MB, 8 * MB, [dn]))
+    res["down64_8_chunks_two_streams_ms"] = timed(lambda: down(64 * MB, 8 * MB, [dn, dn2]))
+    res["down64_16_chunks_two_streams_ms"] = timed(lambda: down(64 * MB, 4 * MB, [dn, dn2]))
     res["one_copy_gbps"] = round(N / res["one_copy_ms"] / 1e6, 1)
     res["chunks_32_gbps"] = round(N / res["chunks_32_ms"] / 1e6, 1)
     js = json.dumps(res)
