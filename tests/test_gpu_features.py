@@ -53,6 +53,45 @@ def test_wave_gpu_and_gpu_plus_cpu(gpu, zero_copy):
         w.cr.dispose()
 
 
+def test_gpu_plus_cpu_host_resident_pipeline_exact(gpu):
+    """CPU + GPU co-execution on host-resident arrays (bench/hetero_stream.py
+    at a small size): the GPU's share goes through the event pipeline, the
+    CPU device works in place; the law gives both a share and every element
+    matches the scalar fp32 chain (a guarded loop kernel: the CPU runner's
+    vectorized path)."""
+    src = """__global__ void gpoly(const float* x, float* y, const int* n) {
+      long long i = get_global_id(0);
+      if (i >= n[0]) return;
+      float v = x[i], acc = y[i];
+      for (int k = 0; k < 16; ++k) acc = fmaf(acc, v, 0.25f);
+      y[i] = acc;
+    }"""
+    cr = ck.ClNumberCruncher(gpu[0] + ck.ClPlatforms.all().cpus(True), src)
+    g = 1 << 22
+    lim = g - 1000
+    rng = np.random.default_rng(3)
+    x = ck.ClArray(g, np.float32)
+    x.array[:] = rng.uniform(-0.9, 0.9, g).astype(np.float32)
+    x.read_only = True
+    x.partial_read = True
+    y = ck.ClArray(g, np.float32)
+    y.partial_read = True
+    nn = ck.ClArray(np.array([lim], np.int32))
+    nn.write = False
+    y0 = rng.uniform(-1, 1, g).astype(np.float32)
+    for _ in range(6):  # the balancer moves the split between calls
+        y.array[:] = y0
+        x.next_param(y, nn).compute(cr, 1, "gpoly", g, 256, pipeline=True, pipeline_blobs=8)
+    acc = y0[:lim].copy()
+    for _ in range(16):
+        acc = (acc.astype(np.float64) * x.array[:lim] + 0.25).astype(np.float32)
+    np.testing.assert_array_equal(y.array[:lim], acc)
+    np.testing.assert_array_equal(y.array[lim:], y0[lim:])
+    r = cr.ranges(1)
+    assert len(r) == 2 and min(r) > 0 and sum(r) == g
+    cr.dispose()
+
+
 def test_aux_wave_sum_gpu(gpu):
     aux = ck.ClBuiltInAuxilliaryFunctions(wave_sum=True, block_sum=True)
     src = aux.wrap("""
