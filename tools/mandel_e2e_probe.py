@@ -21,7 +21,8 @@ if "np" in sys.argv[1:]:  # image in registered numpy memory instead of hipHostM
     m.out.elements_per_work_item = e
 for wcs in ((False,) if "np" in sys.argv[1:] else (False, True)):
     m.cr.cores.pipeline_writes_on_compute_stream = wcs
-    for blobs in (4, 8, 16):
+    for blobs in next((tuple(int(x) for x in a[6:].split(",")) for a in sys.argv[1:] if a.startswith("blobs=")),
+                      (4, 8, 16)):
         for fin in (False, True):
             cid = 100 + blobs + (50 if wcs else 0)
             for _ in range(3):
