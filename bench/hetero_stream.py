@@ -15,7 +15,10 @@ hits every config alike:
 * ``gpu``      — the GPU alone, event pipeline (``pipeline_blobs`` chunks:
   upload, kernel and download of different chunks overlap);
 * ``gpu+cpu``  — both, the reference balancing law splitting the range and
-  the GPU's part pipelined the same way.
+  the GPU's part pipelined the same way;
+* ``gpu+cpu_fit`` — both, with the overhead-aware balancer (it fits
+  t = a + b·range per device and may drop a device whose share does not pay
+  for its fixed cost; here it should keep both).
 
 ``speedup_over_cpu`` / ``speedup_over_gpu`` per intensity are the headline;
 ``shares`` is where the balancer settled.  Results verified against numpy.
@@ -62,7 +65,7 @@ y.partial_read = True
 
 configs = [("cpu", cpu)]
 if len(gpus):
-    configs += [("gpu", gpus[0]), ("gpu+cpu", gpus[0] + cpu)]
+    configs += [("gpu", gpus[0]), ("gpu+cpu", gpus[0] + cpu), ("gpu+cpu_fit", gpus[0] + cpu)]
 
 out = {"config": "hetero_stream", "n": n, "bytes_per_call": 12 * n,
        "timing": f"median of {a.rounds} interleaved rounds of {a.calls} calls per config",
@@ -82,6 +85,8 @@ for iters in [int(s) for s in a.iters.split(",")]:
     crs = {}
     for name, devs in configs:
         cr = ck.ClNumberCruncher(devs, src)
+        if name.endswith("_fit"):  # the overhead-aware balancer (t = a + b·range per device)
+            cr.overhead_aware_balancer = True
         out["devices"][name] = cr.device_names()
         crs[name] = cr
 
@@ -112,6 +117,8 @@ for iters in [int(s) for s in a.iters.split(",")]:
         if "+" in name:
             rr = cr.ranges(1)
             r["shares"] = [v / sum(rr) for v in rr]
+        if name.endswith("_fit"):
+            r["predictor"] = cr.balancer_predictor_info(1)
         res[name] = r
         cr.dispose()
     if "gpu+cpu" in res:
