@@ -49,10 +49,12 @@ ap.add_argument("--calls", type=int, default=6, help="timed calls per round and 
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--warm", type=int, default=25, help="balancer convergence calls")
 ap.add_argument("--blobs", type=int, default=8)
+ap.add_argument("--cpu-threads", type=int, default=-1,
+                help="cap on the CPU device's threads (default: the process's CPU share minus one)")
 a = ap.parse_args()
 
 plats = ck.ClPlatforms.all()
-cpu, gpus = plats.cpus(True), plats.gpus()
+cpu, gpus = plats.cpus(True, max_cpu_cores=a.cpu_threads), plats.gpus()
 n = a.n
 rng = np.random.default_rng(0)
 x = ck.ClArray(n, np.float32)
@@ -67,7 +69,7 @@ configs = [("cpu", cpu)]
 if len(gpus):
     configs += [("gpu", gpus[0]), ("gpu+cpu", gpus[0] + cpu), ("gpu+cpu_fit", gpus[0] + cpu)]
 
-out = {"config": "hetero_stream", "n": n, "bytes_per_call": 12 * n,
+out = {"config": "hetero_stream", "n": n, "bytes_per_call": 12 * n, "cpu_threads": cpu.device(0).native_info().cpu_threads,
        "timing": f"median of {a.rounds} interleaved rounds of {a.calls} calls per config",
        "pipeline_blobs": a.blobs, "devices": {}}
 
