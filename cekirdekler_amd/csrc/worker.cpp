@@ -1,5 +1,7 @@
 #include "worker.h"
 
+#include <set>
+
 #include <algorithm>
 
 #include "memory.h"
@@ -116,6 +118,7 @@ Worker::Worker(const DeviceInfo& dev, std::shared_ptr<Program> prog, int queue_c
   marker_issued_per_slot_.assign(32, 0);
   if (gpu()) {
     set_device();
+    apply_sync_mode(dev_.ordinal);
     bool pinned = false;
     marker_words_ = static_cast<uint64_t*>(host_alloc(32 * sizeof(uint64_t), 4096, &pinned));
     std::memset(marker_words_, 0, 32 * sizeof(uint64_t));
@@ -153,6 +156,27 @@ Worker::~Worker() {
         if (s) (void)hipStreamDestroy(s);
     host_free(marker_words_);
   }
+}
+
+// CEK_HIP_SYNC=blocking|yield|spin: how a host thread waits in stream and
+// event synchronisation on this device (hipSetDeviceFlags).  The default
+// leaves HIP's own choice.  A waiting thread that spins takes a CPU from a
+// co-executing CPU device's share; "blocking" sleeps until the GPU signals.
+void apply_sync_mode(int ordinal) {
+  static const unsigned flags = [] {
+    const char* e = std::getenv("CEK_HIP_SYNC");
+    const std::string m = e ? e : "";
+    if (m == "blocking") return static_cast<unsigned>(hipDeviceScheduleBlockingSync);
+    if (m == "yield") return static_cast<unsigned>(hipDeviceScheduleYield);
+    if (m == "spin") return static_cast<unsigned>(hipDeviceScheduleSpin);
+    return 0u;
+  }();
+  if (!flags) return;
+  static std::mutex mu;
+  static std::set<int> done;
+  std::lock_guard<std::mutex> g(mu);
+  if (!done.insert(ordinal).second) return;
+  if (hipSetDeviceFlags(flags) != hipSuccess) (void)hipGetLastError();  // too late for this device: keep HIP's mode
 }
 
 void Worker::set_device() const {

@@ -86,6 +86,9 @@ class CpuPool {
   bool stop_ = false;
 };
 
+// How host threads wait for GPU `ordinal` (env CEK_HIP_SYNC, worker.cpp).
+void apply_sync_mode(int ordinal);
+
 class Worker {
  public:
   Worker(const DeviceInfo& dev, std::shared_ptr<Program> prog, int queue_concurrency,
