@@ -92,7 +92,13 @@ void CpuPool::parallel_for(long long n, const std::function<void(long long)>& fn
     next_ = 0;
     gen_.fetch_add(1, std::memory_order_release);
   }
-  cv_.notify_all();
+  // wake only as many pool threads as there are items beyond the caller's
+  // first (a small range need not wake the whole pool)
+  if (n - 1 >= static_cast<long long>(threads_.size())) {
+    cv_.notify_all();
+  } else {
+    for (long long k = 0; k < n - 1; ++k) cv_.notify_one();
+  }
   for (long long i = next_++; i < n; i = next_++) fn(i);
   // every item is claimed; wait (spinning first) for the threads still running one
   if (pool_may_spin()) {
