@@ -109,18 +109,23 @@ def test_guarded_loop_kernel_exact_and_bounded(cpu):
 
 def test_kernel_that_cannot_be_inlined_still_builds(cpu):
     """Kernels are force-inlined into their runner; one the compiler cannot
-    inline (here: recursive) is rebuilt as a plain call."""
-    src = """__global__ void rec(float* x) {
+    inline (here: non-tail recursion, which g++ refuses as "recursive
+    inlining") is rebuilt as a plain call."""
+    src = """__global__ void rec(float* x, int* d) {
       long long i = get_global_id(0);
-      if (x[i] >= 5.0f) return;
+      if (d[i] <= 0) return;
+      d[i] -= 1;
       x[i] += 1.0f;
-      rec(x);
+      rec(x, d);
+      x[i] += 0.5f;
     }"""
     c = ck.ClNumberCruncher(cpu, src)
     assert c.error_code() == 0, c.error_message()
-    x = ck.ClArray(np.arange(256, dtype=np.float32) % 4)
-    x.compute(c, 1, "rec", 256, 64)
-    np.testing.assert_array_equal(x.array, np.full(256, 5.0, np.float32))
+    depth = np.arange(256, dtype=np.int32) % 4
+    x = ck.ClArray(np.zeros(256, np.float32))
+    d = ck.ClArray(depth.copy())
+    x.next_param(d).compute(c, 1, "rec", 256, 64)
+    np.testing.assert_array_equal(x.array, 1.5 * depth.astype(np.float32))
 
 
 def test_elements_per_work_item_and_partial(cpu):
