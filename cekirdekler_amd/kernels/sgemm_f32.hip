@@ -473,8 +473,8 @@ __device__ __forceinline__ void gemm_f32_direct(const int* __restrict__ dims, co
   // pinned by a scheduling barrier, instead of one burst of loads
   auto mma_ld = [&](const f32x4(&a)[FM], const f32x4(&b)[FN], f32x4(&na)[FM], f32x4(&nb)[FN], int kb_next) {
     // VAR 2: over all 4·FM groups; VAR 3: over the first half, so the last
-    // load has half a block of MFMAs more to land
-    constexpr int NL = FM + FN, NG = VAR == 3 ? 2 * FM : 4 * FM;
+    // load has half a block of MFMAs more to land; VAR 4: the first quarter
+    constexpr int NL = FM + FN, NG = VAR == 4 ? FM : VAR == 3 ? 2 * FM : 4 * FM;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -525,7 +525,7 @@ __device__ __forceinline__ void gemm_f32_direct(const int* __restrict__ dims, co
       cek_tie(b1);
       mma(a1, b1);
     } else {
-      static_assert(VAR == 2 || VAR == 3, "VAR is 0, 1, 2 or 3");
+      static_assert(VAR >= 2 && VAR <= 4, "VAR is 0 .. 4");
       mma_ld(a0, b0, a1, b1, kb + 1);
       mma_ld(a1, b1, a0, b0, kb + 2 < nkb ? kb + 2 : 0);
     }
@@ -559,6 +559,7 @@ CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g8, 2, 4, 8, 4, 0)
 CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g8t, 2, 4, 8, 4, 1)
 CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g8i, 2, 4, 8, 4, 2)  // loads spread between MFMA groups
 CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g8h, 2, 4, 8, 4, 3)  // spread over the first half
+CEK_GEMM_F32G_KERNEL(cek_sgemm_f32_256x256g8q, 2, 4, 8, 4, 4)  // spread over the first quarter
 
 #define CEK_GEMM_F32_KERNEL(NAME, WM, WN, FM, FN, PIPE)                                           \
   extern "C" __global__ __launch_bounds__(64 * WM * WN) void NAME(                                 \

@@ -121,6 +121,7 @@ F32_TILES = {
     "256x256g8t": (256, 256, 512, "cek_sgemm_f32_256x256g8t"),
     # the next block's loads spread over all MFMA groups
     "256x256g8i": (256, 256, 512, "cek_sgemm_f32_256x256g8i"),
+    "256x256g8q": (256, 256, 512, "cek_sgemm_f32_256x256g8q"),  # over the first quarter
     "128x128": (128, 128, 256, "cek_sgemm_f32_128x128"),
 }
 

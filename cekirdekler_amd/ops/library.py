@@ -25,7 +25,8 @@ LIBRARY = {
                   "cek_sgemm_f32_256x256ir", "cek_sgemm_f32_256x256ib7", "cek_sgemm_f32_256x128ie",
                   "cek_sgemm_f32_256x256w", "cek_sgemm_f32_256x256g", "cek_sgemm_f32_256x256gt", "cek_sgemm_f32_256x256gh",
                   "cek_sgemm_f32_256x256g8", "cek_sgemm_f32_256x256g8t",
-                  "cek_sgemm_f32_256x256g8i", "cek_sgemm_f32_256x256g8h"],
+                  "cek_sgemm_f32_256x256g8i", "cek_sgemm_f32_256x256g8h",
+                  "cek_sgemm_f32_256x256g8q"],
     "mandelbrot": ["cek_mandelbrot_f32", "cek_mandelbrot_blk8_f32", "cek_mandelbrot_blk8h_f32",
                    "cek_mandelbrot_blk8k_f32", "cek_mandelbrot_blk8m_f32", "cek_mandelbrot_blk8t_f32",
                    "cek_mandelbrot_blk8u_f32"],

@@ -256,7 +256,7 @@ def test_nbody_steps_two_logical_devices(resident):
 
 
 @pytest.mark.parametrize("tile", ["128x128", "256x128", "256x256", "256x256w", "256x256ir", "256x256ib7", "256x128ie",
-                                  "256x256g", "256x256gt", "256x256gh", "256x256g8", "256x256g8t", "256x256g8i", "256x256g8h"])
+                                  "256x256g", "256x256gt", "256x256gh", "256x256g8", "256x256g8t", "256x256g8i", "256x256g8h", "256x256g8q"])
 @pytest.mark.parametrize("shape", [(512, 512, 256), (768, 512, 96), (512, 256, 32)])
 def test_gemm_f32_matches_fp64(tile, shape):
     """fp32 matrix-core GEMM (v_mfma_f32_16x16x4_f32) against a float64 host
