@@ -94,10 +94,14 @@ def rows_to_tile(b: np.ndarray, geom) -> np.ndarray:
 F32_TILES = {
     # production: register-direct, 8 waves of 128×64 — fragments loaded
     # global → VGPR, no LDS, no barrier — with the next block's loads spread
-    # over the first half of the current block's MFMA groups (152.9 TF at
-    # 8192³ vs hipBLASLt 152.8 and the burst-load g8 149.5 in one process,
-    # profiles/round4_session5.md)
+    # evenly over the current block's MFMA groups (152.8 TF at 8192³ vs
+    # hipBLASLt 152.8 on one box, 152.0 / 151.7 vs 152.0 on another, where
+    # the first-half spread g8h ran 151.2 / 150.6; profiles/round4_session5.md,
+    # round4_session6.md)
+    "256x256g8i": (256, 256, 512, "cek_sgemm_f32_256x256g8i"),
+    # the same loads spread over the first half / quarter of the groups
     "256x256g8h": (256, 256, 512, "cek_sgemm_f32_256x256g8h"),
+    "256x256g8q": (256, 256, 512, "cek_sgemm_f32_256x256g8q"),
     # burst loads ahead of each block's MFMAs (151.4 TF vs hipBLASLt 153.4 on
     # another box, 256x256ir 138.6 there)
     "256x256g8": (256, 256, 512, "cek_sgemm_f32_256x256g8"),
@@ -119,9 +123,6 @@ F32_TILES = {
     "256x256gt": (256, 256, 256, "cek_sgemm_f32_256x256gt"),
     "256x256gh": (256, 256, 256, "cek_sgemm_f32_256x256gh"),  # 4-wave form of g8h
     "256x256g8t": (256, 256, 512, "cek_sgemm_f32_256x256g8t"),
-    # the next block's loads spread over all MFMA groups
-    "256x256g8i": (256, 256, 512, "cek_sgemm_f32_256x256g8i"),
-    "256x256g8q": (256, 256, 512, "cek_sgemm_f32_256x256g8q"),  # over the first quarter
     "128x128": (128, 128, 256, "cek_sgemm_f32_128x128"),
 }
 
@@ -557,7 +558,7 @@ class GemmF32(GemmBf16):
     (same grouped tile order, so the same range partitioning and
     wave-quantized balancing apply)."""
 
-    def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256g8h",
+    def __init__(self, M: int, N: int, K: int, devices=None, tile: str = "256x256g8i",
                  cruncher: ClNumberCruncher | None = None, fill: str = "random", seed: int = 0,
                  group_m: int = 4, wave_granularity: bool | None = None):
         BM, BN, L, kname = F32_TILES[tile]
