@@ -262,6 +262,21 @@ static inline double rsqrt(double x) { return 1.0 / std::sqrt(x); }
 static inline float __fdividef(float a, float b) { return a / b; }
 static inline float __fsqrt_rn(float x) { return std::sqrt(x); }
 using std::min; using std::max;
+// float overloads of the math functions in the global namespace, as HIP
+// provides them on the GPU: sin(float) is sinf, not sin(double) rounded
+using std::sin; using std::cos; using std::tan; using std::asin; using std::acos; using std::atan;
+using std::atan2; using std::sinh; using std::cosh; using std::tanh; using std::exp; using std::exp2;
+using std::log; using std::log2; using std::log10; using std::pow; using std::sqrt; using std::cbrt;
+using std::fabs; using std::floor; using std::ceil; using std::fmod; using std::fmin; using std::fmax;
+using std::round; using std::trunc; using std::hypot;
+#if defined(__GNUC__) && !defined(__clang__)
+// vector variants from glibc's libmvec (since 2.22), so g++ can vectorize a
+// work-item loop that calls them (clang gets the same from -fveclib=libmvec)
+extern "C" float sinf(float) noexcept __attribute__((__simd__("notinbranch")));
+extern "C" float cosf(float) noexcept __attribute__((__simd__("notinbranch")));
+extern "C" float expf(float) noexcept __attribute__((__simd__("notinbranch")));
+extern "C" float logf(float) noexcept __attribute__((__simd__("notinbranch")));
+#endif
 template <class T> static inline T atomicAdd(T* p, T v) {
   T old, nv; __atomic_load(p, &old, __ATOMIC_RELAXED);
   do { nv = old + v; } while (!__atomic_compare_exchange(p, &old, &nv, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST));
@@ -636,7 +651,7 @@ bool compile_cpu(const std::string& rsrc, const std::vector<std::string>& option
   for (auto& o : options) flags += " " + o;
   // "vplan": the build may fall back to clang (below); part of the key so a
   // cache entry from before that fallback existed is not reused
-  std::string key = hash_hex(rsrc + "\x01" + cxx + "\x01" + flags + "\x01vplan");
+  std::string key = hash_hex(rsrc + "\x01" + cxx + "\x01" + flags + "\x01vplan-libmvec");
   std::string dir = cache_dir();
   so_path = dir + "/cpu_" + key + ".so";
   struct stat st;
@@ -670,11 +685,21 @@ bool compile_cpu(const std::string& rsrc, const std::vector<std::string>& option
     const char* rocm = getenv("ROCM_PATH");
     const std::string clang = std::string(rocm && *rocm ? rocm : "/opt/rocm") + "/llvm/bin/clang++";
     if (report.find("vectorized") == std::string::npos && stat(clang.c_str(), &st) == 0) {
+      // -fveclib=libmvec: math calls in the loop use glibc's vector
+      // variants; the build is kept only if it loads (every libmvec symbol
+      // it names exists here), else rebuilt without it
       const std::string tmp2 = tmp_so + ".vplan";
-      const std::string alt = clang + " " + flags + " -mllvm -enable-vplan-native-path -o " + tmp2 + " " + src_path +
-                              " > /dev/null 2>&1";
-      if (std::system(alt.c_str()) == 0) rename(tmp2.c_str(), tmp_so.c_str());
-      else unlink(tmp2.c_str());
+      for (const char* veclib : {" -fveclib=libmvec", ""}) {
+        const std::string alt = clang + " " + flags + veclib + " -mllvm -enable-vplan-native-path -o " + tmp2 + " " +
+                                src_path + " > /dev/null 2>&1";
+        if (std::system(alt.c_str()) != 0) continue;
+        void* h = dlopen(tmp2.c_str(), RTLD_NOW | RTLD_LOCAL);
+        if (!h) continue;
+        dlclose(h);
+        rename(tmp2.c_str(), tmp_so.c_str());
+        break;
+      }
+      unlink(tmp2.c_str());
     }
   }
   unlink(vec_path.c_str());
