@@ -176,6 +176,7 @@ class ClNumberCruncher:
         self.repeat_kernel_name = ""
         self.performance_feed = False
         self.number_of_errors_happened = 0
+        self._call_cache = {}
         self._cores = None
         if len(devices) == 0:
             self._error_code, self._error_message = 1, "no device selected"
@@ -602,7 +603,24 @@ class ClNumberCruncher:
                     local_range: int = 256, global_offset: int = 0, pipeline: bool = False,
                     pipeline_type: bool = PIPELINE_EVENT, pipeline_blobs: int = 4, specs=None,
                     granularity: int = 0):
-        """Validate a compute and freeze it into a native ComputeCall."""
+        """Validate a compute and freeze it into a native ComputeCall.
+
+        A repeated compute (same id, kernels, ranges, pipeline settings,
+        repeat settings and the same native array specs — a spec changes with
+        any flag or storage change) reuses the call built the first time:
+        validation and the native struct's construction are ~5-8 µs of the
+        host's per-compute cost, which is most of a small kernel's."""
+        cache_key = None
+        if specs is None and isinstance(pipeline_blobs, (int, np.integer)):
+            pin = bool(self._cores is not None and self._cores.capturing)
+            arr_specs = [a._spec(pin=pin) for a in group.arrays]
+            cache_key = (int(compute_id), kernels if isinstance(kernels, str) else tuple(kernels),
+                         int(global_range), int(local_range), int(global_offset), bool(pipeline),
+                         bool(pipeline_type), int(pipeline_blobs), int(granularity), int(self.repeat_count),
+                         self.repeat_kernel_name, pin, tuple(map(id, arr_specs)))
+            hit = self._call_cache.get(cache_key)
+            if hit is not None:
+                return hit[0]
         names = split_kernel_names(kernels)
         G, L = int(global_range), int(local_range)
         # pipeline_blobs: a count (equal blobs), or explicit work-item bounds
@@ -621,8 +639,12 @@ class ClNumberCruncher:
         call.kernels = names
         call.repeats = max(1, int(self.repeat_count))
         call.repeat_kernel = self.repeat_kernel_name if self.repeat_count > 1 else ""
-        pin = bool(self._cores is not None and self._cores.capturing)
-        call.arrays = specs if specs is not None else [a._spec(pin=pin) for a in group.arrays]
+        if specs is not None:
+            call.arrays = specs
+        else:
+            pin = bool(self._cores is not None and self._cores.capturing)
+            arr_specs = [a._spec(pin=pin) for a in group.arrays]
+            call.arrays = arr_specs
         call.global_range = G
         call.local_range = L
         call.global_offset = int(global_offset)
@@ -638,6 +660,12 @@ class ClNumberCruncher:
                 raise ClComputeError(f"granularity({granularity}) must be a multiple of the local range({L}) "
                                      f"and divide the global range({G})")
             call.granularity = int(granularity)
+        if cache_key is not None:
+            if len(self._call_cache) >= 64:
+                self._call_cache.clear()
+            # the entry holds the spec objects its key names by id(), so no
+            # id is reused while the entry lives
+            self._call_cache[cache_key] = (call, arr_specs)
         return call
 
     def compute(self, arrays, compute_id: int, kernels, global_range: int, local_range: int = 256,

@@ -80,6 +80,30 @@ def test_kernel_with_inner_loop_vectorized_runner_exact(cpu):
     np.testing.assert_array_equal(y.array, acc)
 
 
+def test_repeated_compute_reuses_the_built_call(cpu):
+    """A repeated compute reuses its native call; any flag or storage change
+    of an array, or another range, builds a new one — and the results follow
+    the new flags."""
+    c = ck.ClNumberCruncher(cpu, SRC)
+    x = ck.ClArray(np.zeros(256, np.float32))
+    g = ck.ClParameterGroup([x])
+    first = c._build_call(g, 1, "inc", 256, 64)
+    assert c._build_call(g, 1, "inc", 256, 64) is first
+    assert c._build_call(g, 1, "inc", 128, 64) is not first  # another range
+    x.write = False  # another flag: another spec, another call
+    assert c._build_call(g, 1, "inc", 256, 64) is not first
+    x.write = True
+    x.elements_per_work_item = 2
+    assert c._build_call(g, 1, "inc", 128, 64) is not first
+    x.elements_per_work_item = 1
+    for _ in range(3):
+        x.compute(c, 1, "inc", 256, 64)
+    np.testing.assert_array_equal(x.array, np.full(256, 3.0, np.float32))
+    x.compute(c, 1, "inc", 128, 64)  # half the range: only the first half moves
+    np.testing.assert_array_equal(x.array[:128], np.full(128, 4.0, np.float32))
+    np.testing.assert_array_equal(x.array[128:], np.full(128, 3.0, np.float32))
+
+
 def test_guarded_loop_kernel_exact_and_bounded(cpu):
     """A guard ("if (i >= n) return;") ahead of a loop: the vectorized
     runner must leave the items past the guard untouched and match the
