@@ -48,6 +48,16 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
   if (const char* e = std::getenv("CEK_DEVICE_SPANS")) device_spans = std::string(e) != "0";
   if (const char* e = std::getenv("CEK_KERNEL_D2H")) set_kernel_d2h(std::string(e) != "0");
   if (const char* e = std::getenv("CEK_ZC_RELEASE")) zc_release = std::string(e) != "0";
+  // GPU and CPU devices in one Cores: a GPU worker waiting for its stream
+  // sleeps instead of spinning (a blocking-sync event), so the wait does not
+  // take a core from the CPU device's pool (the process's CPU share is
+  // exactly the pool's size); env CEK_SLEEP_WAITS=0/1 overrides
+  {
+    bool any_gpu = false, any_cpu = false;
+    for (auto& d : devices) (d.type == kGPU ? any_gpu : any_cpu) = true;
+    sleep_waits = any_gpu && any_cpu;
+    if (const char* e = std::getenv("CEK_SLEEP_WAITS")) sleep_waits = std::string(e) != "0";
+  }
   time_scale_.assign(workers_.size(), 1.0);
   time_offset_.assign(workers_.size(), 0.0);
   enabled_.assign(workers_.size(), true);
@@ -1216,7 +1226,7 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
       }
       CEK_HIP(hipEventRecord(ds->gap_a, s));
     }
-    if (wk.gpu()) CEK_HIP(hipStreamSynchronize(s));
+    if (wk.gpu()) wk.wait_stream(s, sleep_waits);
     t_phase_arrived = true;
     const double w0 = now_ms();
     phase_->arrive_and_wait();
@@ -1248,7 +1258,7 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
   span_end(wk, s);
   if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(s);
   if (fine_grained) wk.add_marker(s);
-  if (!enqueue_mode_ && wk.gpu()) CEK_HIP(hipStreamSynchronize(s));
+  if (!enqueue_mode_ && wk.gpu()) wk.wait_stream(s, sleep_waits);
 }
 
 void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long long ref,
@@ -1398,7 +1408,7 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
   span_end(wk, m);
   if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(m);
   if (fine_grained) wk.add_marker(m);
-  if (wk.gpu()) CEK_HIP(hipStreamSynchronize(m));
+  if (wk.gpu()) wk.wait_stream(m, sleep_waits);
 }
 
 void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long long ref,
@@ -1468,7 +1478,7 @@ void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long
   span_end(wk, m);
   if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(m);
   if (fine_grained) wk.add_marker(m);
-  if (wk.gpu()) CEK_HIP(hipStreamSynchronize(m));
+  if (wk.gpu()) wk.wait_stream(m, sleep_waits);
 }
 
 void Cores::run_device(int w, const ComputeCall& c, long long ref, long long range, bool pipelined,

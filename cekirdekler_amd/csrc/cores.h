@@ -347,7 +347,10 @@ class Cores {
   // some processes stayed at 14 ms per streamed GEMM call instead of 8
   // (profiles/hostres_streaming.md, tools/hostres_stall_probe.py)
   bool pipeline_reads_on_main_stream = true;
-  bool pipeline_reads_two_streams = false;  // explicit blobs: partial arrays alternate over two upload streams (slower: 12.7 vs 7.1 ms for the shells, the extra stream shares a hardware queue)
+  bool pipeline_reads_two_streams = false;
+  // GPU workers wait for their streams by sleeping on a blocking-sync event
+  // (default: when the Cores has both GPU and CPU devices; CEK_SLEEP_WAITS)
+  bool sleep_waits = false;  // explicit blobs: partial arrays alternate over two upload streams (slower: 12.7 vs 7.1 ms for the shells, the extra stream shares a hardware queue)
   uint64_t peer_read_min_bytes = 1u << 20;
 
  private:

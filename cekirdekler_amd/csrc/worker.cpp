@@ -154,6 +154,7 @@ Worker::~Worker() {
     for (auto e : join_ev_)
       if (e) (void)hipEventDestroy(e);
     if (sys_ev_) (void)hipEventDestroy(sys_ev_);
+    if (sleep_ev_) (void)hipEventDestroy(sleep_ev_);
     if (main_) (void)hipStreamDestroy(main_);
     for (auto s : cq_)
       if (s) (void)hipStreamDestroy(s);
@@ -409,6 +410,20 @@ void Worker::join_streams(hipStream_t target) {
   for (auto s : cq_) join(s);
   for (auto& h : pq_)
     for (auto s : h) join(s);
+}
+
+void Worker::wait_stream(hipStream_t s, bool sleep) {
+  if (!gpu()) return;
+  if (!sleep) {
+    CEK_HIP(hipStreamSynchronize(s));
+    return;
+  }
+  if (!sleep_ev_) {
+    set_device();
+    CEK_HIP(hipEventCreateWithFlags(&sleep_ev_, hipEventBlockingSync | hipEventDisableTiming));
+  }
+  CEK_HIP(hipEventRecord(sleep_ev_, s));
+  CEK_HIP(hipEventSynchronize(sleep_ev_));
 }
 
 void Worker::system_release(hipStream_t s) {

@@ -124,6 +124,9 @@ class Worker {
   int next_compute_queue();                 // round robin (Worker.cs:435-458)
   int queue_concurrency() const { return qconc_; }
   hipEvent_t event(int slot);               // pooled, timing disabled
+  // wait until stream s is idle: hipStreamSynchronize, or (sleep) a
+  // blocking-sync event the host thread sleeps on
+  void wait_stream(hipStream_t s, bool sleep);
   // `target` waits for everything queued so far on every other stream of
   // this worker (compute queues and pipeline streams): a copy issued next on
   // `target` neither overtakes a kernel still reading its destination nor
@@ -233,6 +236,7 @@ class Worker {
   hipStream_t pq_[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
   std::vector<hipEvent_t> events_;
   std::vector<hipEvent_t> join_ev_;  // one per stream slot (join_streams)
+  hipEvent_t sleep_ev_ = nullptr;
   hipEvent_t sys_ev_ = nullptr;      // system_release
   std::atomic<int> rr_{0};
 
