@@ -349,7 +349,7 @@ class Cores {
   bool pipeline_reads_on_main_stream = true;
   bool pipeline_reads_two_streams = false;
   // GPU workers wait for their streams by sleeping on a blocking-sync event
-  // (default: when the Cores has both GPU and CPU devices; CEK_SLEEP_WAITS)
+  // (off by default; CEK_SLEEP_WAITS=1)
   bool sleep_waits = false;  // explicit blobs: partial arrays alternate over two upload streams (slower: 12.7 vs 7.1 ms for the shells, the extra stream shares a hardware queue)
   uint64_t peer_read_min_bytes = 1u << 20;
 
