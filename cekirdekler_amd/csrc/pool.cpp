@@ -2,10 +2,6 @@
 // DevicePoolThread consumer loops, ClPipeline.cs:4132-4312 and :4841-5047.
 #include "pool.h"
 
-#include <sys/prctl.h>
-
-#include <cstdlib>
-
 #include <chrono>
 
 namespace cek {
@@ -199,15 +195,6 @@ int DevicePool::retire(int dev, std::vector<Inflight>& inflight) {
 }
 
 void DevicePool::consumer(int dev) {
-  // The consumer polls its in-flight tasks' marker words with 10 µs sleeps;
-  // Linux stretches a sleep by the thread's timer slack (50 µs by default),
-  // which would set the pace of a pool of short tasks.  1 µs of slack.
-  // (env CEK_POOL_SLACK_NS overrides; 0 keeps the thread's default)
-  static const unsigned long slack = [] {
-    const char* e = std::getenv("CEK_POOL_SLACK_NS");
-    return e ? std::strtoul(e, nullptr, 10) : 1000UL;
-  }();
-  if (slack) (void)prctl(PR_SET_TIMERSLACK, slack, 0UL, 0UL, 0UL);
   Cores& cr = *devs_[dev];
   const bool async = max_in_flight_ > 1;
   if (async) cr.fine_grained = true;  // a marker word after every compute
