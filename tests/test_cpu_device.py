@@ -104,7 +104,8 @@ def test_repeated_compute_reuses_the_built_call(cpu):
     np.testing.assert_array_equal(x.array[128:], np.full(128, 3.0, np.float32))
 
 
-def test_guarded_loop_kernel_exact_and_bounded(cpu):
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_guarded_loop_kernel_exact_and_bounded(cpu, pipeline):
     """A guard ("if (i >= n) return;") ahead of a loop: the vectorized
     runner must leave the items past the guard untouched and match the
     scalar fp32 chain on the others."""
@@ -123,7 +124,7 @@ def test_guarded_loop_kernel_exact_and_bounded(cpu):
     y = ck.ClArray(y0.copy())
     nn = ck.ClArray(np.array([lim], np.int32))
     nn.write = False
-    x.next_param(y, nn).compute(c, 1, "gpoly", g, 256)
+    x.next_param(y, nn).compute(c, 1, "gpoly", g, 256, pipeline=pipeline, pipeline_blobs=4)
     acc = y0[:lim].copy()
     for _ in range(16):
         acc = (acc.astype(np.float64) * x.array[:lim] + 0.25).astype(np.float32)
