@@ -44,5 +44,5 @@ for call in range(12):
     ms = (time.perf_counter() - t) * 1e3
     shares = [r / n for r in cr.ranges(1)]
     print(f"call {call:2d}: {ms:7.3f} ms  shares " + "  ".join(
-        f"{name.split()[0]} {s:.3f}" for name, s in zip(cr.device_names(), shares)))
+        f"{name[:24]} {s:.3f}" for name, s in zip(cr.device_names(), shares)))
 cr.dispose()
