@@ -20,8 +20,16 @@ device-resident after the first call and C stays in device memory
 (BASELINE.md "device-resident"); the host-resident variant (A/B uploaded and
 C slices downloaded each call) is reported separately.  Data: synthetic
 uniform [-1, 1) bf16.  After the timed loops every rank downloads its device
-replica of C and compares sampled tiles of its own range with a float64 host
-product; the bench exits non-zero when the relative error exceeds 5e-3.  Rank 0 prints one JSON line.
+replica of C and compares EVERY tile of its own range with a float64 product
+computed by torch on its GPU (``GemmBf16.verify_full``); the bench exits
+non-zero when the relative error exceeds 1e-4 (measured: ~1.5e-6).
+
+Rank 0 prints ONE compact JSON line (< 6 KB, so a log tail keeps it whole):
+the headline fields, then ``extra`` with one short summary per config and
+the metric's own components LAST (``load_balance_iters``,
+``mandelbrot_4k``, ``sgemm``).  Everything measured — per-round arrays,
+predictor fits, placements — goes to ``--detail`` (default
+``gpurun_out/bench_detail_n{N}.json`` and ``profiles/bench_detail_n{N}.json``).
 
 In a container without a GPU the headline runs a plain kernel-string GEMM on
 each rank's CPU device instead (``"device": "cpu"`` in the config): that is
@@ -155,10 +163,12 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
                enter=lambda: setattr(cr, "enqueue_mode", True),
                leave=lambda: setattr(cr, "enqueue_mode", False))
     ranges = cr.ranges(1)
-    # the benchmarked output itself: sampled tiles of this rank's C replica
-    # against a float64 host product (before the host-resident run below
-    # re-splits compute id 2 and overwrites the host copy)
-    err = _max_over_ranks(ctx, g.verify(compute_id=1))
+    # the benchmarked output itself: EVERY tile of this rank's C replica
+    # against a float64 product on its GPU (before the host-resident run
+    # below re-splits compute id 2 and overwrites the host copy)
+    err, tiles_checked = g.verify_full(compute_id=1)
+    err = _max_over_ranks(ctx, err)
+    tiles_checked = int(_sum_over_ranks(ctx, tiles_checked))
     # owners that found their split-K helper late and multiplied its K-range
     # themselves (C correct either way; nonzero = a shared GPU)
     fallbacks = int(_sum_over_ranks(ctx, g.handover_fallbacks()))
@@ -191,7 +201,9 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
         step_a()
     leave_async()
     ms_async = timed(ctx, step_a, steps, 0, enter=enter_async, leave=leave_async)
-    err_async = _max_over_ranks(ctx, ga.verify(compute_id=cid_a))
+    err_async, tiles_async = ga.verify_full(compute_id=cid_a)
+    err_async = _max_over_ranks(ctx, err_async)
+    tiles_async = int(_sum_over_ranks(ctx, tiles_async))
     if ga is not g:
         for a in (ga.A, ga.B, ga.C, ga.dims):
             a.dispose()
@@ -217,7 +229,7 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
 
     ms_host = timed(ctx, host_step, host_steps, 2)
     # the streamed host-resident output: this rank's tiles of the host C
-    err_host = _max_over_ranks(ctx, g.verify(compute_id=2, host=True))
+    err_host = _max_over_ranks(ctx, g.verify_full(compute_id=2, host=True)[0])
     ms_blobs, mode = ms_host, f"compute() event pipeline, {blobs} equal blobs" if blobs else "compute() serial 3-phase"
     ms_shells = ms_native_shells = ms_shells_cu = None
     panels = HOST_RESIDENT_PANELS
@@ -227,7 +239,7 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
         # shell s; A and B go up one row panel per blob), whose first kernels
         # need two panels instead of all of B
         ms_shells = timed(ctx, lambda: g.run_shells(panels, compute_id=3), host_steps, 2)
-        err_shells = g.verify(compute_id=3, host=True)
+        err_shells = g.verify_full(compute_id=3, host=True)[0]
         err_host = max(err_host, err_shells)
         if ms_shells < ms_host:
             ms_host, mode = ms_shells, f"compute() event pipeline, {panels} shell blobs"
@@ -237,7 +249,7 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
         try:
             cr.copy_cus, cr.kernel_d2h = HOST_RESIDENT_COPY_CUS, True
             ms_shells_cu = timed(ctx, lambda: g.run_shells(panels, compute_id=4), host_steps, 2)
-            err_host = max(err_host, g.verify(compute_id=4, host=True))
+            err_host = max(err_host, g.verify_full(compute_id=4, host=True)[0])
         finally:
             cr.kernel_d2h, cr.copy_cus = False, 0
         if ms_shells_cu < ms_host:
@@ -250,9 +262,10 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
     for a in (g.A, g.B, g.C, g.dims):
         a.dispose()  # release 0.5 GB of pinned host memory before the next config
     # headline: the faster of the two enqueue schedules (both reported)
-    single = {"ms": ms, "gflops": g.flops / (ms * 1e-3) / 1e9, "tile": tile, "max_rel_err": err}
+    single = {"ms": ms, "gflops": g.flops / (ms * 1e-3) / 1e9, "tile": tile, "max_rel_err": err,
+              "tiles_checked": tiles_checked}
     overlapped = {"ms": ms_async, "gflops": g.flops / (ms_async * 1e-3) / 1e9, "tile": ga.tile,
-                  "max_rel_err": err_async, "balancer_setup_calls": converge_a}
+                  "max_rel_err": err_async, "tiles_checked": tiles_async, "balancer_setup_calls": converge_a}
     best = overlapped if ms_async < ms else single
     timing = ("enqueue mode on async queues (consecutive GEMMs overlap; reference enqueueModeAsyncEnable)"
               if best is overlapped else "enqueue mode, one queue")
@@ -265,6 +278,7 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
             "host_resident_blob_pipeline_ms": ms_blobs, "host_resident_shells_ms": ms_shells,
             "host_resident_native_shells_ms": ms_native_shells, "host_resident_shells_copy_cus_ms": ms_shells_cu,
             "ranges": ranges, "max_rel_err": max(err, err_async, err_host), "max_rel_err_host_resident": err_host,
+            "tiles_checked": tiles_checked, "tiles_total": g.tiles,
             "handover_fallbacks": fallbacks, "device": "gpu"}
 
 
@@ -316,7 +330,8 @@ def bench_sgemm_cpu(ctx, steps, warmup, size=256):
     return {"ms": ms, "gflops": flops / (ms * 1e-3) / 1e9, "tile": "cpu-naive", "balancer_setup_calls": converge,
             "sync_per_step_ms": ms, "sync_per_step_gflops": flops / (ms * 1e-3) / 1e9,
             "host_resident_ms": ms, "host_resident_gflops": flops / (ms * 1e-3) / 1e9,
-            "ranges": ranges, "max_rel_err": err, "handover_fallbacks": 0, "device": "cpu"}
+            "ranges": ranges, "max_rel_err": err, "handover_fallbacks": 0, "device": "cpu",
+            "tiles_checked": size * size, "tiles_total": size * size}
 
 
 def _all_ranges(ctx, ranges):
@@ -381,11 +396,12 @@ def _row_major_comparison(steps: int) -> dict:
         cr.enqueue_mode = False
         torch.cuda.synchronize()
         runs.append((time.perf_counter() - t0) / steps)
-    err = g.verify(compute_id=1, tiles_per_device=4)
+    err, tiles = g.verify_full(compute_id=1)
     cr.dispose()
     for arr in (g.A, g.B, g.C, g.dims):
         arr.dispose()
-    out = {"tile": "256x256pbr", "gflops": round(flops / statistics.median(runs) / 1e9, 1), "max_rel_err": err}
+    out = {"tile": "256x256pbr", "gflops": round(flops / statistics.median(runs) / 1e9, 1), "max_rel_err": err,
+           "tiles_checked": tiles}
     try:
         a = torch.randn(size, size, device="cuda", dtype=torch.bfloat16)
         b = torch.randn(size, size, device="cuda", dtype=torch.bfloat16).T
@@ -550,6 +566,8 @@ def bench_node_configs(world: int) -> dict:
         out["sgemm_host_resident_rccl"] = {"skipped": f"{world} ranks on {torch.cuda.device_count()} GPU(s); "
                                                       "RCCL needs one GPU per rank"}
     configs.append(("hetero_stream", [sys.executable, "hetero_stream.py"]))
+    # the reference's read/compute/write overlap claim on a balanced workload
+    configs.append(("pipeline_overlap", [sys.executable, "pipeline_overlap.py"]))
     t_start = time.monotonic()
     for name, cmd in configs:
         # the extras share one time budget, so a hung config cannot push the
@@ -576,11 +594,148 @@ def bench_node_configs(world: int) -> dict:
     return out
 
 
-MAX_REL_ERR = 5e-3
+MAX_REL_ERR = 1e-4  # bf16 inputs, fp32 accumulation: measured ~1.5e-6 relative to max |ref| per tile
 NODE_CONFIGS_BUDGET_S = 360  # all of bench_node_configs' child processes together
 HOST_RESIDENT_BLOBS = 8
 HOST_RESIDENT_PANELS = 16
 HOST_RESIDENT_COPY_CUS = 8
+
+
+def write_detail(full: dict, world: int, path=None, gpu: bool = True) -> str:
+    """Everything the run measured, as one JSON file (the printed line only
+    summarises it): ``path``, else ``gpurun_out/bench_detail_n{N}.json`` and,
+    for a GPU run, ``profiles/bench_detail_n{N}.json``.  Returns the path the
+    line cites."""
+    paths = [path] if path else [os.path.join(ROOT, "gpurun_out", f"bench_detail_n{world}.json")] + (
+        [os.path.join(ROOT, "profiles", f"bench_detail_n{world}.json")] if gpu else [])
+    written = None
+    for p in paths:
+        try:
+            os.makedirs(os.path.dirname(p) or ".", exist_ok=True)
+            with open(p, "w") as f:
+                json.dump(full, f, indent=1, default=str)
+            written = written or os.path.relpath(p, ROOT)
+        except OSError:
+            pass
+    return written or ""
+
+
+def _r(x, nd=3):
+    """Round a number for the summary line (None and non-numbers pass)."""
+    if isinstance(x, bool) or not isinstance(x, (int, float)):
+        return x
+    return round(float(x), nd)
+
+
+def _pick(d, keys, nd=3):
+    """{key: rounded value} for the keys of ``d`` that exist (an error or
+    skip note passes through whole, cut to 160 characters)."""
+    if not isinstance(d, dict):
+        return d
+    if "error" in d or "skipped" in d:
+        return {k: str(d[k])[:160] for k in ("error", "skipped") if k in d}
+    return {k: _r(d[k], nd) for k in keys if k in d}
+
+
+def compact_extra(full: dict, detail: str) -> dict:
+    """The printed line's ``extra``: one short summary per config, with the
+    headline metric's own components last (load-balance iters,
+    Mandelbrot-4k, SGEMM), so even a truncated log keeps them (VERDICT r4
+    next #1).  ``full`` is what :func:`write_detail` writes."""
+    ex = {"detail_file": detail}
+    peers = full.get("peer_topology") or {}
+    if peers:
+        bw = peers.get("bandwidth") or {}
+        same = (bw.get("same_gpu") or {}).get("sdma") or {}
+        pairs = bw.get("pairs") or []
+        ex["peer"] = {"gpus_visible": peers.get("gpus_visible"), "path": peers.get("path"),
+                      "same_gpu_sdma_gbps": _r(same.get("gbps"), 1),
+                      "pair_gbps_max": _r(max((q.get("gbps", 0) for q in pairs if isinstance(q, dict)), default=None), 1),
+                      "all_verified": bw.get("all_verified")}
+    if full.get("sgemm_host_resident_rccl") is not None:
+        ex["rccl_host_resident"] = _pick(full["sgemm_host_resident_rccl"],
+                                         ["ranks", "split_reads_ms", "max_rel_err_split_reads",
+                                          "max_rel_err_gathered_replicas"], 7)
+    hs = full.get("hetero_stream")
+    if isinstance(hs, dict):
+        if "error" in hs or "skipped" in hs:
+            ex["hetero_stream"] = _pick(hs, [])
+        else:
+            ex["hetero_stream"] = {k: {**{c: _r((v.get(c) or {}).get("ms")) for c in ("cpu", "gpu", "gpu+cpu", "gpu+cpu_fit")
+                                           if isinstance(v.get(c), dict)},
+                                       "x_cpu": _r(v.get("speedup_over_cpu")), "x_gpu": _r(v.get("speedup_over_gpu"))}
+                                   for k, v in hs.items() if k.startswith("iters_") and isinstance(v, dict)}
+    wv = full.get("wave_cpu_gpu")
+    if isinstance(wv, dict):
+        w = _pick(wv, ["cpu_ms_per_frame", "gpu_ms_per_frame", "gpu+cpu_ms_per_frame", "gpu+cpu_fit_ms_per_frame",
+                       "speedup_gpu+cpu_over_cpu", "speedup_gpu_over_cpu", "speedup_gpu+cpu_fit_over_cpu"], 4)
+        pred = wv.get("gpu+cpu_fit_predictor")
+        if isinstance(pred, dict):
+            w["fit_decision"] = pred.get("decision")
+        ex["wave_cpu_gpu"] = w
+    if full.get("saxpy_1m_cpu") is not None:
+        ex["saxpy_1m_cpu"] = _pick(full["saxpy_1m_cpu"], ["ms", "GBps", "bit_exact_vs_numpy"], 4)
+    po = full.get("pipeline_overlap")
+    if isinstance(po, dict):
+        p = _pick(po, ["read_compute_write_ms", "ideal_speedup_sum_over_max", "pipeline_speedup_event",
+                       "pipeline_speedup_driver", "best_event", "best_event_4streams", "best_driver_q4",
+                       "best_driver_q16", "event_5_vs_4_streams", "driver_q4_vs_q16", "outputs_exact", "lcg_iters"])
+        if isinstance(po.get("ms"), dict):
+            p["3phase_ms"] = po["ms"].get("3phase")
+        ex["pipeline_overlap"] = p
+    tp = full.get("task_pool")
+    if isinstance(tp, dict):
+        t = _pick(tp, ["tasks", "pool_devices", "cu_partitioned", "makespan_ms", "ideal_ms_sum_over_devices",
+                       "makespan_over_ideal", "dispatch_tasks_per_s", "host_us_per_task", "median_task_device_us",
+                       "serial_group_in_order", "gemm_task_max_rel_err", "reduce_task_rel_err"])
+        rr = tp.get("round_robin")
+        if isinstance(rr, dict):
+            t["round_robin_makespan_over_ideal"] = _r(rr.get("makespan_over_ideal"))
+        ex["task_pool"] = t
+    nb = full.get("nbody_pipeline")
+    if isinstance(nb, dict):
+        n = _pick(nb, ["n", "gpus_used", "cu_partitioned", "push_ms_median", "force_stage_pct_fp32_peak",
+                       "min_device_busy_fraction", "device_busy_fraction", "overlap_efficiency",
+                       "step_check_max_rel_err"], 4)
+        co = nb.get("copy_overlap")
+        if isinstance(co, dict):
+            n["copy_overlap_with_force"] = co.get("with_force_stage")
+        ex["nbody_pipeline"] = n
+    # ---- the headline metric's components, last ----
+    lb = full.get("load_balance_iters") or {}
+    ex["load_balance_iters"] = _pick(lb, ["iters", "steady_share_dev0"], 4) if lb else None
+    mb = full.get("mandelbrot_4k") or {}
+    if mb:
+        m = _pick(mb, ["ms", "gflops", "kernel"], 4)
+        ko = mb.get("kernel_only")
+        if isinstance(ko, dict):
+            m["kernel_only"] = _pick(ko, ["kernel", "ms", "pct_fp32_peak_157_3"], 4)
+            two = ko.get("frames_in_flight_2")
+            if isinstance(two, dict):
+                m["kernel_only"]["pct_2_frames"] = two.get("pct_fp32_peak_157_3")
+                m["kernel_only"]["images_equal"] = two.get("images_equal")
+        ex["mandelbrot_4k"] = m
+    else:
+        ex["mandelbrot_4k"] = None
+    sg = full.get("sgemm") or {}
+    rc = full.get("sgemm_row_major_c") or {}
+    all_ranges = full.get("sgemm_ranges_all_ranks") or [sg.get("ranges")]
+    sq, aq = sg.get("single_queue") or {}, sg.get("async_queues") or {}
+    ex["sgemm"] = {
+        "gflops_single_queue": _r(sq.get("gflops"), 1), "gflops_async_queues": _r(aq.get("gflops"), 1),
+        "gflops_sync_per_step": _r(sg.get("sync_per_step_gflops"), 1),
+        "tile": sg.get("tile"), "ranges": sg.get("ranges"),
+        "ranges_identical_on_all_ranks": all(r == all_ranges[0] for r in all_ranges),
+        "balancer_setup_calls": sg.get("balancer_setup_calls"),
+        "max_rel_err_full": _r(sg.get("max_rel_err"), 9),
+        "tiles_checked": sg.get("tiles_checked"), "tiles_total": sg.get("tiles_total"),
+        "host_resident_ms": _r(sg.get("host_resident_ms")),
+        "host_resident_mode": sg.get("host_resident_mode"),
+        "host_resident_max_rel_err": _r(sg.get("max_rel_err_host_resident"), 9),
+        "row_major_c_gflops": _r(rc.get("gflops"), 1), "hipblaslt_fp32_out_gflops": rc.get("hipblaslt_fp32_out_gflops"),
+        "vs_hipblaslt": rc.get("vs_hipblaslt"), "handover_fallbacks": sg.get("handover_fallbacks"),
+    }
+    return ex
 
 
 def _peer_topology(world: int) -> dict:
@@ -632,6 +787,8 @@ def parse_args(argv=None):
     ap.add_argument("--skip-mandelbrot", action="store_true")
     ap.add_argument("--skip-node-configs", action="store_true",
                     help="skip the N-body pipeline and task-pool configs (rank 0, after the headline)")
+    ap.add_argument("--detail", default=None,
+                    help="path of the full results JSON (default: gpurun_out/ and profiles/bench_detail_n{N}.json)")
     return ap.parse_args(argv)
 
 
@@ -671,6 +828,12 @@ def main(argv=None) -> int:
     ok = sg["max_rel_err"] <= MAX_REL_ERR
     if ctx.rank == 0:
         size = args.size if use_gpu else min(args.size, 512)
+        full = {
+            "sgemm": sg, "sgemm_ranges_all_ranks": all_ranges,
+            "sgemm_row_major_c": rowc, "mandelbrot_4k": mb, "load_balance_iters": lb, **node,
+            "peer_topology": peers,
+        }
+        detail = write_detail(full, ctx.world, args.detail, gpu=use_gpu)
         out = {
             "metric": METRIC,
             "value": round(sg["gflops"], 1),
@@ -690,41 +853,9 @@ def main(argv=None) -> int:
                        "parallelism": f"range-partition dp{ctx.world}",
                        "timing": sg.get("timing", "enqueue mode, one queue"),
                        "device": sg["device"]},
-            "extra": {
-                "sgemm_device_resident_gflops": round(sg["gflops"], 1),
-                "sgemm_sync_per_step_gflops": round(sg["sync_per_step_gflops"], 1),
-                "sgemm_single_queue": sg.get("single_queue"),
-                "sgemm_async_queues": sg.get("async_queues"),
-                "sgemm_host_resident_gflops": round(sg["host_resident_gflops"], 1),
-                "sgemm_host_resident_ms": round(sg["host_resident_ms"], 3),
-                "sgemm_host_resident_stream_blobs": sg.get("host_resident_blobs", 0),
-                "sgemm_host_resident_calls_ms": sg.get("host_resident_calls_ms", []),
-                "sgemm_host_resident_pipelined": sg.get("host_resident_pipelined", []),
-                "sgemm_host_resident_max_rel_err": sg.get("max_rel_err_host_resident"),
-                "sgemm_host_resident_mode": sg.get("host_resident_mode"),
-                "sgemm_host_resident_blob_pipeline_ms": sg.get("host_resident_blob_pipeline_ms"),
-                "sgemm_host_resident_shells_ms": sg.get("host_resident_shells_ms"),
-                "sgemm_host_resident_native_shells_ms": sg.get("host_resident_native_shells_ms"),
-                "sgemm_host_resident_shells_copy_cus_ms": sg.get("host_resident_shells_copy_cus_ms"),
-                "sgemm_max_rel_err": sg["max_rel_err"],
-                "sgemm_handover_fallbacks": sg["handover_fallbacks"],
-                "sgemm_balancer_setup_calls": sg["balancer_setup_calls"],
-                "sgemm_ranges": sg["ranges"],
-                "sgemm_ranges_identical_on_all_ranks": all(r == all_ranges[0] for r in all_ranges),
-                "sgemm_row_major_c_gflops": rowc.get("gflops"),
-                "sgemm_row_major_c": rowc,
-                "mandelbrot_4k": mb,
-                "load_balance_iters": lb,
-                "nbody_pipeline": node.get("nbody_pipeline"),
-                "task_pool": node.get("task_pool"),
-                "saxpy_1m_cpu": node.get("saxpy_1m_cpu"),
-                "wave_cpu_gpu": node.get("wave_cpu_gpu"),
-                "sgemm_host_resident_rccl": node.get("sgemm_host_resident_rccl"),
-                "hetero_stream": node.get("hetero_stream"),
-                "peer_topology": peers,
-            },
+            "extra": compact_extra(full, detail),
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out, separators=(",", ":")), flush=True)
         if not ok:
             print(f"bench.py: SGEMM output check failed: max rel err {sg['max_rel_err']:.3e} "
                   f"(limit {MAX_REL_ERR})", file=sys.stderr, flush=True)

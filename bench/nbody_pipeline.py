@@ -157,10 +157,18 @@ ap.add_argument("--pushes", type=int, default=14)
 ap.add_argument("--gpus", type=int, default=0, help="0 = all visible")
 ap.add_argument("--logical", type=int, default=0, help="rehearsal: act as if GPU 0 were this many GPUs")
 ap.add_argument("--placement", choices=("shared", "split"), default="shared")
+ap.add_argument("--cu-partition", type=int, choices=(0, 1), default=1,
+                help="with --logical: the logical devices are disjoint CU partitions of GPU 0 (default) "
+                     "or share all of its CUs")
 a = ap.parse_args()
 n = a.n
 g = ck.ClPlatforms.all().gpus()
-if a.logical > 1:
+if a.logical > 1 and a.cu_partition:
+    # four logical devices that each own a quarter of the
+    # CUs (every XCD represented): the 4-GPU placement with each "GPU" a
+    # disjoint CU set, so device busy fractions mean what they would on 4 GPUs
+    g = g[0:1].cu_partitions(a.logical)
+elif a.logical > 1:
     g0 = g[0]
     for _ in range(a.logical - 1):
         g0 = g0 + g[0]
@@ -302,7 +310,9 @@ emit({"config": "nbody_pipeline_3stage", "n": n, "systems_in_flight": M, "gpus_u
       / len({devs[0].device(k).info.ordinal for k in range(len(devs[0]))}),
       "overlap_efficiency": max(stage_ms) / ms, "serial_over_push": sum(stage_ms) / ms,
       "steps_per_system": steps, "step_check_max_rel_err": check,
-      "logical_rehearsal": a.logical > 1, "placement": [[d.device(k).name + f"#{d.device(k).info.ordinal}"
+      "logical_rehearsal": a.logical > 1, "cu_partitioned": bool(a.logical > 1 and a.cu_partition),
+      "placement": [[d.device(k).name + f"#{d.device(k).info.ordinal}" + (
+          f"/cu{d.device(k).cu_partition[0]}of{d.device(k).cu_partition[1]}" if d.device(k).cu_partition else "")
                                                            for k in range(len(d))] for d in devs],
       "copy_ms_per_push": ov_any["copy_ms"] / a.pushes,
       "copy_overlap": {"with_force_stage": round(ov_force["fraction"], 4),

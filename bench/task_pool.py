@@ -23,11 +23,17 @@ and DEVICE_ROUND_ROBIN, ClPipeline.cs:3792-3806), and the pool's dispatch
 rate is measured on 4096 near-zero-cost tasks (``dispatch``).  With one GPU
 the pool has 8 logical devices of it, the node's width.
 
-Makespan is compared with the ideal Σ(task time) / physical GPUs, where a
-task's time is its kernel's hipEvent device time run alone on one GPU.  The
-ideal is not a strict floor: tasks that occupy a fraction of the CUs (gemm,
-nbody) run beside each other on one GPU when several are in flight.  The
-outputs of the serial group, of a GEMM task and of a reduction task are
+Makespan is compared with the ideal Σ(task time) / pool devices, where a
+task's time is its kernel's hipEvent device time run alone on one pool
+device.  At N GPUs the pool devices are the GPUs.  On one GPU (VERDICT r4
+next #7) the 8 pool devices are CU PARTITIONS of it (``--cu-partition``,
+the default there): logical device d owns 32 of the 256 CUs, spread over
+all 8 XCDs (``ClDevices.cu_partitions``, CU-masked HIP streams), so the 8
+devices run side by side on disjoint CUs like 8 small GPUs, every task is
+timed alone on one partition, and ``makespan_over_ideal`` is a physically
+meaningful proxy for the 8-GPU target (≤ 1.15).  Without partitions the 8
+logical devices share every CU and the ratio divides by one GPU's time.
+The outputs of the serial group, of a GEMM task and of a reduction task are
 checked against numpy.  The same script runs unchanged at N GPUs.
 """
 import argparse
@@ -66,16 +72,22 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--gpus", type=int, default=0)
 ap.add_argument("--logical", type=int, default=8, help="logical devices per GPU when only one GPU (8: the node's width)")
 ap.add_argument("--queues", type=int, default=3)
+ap.add_argument("--cu-partition", type=int, choices=(0, 1), default=1,
+                help="one GPU: the logical devices are disjoint CU partitions of it (default) or share it whole")
 a = ap.parse_args()
 g = ck.ClPlatforms.all().gpus()
 ng = len(g) if a.gpus <= 0 else min(a.gpus, len(g))
 devs = g[0:ng]
-if ng == 1 and a.logical > 1:
+partitioned = ng == 1 and a.logical > 1 and bool(a.cu_partition)
+if partitioned:
+    devs = g[0:1].cu_partitions(a.logical)
+elif ng == 1 and a.logical > 1:
     for _ in range(a.logical - 1):
         devs = devs + g[0]
 rng = np.random.default_rng(3)
 prebuilt = library(*LIBS)
-ref_cr = ck.ClNumberCruncher(g[0], SRC, prebuilt=prebuilt)
+# the per-task reference times: alone on ONE pool device (a partition when partitioned)
+ref_cr = ck.ClNumberCruncher(devs[0], SRC, prebuilt=prebuilt)
 NS = 1 << 22  # streaming / reduction elements
 
 
@@ -255,7 +267,7 @@ def run_policy(policy):
 
 
 ntasks, makespan, counts, dispatch = run_policy(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL)
-ideal = sum(single) / max(1, ng)
+ideal = sum(single) / (len(devs) if partitioned else max(1, ng))
 _, makespan_rr, counts_rr, dispatch_rr = run_policy(ClDevicePoolType.DEVICE_ROUND_ROBIN)
 
 # checks: serial group order (x ← 2x + 1, eight times from 0 = 255), one GEMM, one reduction
@@ -274,8 +286,15 @@ emit({"config": "task_pool_256", "tasks": ntasks, "gpus": ng, "logical_devices":
       "kernel_mix": {k: len(v) for k, v in per_kind.items()} | {"add(serial group)": SERIAL, "barrier": 1},
       "task_device_ms": {k: {"median": float(np.median(v)), "min": float(np.min(v)), "max": float(np.max(v))}
                          for k, v in per_kind.items()},
-      "makespan_ms": makespan, "ideal_ms_sum_over_gpus": ideal, "ideal_basis": "hipEvent device time per task, alone",
+      "cu_partitioned": partitioned,
+      "makespan_ms": makespan, "ideal_ms_sum_over_devices": ideal,
+      "ideal_basis": ("hipEvent device time per task, alone on one CU partition; sum / partitions" if partitioned
+                      else "hipEvent device time per task, alone on one GPU; sum / GPUs"),
       "makespan_over_ideal": makespan / ideal, "tasks_per_s": ntasks / (makespan * 1e-3),
+      # the pool's host cost per task (one producer, D consumers) against
+      # the device time one task feeds: the pool keeps up when it is below
+      "host_us_per_task": round(1e6 / dispatch, 2),
+      "median_task_device_us": round(1e3 * float(np.median(single)), 2),
       "per_device_tasks": counts, "serial_group_in_order": serial_ok,
       "round_robin": {"makespan_ms": makespan_rr, "makespan_over_ideal": makespan_rr / ideal,
                       "per_device_tasks": counts_rr, "dispatch_tasks_per_s": round(dispatch_rr)},

@@ -22,7 +22,7 @@ import numpy as np
 
 from ._native import cek, kernel_dir
 from .arrays import ClArray, ClParameterGroup, _register_cores, as_clarray
-from .hardware import ClDevices, ClPlatforms
+from .hardware import ClDevices, ClPlatforms, hw_queue_count
 
 PIPELINE_EVENT = True    # Cores.PIPELINE_EVENT (Cores.cs:416-423)
 PIPELINE_DRIVER = False  # Cores.PIPELINE_DRIVER
@@ -151,7 +151,7 @@ class ClNumberCruncher:
     """
 
     def __init__(self, devices, kernel_source: str = "", cpu_cores: int = -1, num_gpus: int = -1,
-                 stream: bool = True, no_pipelining: bool = False, queue_concurrency: int = 16,
+                 stream: bool = True, no_pipelining: bool = False, queue_concurrency: Optional[int] = None,
                  prebuilt: Optional[Sequence] = None, options: Optional[Sequence[str]] = None,
                  smooth: bool = True):
         if isinstance(devices, (AcceleratorType, int, str)):
@@ -166,6 +166,10 @@ class ClNumberCruncher:
                 "with `__cek_child__ void child(long long id, long long param, <parent's params>)` "
                 "(GPU-resident child levels, see ClNumberCruncher.device_enqueue_errors)")
         cfg = cek.CoresConfig()
+        # async-enqueue / driver-pipeline streams per device: one per hardware
+        # queue unless asked (the reference's fixed 16 aliases onto 4 queues)
+        if queue_concurrency is None:
+            queue_concurrency = hw_queue_count()
         cfg.queue_concurrency = int(queue_concurrency)
         self._queue_concurrency = max(1, min(16, int(queue_concurrency)))
         cfg.no_pipelining = bool(no_pipelining)

@@ -95,9 +95,12 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("pci_device", &DeviceInfo::pci_device)
       .def_readwrite("clock_khz", &DeviceInfo::clock_khz)
       .def_readwrite("lds_per_block", &DeviceInfo::lds_per_block)
+      .def_readwrite("cu_part", &DeviceInfo::cu_part)
+      .def_readwrite("cu_parts", &DeviceInfo::cu_parts)
       .def("describe", &DeviceInfo::describe)
       .def("__repr__", [](const DeviceInfo& d) { return "<DeviceInfo " + d.describe() + ">"; });
 
+  m.def("partition_cus", &partition_cus, py::arg("ncu"), py::arg("parts"), py::arg("p"));
   m.def("gpu_count", &gpu_count);
   m.def("enumerate_devices", &enumerate_devices);
   m.def("gpu_info", &gpu_info);
@@ -342,6 +345,15 @@ PYBIND11_MODULE(_cek, m) {
       .def("allreduce_sum_f32", [](RcclComm& c, uint64_t p, uint64_t n, uint64_t stream) {
         c.allreduce_sum_f32(reinterpret_cast<void*>(p), n, reinterpret_cast<hipStream_t>(stream));
       }, py::call_guard<py::gil_scoped_release>());
+
+  m.def("allgatherv_plan", [](int rank, int world, const std::vector<uint64_t>& offsets,
+                              const std::vector<uint64_t>& sizes) {
+        py::list out;
+        for (const auto& op : allgatherv_plan(rank, world, offsets, sizes))
+          out.append(py::make_tuple(op.send ? "send" : "recv", op.peer, op.offset, op.bytes));
+        return out;
+      }, py::arg("rank"), py::arg("world"), py::arg("offsets"), py::arg("sizes"),
+      "The (kind, peer, offset, bytes) point-to-point ops one rank issues for an uneven all-gather-v.");
 
   // device→device copy engines (xgmi.h)
   m.def("measure_copy", [](int src, int dst, uint64_t bytes, int engine, int reps, int stream_ordinal) {

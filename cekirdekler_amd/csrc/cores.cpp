@@ -1304,8 +1304,12 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
       const long long k = explicit_blobs ? q : q / halves;
       const int h = explicit_blobs ? static_cast<int>(q % 2) : static_cast<int>(q % halves);
       // reads_on_main_stream: every blob's upload follows the full reads on
-      // the main stream (one in-order chain of copies)
-      hipStream_t rs = pipeline_reads_on_main_stream ? m : wk.pipe_stream(h, 0), ks = wk.pipe_stream(h, 1);
+      // the main stream (one in-order chain of copies).  Explicit blobs always
+      // upload there: blob q's kernels may read panels uploaded by earlier
+      // blobs of the OTHER half (shell s reads panels 0..s), which only one
+      // in-order upload chain orders before them
+      const bool reads_main = pipeline_reads_on_main_stream || explicit_blobs;
+      hipStream_t rs = reads_main ? m : wk.pipe_stream(h, 0), ks = wk.pipe_stream(h, 1);
       // writes_on_compute_stream: a blob's D2H follows its kernel on the same
       // stream (in-stream order) instead of a write stream gated by an event
       hipStream_t ws = pipeline_writes_on_compute_stream ? ks : wk.pipe_stream(pipeline_writes_one_stream ? 0 : h, 2);
@@ -1313,7 +1317,7 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
       const long long len = explicit_blobs ? c.blob_bounds[q + 1] - c.blob_bounds[q] : chunk;
       const int ksid = 17 + 3 * h + 1;
       const int wsid = pipeline_writes_on_compute_stream ? ksid : (pipeline_writes_one_stream ? 19 : ksid + 1);
-      const int rsid = pipeline_reads_on_main_stream ? 0 : ksid - 1;  // as logged for the schedule checker
+      const int rsid = reads_main ? 0 : ksid - 1;  // as logged for the schedule checker
       auto blob_slice = [&](const ArraySpec& a, uint64_t& b, uint64_t& n) {
         if (explicit_blobs && a.blob_begin.size() == c.blob_bounds.size() - 1) {
           b = a.blob_begin[q];
@@ -1516,7 +1520,10 @@ void Cores::run_device_body(int w, const ComputeCall& c, long long ref, long lon
       run_driver_pipeline(wk, gidx, c, ref, range, h2d, d2h);
   } else if (collective(c)) {
     // still take part in the collectives (a rank the split rounded down to
-    // an empty range must join every RCCL call the others make)
+    // an empty range must join every RCCL call the others make).  On the
+    // inline path the calling thread's device is the caller's, not this
+    // worker's: its streams, events and communicator need the worker's
+    wk.set_device();
     run_3phase(wk, gidx, c, ref, 0, h2d, d2h);
   }
   double el = now_ms() - t0 - t_phase_wait;

@@ -7,7 +7,8 @@
 //   * event-driven pipeline: the device's range cut into `blobs` chunks that
 //     stream through two half-pipelines, each {read, compute, write} HIP
 //     streams joined by hipEvents (Cores.cs:1197-1367, Worker.cs:1411-1567),
-//   * driver pipeline: chunk k on round-robin stream k mod 16
+//   * driver pipeline: chunk k on round-robin stream k mod Q (Q = queue
+//     concurrency, by default the GPU_MAX_HW_QUEUES hardware queues)
 //     (Cores.cs:1368-1958).
 // plus enqueue mode / async enqueue / no-compute / fine-grained markers /
 // repeat + sync kernel (ClNumberCruncher.cs:66-187, Cores.cs:72-126,

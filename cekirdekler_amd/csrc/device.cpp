@@ -22,7 +22,18 @@ std::string DeviceInfo::describe() const {
   os << " CUs=" << compute_units << " mem=" << (mem_bytes >> 20) << "MiB";
   if (type == kCPU) os << " threads=" << cpu_threads;
   os << (dedicated_memory ? " dedicated" : " shared") << (streaming ? " stream" : "");
+  if (cu_parts > 1) os << " cu-part=" << cu_part << "/" << cu_parts;
   return os.str();
+}
+
+std::vector<int> partition_cus(int ncu, int parts, int p) {
+  if (parts < 1 || ncu < parts || ncu % parts != 0) throw Error("partition_cus: CUs must split into whole partitions");
+  if (p < 0 || p >= parts) throw Error("partition_cus: partition index out of range");
+  const int block = ncu / parts;
+  std::vector<int> out;
+  for (int c = 0; c < ncu; ++c)
+    if ((c % parts + c / block) % parts == p) out.push_back(c);
+  return out;
 }
 
 int gpu_count() {

@@ -28,8 +28,22 @@ struct DeviceInfo {
   int pci_device = -1;
   int clock_khz = 0;
   uint64_t lds_per_block = 0;
+  // CU partition of a logical GPU device (cu_parts > 1): every stream of its
+  // worker is created with a CU mask holding only partition cu_part's CUs
+  // (partition_cus), so logical devices of one GPU run side by side on
+  // disjoint CUs instead of sharing all of them
+  int cu_part = -1;
+  int cu_parts = 0;
   std::string describe() const;
 };
+
+// CUs of partition p of `parts` equal partitions of a GPU with `ncu` CUs
+// (ncu divisible by parts; MI355X: 256 CUs in 8 XCDs of 32).  CU c belongs to
+// partition (c mod parts + c div (ncu / parts)) mod parts.  Whether the CU
+// mask numbers the CUs XCD by XCD (XCD = c div 32) or round robin over the
+// XCDs (XCD = c mod 8), each partition gets the same number of CUs on every
+// XCD: ncu / parts / 8 (tests/test_cu_partition.py checks both numberings).
+std::vector<int> partition_cus(int ncu, int parts, int p);
 
 // Number of HIP GPUs (0 when no runtime / no device; never throws).
 int gpu_count();

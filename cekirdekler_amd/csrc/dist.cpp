@@ -162,20 +162,54 @@ void RcclComm::allgatherv(void* dptr, const std::vector<uint64_t>& offsets,
     return;
   }
   // Uneven slices (the balancer moved work): every rank sends its slice
-  // straight to each peer.  The MI355X node is a full xGMI mesh — one link
-  // per GPU pair — so the N−1 sends of a rank leave on N−1 different links
-  // at once and each link carries one slice, where a ring (or a group of
-  // ring broadcasts) pushes every slice over every link it passes.  Sizes
-  // are identical on all ranks, so zero-byte pairs are skipped on both
-  // sides.
+  // straight to each peer (allgatherv_plan).  The MI355X node is a full xGMI
+  // mesh — one link per GPU pair — so the N−1 sends of a rank leave on N−1
+  // different links at once and each link carries one slice, where a ring (or
+  // a group of ring broadcasts) pushes every slice over every link it passes.
   auto* comm = static_cast<ncclComm_t>(comm_);
-  CEK_NCCL(ncclGroupStart());
-  for (int k = 1; k < world_; ++k) {
-    const int to = (rank_ + k) % world_, from = (rank_ - k + world_) % world_;
-    if (sizes[rank_] > 0) CEK_NCCL(ncclSend(base + offsets[rank_], sizes[rank_], ncclChar, to, comm, s));
-    if (sizes[from] > 0) CEK_NCCL(ncclRecv(base + offsets[from], sizes[from], ncclChar, from, comm, s));
+  const auto plan = allgatherv_plan(rank_, world_, offsets, sizes);
+  if (plan.empty()) return;
+  // A throw between ncclGroupStart and ncclGroupEnd must still close the
+  // group: an open group turns every later call on this communicator into a
+  // confusing failure.
+  struct Group {
+    bool open = false;
+    void start() {
+      CEK_NCCL(ncclGroupStart());
+      open = true;
+    }
+    void end() {
+      open = false;
+      CEK_NCCL(ncclGroupEnd());
+    }
+    ~Group() {
+      if (open) (void)ncclGroupEnd();
+    }
+  } group;
+  group.start();
+  for (const auto& op : plan) {
+    if (op.send)
+      CEK_NCCL(ncclSend(base + op.offset, op.bytes, ncclChar, op.peer, comm, s));
+    else
+      CEK_NCCL(ncclRecv(base + op.offset, op.bytes, ncclChar, op.peer, comm, s));
   }
-  CEK_NCCL(ncclGroupEnd());
+  group.end();
+}
+
+std::vector<P2POp> allgatherv_plan(int rank, int world, const std::vector<uint64_t>& offsets,
+                                   const std::vector<uint64_t>& sizes) {
+  if (world < 1 || rank < 0 || rank >= world) throw Error("allgatherv_plan: bad rank / world");
+  if (static_cast<int>(offsets.size()) != world || static_cast<int>(sizes.size()) != world)
+    throw Error("allgatherv_plan: one offset and one size per rank");
+  std::vector<P2POp> plan;
+  // step k: send to rank+k, receive from rank−k (every rank's k-th pair is a
+  // matched shift, so no link carries two slices in one step)
+  for (int k = 1; k < world; ++k) {
+    const int to = (rank + k) % world, from = (rank - k + world) % world;
+    if (sizes[rank] > 0) plan.push_back({true, to, offsets[rank], sizes[rank]});
+    if (sizes[from] > 0) plan.push_back({false, from, offsets[from], sizes[from]});
+  }
+  return plan;
 }
 
 void RcclComm::allreduce_sum_f32(void* dptr, uint64_t count, hipStream_t s) {

@@ -61,6 +61,22 @@ class Comm {
   virtual void allreduce_sum_f64(void* dptr, uint64_t count, hipStream_t s) = 0;
 };
 
+// One point-to-point transfer of an uneven all-gather-v, from this rank's
+// point of view: send this rank's slice to `peer`, or receive `peer`'s.
+struct P2POp {
+  bool send;
+  int peer;
+  uint64_t offset, bytes;
+};
+
+// The grouped sends/receives rank `rank` issues for an uneven all-gather-v
+// (RcclComm::allgatherv).  Pure function of the (identical on every rank)
+// offsets/sizes, so the pairing — every send matched by exactly one receive
+// of the same bytes at the peer, zero-byte pairs skipped on both sides — is
+// checked on the CPU for every world size (tests/test_allgatherv_plan.py).
+std::vector<P2POp> allgatherv_plan(int rank, int world, const std::vector<uint64_t>& offsets,
+                                   const std::vector<uint64_t>& sizes);
+
 // RCCL communicator over xGMI (one GPU per rank).
 class RcclComm : public Comm {
  public:

@@ -63,13 +63,19 @@ void DevicePool::enqueue(const std::vector<PoolTask>& tasks) {
         for (int d = 0; d < num_devices(); ++d) {
           Item c = it;
           c.target = d;
+          // the first copy is the barrier; the others follow it at once
+          if (d > 0) c.task.type &= ~static_cast<uint32_t>(kTaskSyncFirst);
           queue_.push_back(std::move(c));
           ++outstanding_;
           ++pools_[pid].total;
         }
       } else {
-        if (policy_ == 1 && !(it.task.type & kTaskSyncFirst)) {
-          // strict rotation; a select/serial group keeps its first task's device
+        if (policy_ == 1) {
+          // strict rotation; a select/serial group keeps its first task's
+          // device.  Barrier tasks (SyncFirst, also inherited from the
+          // previous task's SyncLast) are targeted too: the barrier itself is
+          // enforced at take time, and a group whose BEGIN or END carries one
+          // must still open / close its rotation slot
           if (rr_group_ >= 0) {
             it.target = rr_group_;
           } else {
@@ -124,12 +130,14 @@ int DevicePool::limit_locked() {
 bool DevicePool::take_locked(int dev, Item& out) {
   for (size_t j = 0; j < queue_.size(); ++j) {
     Item& u = queue_[j];
-    if (u.target >= 0 && u.target != dev) continue;  // another device's broadcast copy
-    if (u.target < 0 && owner_ >= 0 && owner_ != dev) return false;  // group pinned elsewhere
     if (u.task.type & kTaskSyncFirst) {
-      // a barrier: every earlier task has retired and nothing precedes it
+      // a barrier: every earlier task has retired and nothing precedes it;
+      // no later task passes it, whichever device it is targeted at
+      if (u.target >= 0 && u.target != dev) return false;
       if (j != 0 || running_ > 0) return false;
     }
+    if (u.target >= 0 && u.target != dev) continue;  // another device's broadcast copy / rotation slot
+    if (u.target < 0 && owner_ >= 0 && owner_ != dev) return false;  // group pinned elsewhere
     if (u.target < 0 && owner_ < 0 && (u.task.type & (kTaskSelectBegin | kTaskSerialBegin))) {
       // a new select/serial group: pin it to the least-loaded device
       owner_ = least_loaded_locked();

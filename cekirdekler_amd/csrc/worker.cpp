@@ -321,6 +321,15 @@ void Worker::release_all() {
 hipStream_t Worker::new_stream(bool copy_cus) {
   set_device();
   hipStream_t s = nullptr;
+  if (dev_.cu_parts > 1) {
+    // a CU-partitioned logical device: every stream (copy-kernel ones too)
+    // sees its partition's CUs only
+    const int ncu = std::max(1, dev_.compute_units);
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0);
+    for (int cu : partition_cus(ncu, dev_.cu_parts, dev_.cu_part)) mask[cu / 32] |= 1u << (cu % 32);
+    CEK_HIP(hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask.size()), mask.data()));
+    return s;
+  }
   if (cu_reserve_ <= 0) {
     CEK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     return s;

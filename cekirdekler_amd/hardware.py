@@ -54,14 +54,33 @@ def usable_cpus() -> int:
     return max(1, n)
 
 
+def hw_queue_count() -> int:
+    """Hardware queues HIP gives this process per GPU: ``GPU_MAX_HW_QUEUES``
+    (HIP's default, and the MI355X box's setting, is 4), clamped to 1..16.
+
+    Streams beyond this count alias onto shared hardware queues and pick up
+    false dependencies (one stream's copy waits behind another stream's
+    kernel): on one box 4 async GEMM queues gave 1399 TF/s against 1329 with
+    16 (profiles/round4_session4.md).  So the default async-enqueue and
+    driver-pipeline queue count is this, not the reference's 16
+    (Worker.cs:435-458, Cores.cs:1383-1855)."""
+    v = os.environ.get("GPU_MAX_HW_QUEUES", "").strip()
+    n = int(v) if v.isdigit() and int(v) > 0 else 4
+    return max(1, min(16, n))
+
+
 class ClDevice:
     """One selectable device plus its selection flags."""
 
-    def __init__(self, info, partition: bool = False, streaming: bool = False, max_cpu_cores: int = -1):
+    def __init__(self, info, partition: bool = False, streaming: bool = False, max_cpu_cores: int = -1,
+                 cu_partition: Optional[tuple] = None):
         self.info = info
         self.partition = bool(partition)
         self.streaming = bool(streaming)
         self.max_cpu_cores = int(max_cpu_cores)
+        # (p, k): this logical GPU device runs on CU partition p of k
+        # (ClDevices.cu_partitions); None = every CU of the GPU
+        self.cu_partition = tuple(cu_partition) if cu_partition else None
 
     @property
     def is_gpu(self) -> bool:
@@ -81,6 +100,8 @@ class ClDevice:
 
     @property
     def compute_units(self) -> int:
+        if self.cu_partition:
+            return self.info.compute_units // self.cu_partition[1]
         return self.info.compute_units
 
     numberOfComputeUnits = compute_units
@@ -99,7 +120,11 @@ class ClDevice:
     def native_info(self):
         """DeviceInfo handed to the native runtime (CPU pool sized here)."""
         if not self.is_cpu:
-            return self.info
+            if not self.cu_partition:
+                return self.info
+            info = cek.gpu_info(self.info.ordinal)
+            info.cu_part, info.cu_parts = self.cu_partition
+            return info
         hw = usable_cpus()
         threads = hw - 1 if (self.partition and hw > 1) else hw
         if self.max_cpu_cores > 0:
@@ -114,10 +139,11 @@ class ClDevice:
     def copy(self, partition=None, streaming=None, max_cpu_cores=None) -> "ClDevice":
         return ClDevice(self.info, self.partition if partition is None else partition,
                         self.streaming if streaming is None else streaming,
-                        self.max_cpu_cores if max_cpu_cores is None else max_cpu_cores)
+                        self.max_cpu_cores if max_cpu_cores is None else max_cpu_cores, self.cu_partition)
 
     def __repr__(self) -> str:
-        return f"<ClDevice {self.info.describe()}>"
+        part = f" cu-part={self.cu_partition[0]}/{self.cu_partition[1]}" if self.cu_partition else ""
+        return f"<ClDevice {self.info.describe()}{part}>"
 
 
 class ClDevices:
@@ -146,6 +172,28 @@ class ClDevices:
 
     def __add__(self, other: "ClDevices") -> "ClDevices":
         return ClDevices(self.devices + list(other.devices))
+
+    def cu_partitions(self, parts: int) -> "ClDevices":
+        """Every GPU of the list as ``parts`` logical devices, each running on
+        its own 1/parts of the GPU's CUs (CU-masked streams,
+        ``hipExtStreamCreateWithCUMask``; every partition holds CUs of every
+        XCD, ``cek.partition_cus``).  The reference lets one device be added
+        to a pool or a stage several times (ClPipeline.cs:1728, :4337) and
+        then shares it whole; partitions make the same logical devices run
+        side by side on disjoint CUs, so a one-GPU box can stand in for
+        ``parts`` smaller GPUs.  Non-GPU devices are kept as they are."""
+        parts = int(parts)
+        out = []
+        for d in self.devices:
+            if not d.is_gpu or parts <= 1:
+                out.append(d)
+                continue
+            if d.info.compute_units % parts:
+                raise ValueError(f"{d.info.compute_units} CUs do not split into {parts} partitions")
+            out += [ClDevice(d.info, d.partition, d.streaming, d.max_cpu_cores, (p, parts)) for p in range(parts)]
+        return ClDevices(out)
+
+    cuPartitions = cu_partitions
 
     def _copy(self, devs, partition, streaming, max_cpu_cores) -> "ClDevices":
         return ClDevices(d.copy(partition, streaming, max_cpu_cores) for d in devs)

@@ -536,6 +536,69 @@ class GemmBf16:
         self.C.array[:] = saved
         return worst
 
+    def verify_full(self, compute_id: int = 1, host: bool = False, device=None) -> tuple:
+        """Whole-output check: EVERY C tile this process's devices own under
+        the split of ``compute_id``, against a float64 product computed by
+        torch on ``device`` (default: torch's current GPU, else the CPU).
+        Each local device's C replica is downloaded (``host=True``: the host C
+        of a host-resident call is checked as it is), untiled on ``device``
+        and compared tile by tile.  Returns ``(max_rel_err, tiles_checked)``;
+        the error of a tile is ``max |C - ref| / max |ref|`` over the tile."""
+        import torch
+
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else (
+                torch.device("cpu"))
+        M, N, K, BM, BN = self.M, self.N, self.K, self.BM, self.BN
+        ntm, ntn = M // BM, N // BN
+
+        def operand(arr, rows):
+            x = arr.array
+            if x.dtype == np.uint16:  # bf16 bit patterns
+                t = torch.from_numpy(x.view(np.int16)).to(device).view(torch.bfloat16)
+            else:
+                t = torch.from_numpy(x).to(device)
+            return t.reshape(rows, K).double()
+
+        ref = operand(self.A, M) @ operand(self.B, N).T  # [M][N] float64
+        ref_tiles = ref.view(ntm, BM, ntn, BN).permute(0, 2, 1, 3)  # [ntm][ntn][BM][BN]
+        del ref
+        ranges = self.cr.ranges(compute_id)
+        refs = self.cr.references(compute_id)
+        unit = self.L * self.split_k
+        saved = self.C.array.copy()
+        worst, checked = 0.0, 0
+        try:
+            for dev in range(self.cr._cores.num_devices):
+                g = self.cr._cores.global_base + dev
+                t0, nt = refs[g] // unit, ranges[g] // unit
+                if nt == 0:
+                    continue
+                if not host:
+                    self.cr.download(self.C, dev)
+                tm, tn = tile_coords(np.arange(t0, t0 + nt), M, N, BM, BN, self.group_m,
+                                     self._orders.get(compute_id, 0))
+                tm_t = torch.from_numpy(np.asarray(tm, np.int64)).to(device)
+                tn_t = torch.from_numpy(np.asarray(tn, np.int64)).to(device)
+                c = torch.from_numpy(self.C.array).to(device)
+                if getattr(self, "row_major_c", False):
+                    got = c.view(ntm, BM, ntn, BN).permute(0, 2, 1, 3)[tm_t, tn_t]
+                else:
+                    flat = c.view(-1, BM * BN)[t0:t0 + nt]
+                    if self.geom is None:
+                        got = flat.view(nt, BM, BN)
+                    else:
+                        WM, WN, FM, FN = self.geom
+                        got = flat.view(nt, WM, WN, FM, FN, 4, 16, 4).permute(0, 1, 3, 5, 7, 2, 4, 6).reshape(nt, BM, BN)
+                want = ref_tiles[tm_t, tn_t]
+                err = (got.double() - want).abs().amax(dim=(1, 2)) / want.abs().amax(dim=(1, 2)).clamp_min(1e-30)
+                worst = max(worst, float(err.max()))
+                checked += nt
+                del c, got, want, err
+        finally:
+            self.C.array[:] = saved
+        return worst, checked
+
     def _download_slice(self, dev: int, lo: int, n: int) -> None:
         # a sub-view ClArray sharing the same uid would alias buffers; the
         # native download copies the whole replica, slice afterwards

@@ -495,7 +495,7 @@ def _intersection(b, e, intervals) -> float:
 class DevicePipeline:
     """N stages on one device, overlapped on separate HIP streams."""
 
-    def __init__(self, device: ClDevices, kernel_source: str, queue_concurrency: int = 16):
+    def __init__(self, device: ClDevices, kernel_source: str, queue_concurrency: Optional[int] = None):
         if len(device) != 1:
             raise ValueError("DevicePipeline runs on exactly one device")
         self.cruncher = ClNumberCruncher(device, kernel_source, queue_concurrency=queue_concurrency)

@@ -296,7 +296,8 @@ class ClDevicePool:
             if t.group is not None and t.kernels and not (t.type & ClTaskType.TASK_MESSAGE_NO_COMPUTE
                                                           and not t.kernels):
                 bl = t.pipeline_blobs if isinstance(t.pipeline_blobs, int) else tuple(t.pipeline_blobs)
-                key = (t.compute_id, t.kernels, t.global_range, t.local_range, t.global_offset, bool(t.pipeline),
+                kn = t.kernels if isinstance(t.kernels, str) else tuple(t.kernels)
+                key = (t.compute_id, kn, t.global_range, t.local_range, t.global_offset, bool(t.pipeline),
                        bool(t.pipeline_type), bl, int(t.kernel_repeats), t.kernel_repeat_name)
                 j = index.get(key)
                 if j is None:

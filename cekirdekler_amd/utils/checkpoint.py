@@ -72,12 +72,18 @@ def _owned_slices(a: ClArray, cruncher, compute_id: Optional[int] = None) -> Opt
 def _assemble(a: ClArray, cruncher, compute_id: Optional[int]) -> List[tuple]:
     """Fill ``a``'s host copy from the device replicas: device 0's whole
     replica, then every other local device's own slice from its replica.
-    Returns the (first, end) element ranges this process owns."""
+    Returns the (first, end) element ranges this process owns: the whole
+    array when the replicas are whole (``owned is None``), nothing when the
+    split left every local device an empty range (``owned == []``: the
+    reference law does give a slow device range 0, HelperFunctions.cs:190-280,
+    and such a replica holds stale data everywhere)."""
     cores = cruncher.cores
     owned = _owned_slices(a, cruncher, compute_id)
     cruncher.download(a, 0)
-    if not owned:
+    if owned is None:
         return [(0, a.N)]
+    if not owned:
+        return []
     host = a.array
     if any(dev != 0 for dev, _, _ in owned):
         base = host.copy()
@@ -110,6 +116,9 @@ def save(path: str, arrays: Dict[str, ClArray], cruncher=None, download: bool = 
         a = arrays[name]
         if download and cruncher is not None and not a.write and not a.zero_copy:
             owned = _assemble(a, cruncher, compute_ids.get(name))
+            # a rank ships only the slices its devices computed (possibly
+            # none); a whole replica (gathered / keep-resident) is never
+            # shipped: rank 0's own copy is already whole
             if dist_job and _owned_slices(a, cruncher, compute_ids.get(name)) is not None:
                 pieces[name] = [(lo, hi, a.array[lo:hi].tobytes()) for lo, hi in owned]
     if dist_job:

@@ -46,9 +46,14 @@ def happens_before(ops: Sequence[Op]) -> List[set]:
     return reach
 
 
-def check_pipeline_schedule(schedule: Sequence[Op]) -> int:
+def check_pipeline_schedule(schedule: Sequence[Op], prefix_uploads: bool = False) -> int:
     """Raises AssertionError on a missing dependency; returns the number of
-    checked (kernel, transfer) pairs."""
+    checked (kernel, transfer) pairs.
+
+    ``prefix_uploads``: every chunk's kernels must also run after the H2D of
+    every EARLIER chunk (explicit blobs of a shell-streamed GEMM: shell s
+    reads the row panels uploaded by blobs 0..s, which alternate between the
+    two half-pipelines)."""
     by_dev: Dict[int, List[Op]] = defaultdict(list)
     for op in schedule:
         by_dev[op[0]].append(tuple(op))
@@ -71,6 +76,11 @@ def check_pipeline_schedule(schedule: Sequence[Op]) -> int:
             for u in h2d.get(chunk, []):
                 if k not in reach[u]:
                     raise AssertionError(f"device {dev}: kernel {chunk} may start before its H2D")
+            if prefix_uploads:
+                for other, ups in h2d.items():
+                    if other[0] < chunk[0] and any(k not in reach[u] for u in ups):
+                        raise AssertionError(f"device {dev}: kernel {chunk} may start before the H2D of "
+                                             f"earlier blob {other}")
             if chunk in d2h and d2h[chunk] not in reach[k]:
                 raise AssertionError(f"device {dev}: D2H {chunk} may start before its kernels")
             checked += 1

@@ -92,3 +92,34 @@ def test_explicit_blob_count_does_not_stretch_the_range():
         g.run_shells(4, compute_id=3 + split, split_last=split)
         assert cr.ranges(3 + split) == [g.global_range]
     cr.dispose()
+
+
+@pytest.mark.parametrize("cls,tile", [(GemmBf16, "256x256pb"), (GemmBf16, "256x256pbr"), (GemmBf16, "256x128pe"),
+                                      (GemmF32, "256x256g8i")])
+def test_verify_full_checks_every_tile(cls, tile):
+    """the whole-output check compares every tile a
+    process owns (untiled from the kernel's fragment order / tile order on
+    the torch device) with a float64 product, and catches one wrong element
+    anywhere."""
+    from cekirdekler_amd.ops.gemm import rows_to_tile
+
+    cpu = ck.ClPlatforms.all().cpus(True)
+    cr = ck.ClNumberCruncher(cpu + cpu, "__global__ void nop(float* x) {}")
+    g = cls(512, 768, 256, cruncher=cr, tile=tile)
+    unit = g.L * g.split_k
+    half = g.tiles // 2 * unit
+    cr.cores.set_state(1, [half, g.tiles * unit - half], [[0.0, 0.0] for _ in range(10)], [1.0, 1.0])
+    ref = g.reference()
+    if g.row_major_c:
+        g.C.array[:] = ref.astype(np.float32).ravel()
+    else:
+        tm, tn = tile_coords(np.arange(g.tiles), g.M, g.N, g.BM, g.BN, g.group_m)
+        blocks = [ref[r * g.BM:(r + 1) * g.BM, c * g.BN:(c + 1) * g.BN].astype(np.float32) for r, c in zip(tm, tn)]
+        tiles = np.stack(blocks)
+        g.C.array[:] = (rows_to_tile(tiles, g.geom) if g.geom is not None else tiles).ravel()
+    err, checked = g.verify_full(1, host=True, device="cpu")
+    assert checked == g.tiles and err < 1e-6, (err, checked)
+    g.C.array[g.C.N - 7] += 0.5  # one element of the last tile
+    err, _ = g.verify_full(1, host=True, device="cpu")
+    assert err > 1e-4
+    cr.dispose()

@@ -48,7 +48,7 @@ def _worker(rank, world, port, q):
         lo, hi = refs[rank] * e, (refs[rank] + rng[rank]) * e
         mine[lo:hi] = 1
         mask = untile(mine, g.M, g.N, g.BM, g.BN, g.group_m, g.geom) > 0
-        ok = bool(np.abs(c[mask] - ref[mask]).max() < 5e-3 * np.abs(ref).max()) if mask.any() else True
+        ok = bool(np.abs(c[mask] - ref[mask]).max() < 1e-4 * np.abs(ref).max()) if mask.any() else True
         src = "__global__ void k(float* x) { long long i = get_global_id(0); x[i] = x[i] * 2.0f + 1.0f; }"
         cj = DistributedCruncher(src, ctx=ctx, devices=gpu)
         n = 256 * 64

@@ -640,3 +640,83 @@ def test_checkpoint_partitioned_device_state(gpu, tmp_path, ndev):
         cr.download(y, d)
         np.testing.assert_array_equal(y.array, want)
     cr.dispose()
+
+
+@pytest.mark.parametrize("zero_dev", [0, 2])
+def test_checkpoint_zero_range_device(gpu, tmp_path, zero_dev):
+    """VERDICT r4 missing #1 on one process: 4 logical devices, one of which a
+    restored state leaves with an empty range after an equal-split compute.
+    Its replica then holds the previous call's values; save() must take
+    every element from the device that computed it last."""
+    from cekirdekler_amd.utils import checkpoint
+
+    devs = gpu[0] + gpu[0] + gpu[0] + gpu[0]
+    cr = ck.ClNumberCruncher(devs, PART_SRC)
+    n = 1 << 16
+    it = ck.ClArray(np.zeros(1, np.int32))
+    y = ck.ClArray(np.full(n, -1.0, np.float32))
+    it.write = False
+    y.write = False
+    it.next_param(y).compute(cr, 7, "fill", n, 256)  # equal split, it = 0
+    share = [n // 3 // 256 * 256] * 4
+    share[zero_dev] = 0
+    share[(zero_dev + 1) % 4] += n - sum(share)
+    bench = [1.0] * 4
+    bench[zero_dev] = 1e9
+    cr.cores.set_state(7, share, [[0.0] * 4 for _ in range(10)], bench)
+    it.array[0] = 9
+    y.read = False
+    it.next_param(y).compute(cr, 7, "fill", n, 256)
+    assert cr.ranges(7)[zero_dev] == 0, cr.ranges(7)
+    want = (np.arange(n) % 1000).astype(np.float32) * 0.5 + 9.0
+    path = str(tmp_path / "zero.cek")
+    checkpoint.save(path, {"y": y}, cr)
+    y2 = ck.ClArray(np.zeros(n, np.float32))
+    checkpoint.load(path, {"y": y2})
+    np.testing.assert_array_equal(y2.array, want)
+    cr.dispose()
+
+
+WHERE_SRC = r"""
+__global__ void where(int* out, const int* spin) {
+  long long i = get_global_id(0);
+  unsigned x, h;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(h));
+  float v = (float)i;
+  for (int k = 0; k < spin[0]; ++k) v = v * 0.999f + 1.0f;
+  if (threadIdx.x == 0) { long long g = i / 64; out[2 * g] = (int)x; out[2 * g + 1] = (int)h + (v == -1.0f); }
+}
+"""
+
+
+@pytest.mark.parametrize("parts", [4, 8])
+def test_cu_partition_runs_on_its_own_cus(gpu, parts):
+    """a CU-partitioned logical device's work-groups run
+    on 1/parts of the CUs, on every XCD, and two partitions never share a
+    CU.  Each work-group records its XCC id and hardware id (CU / shader
+    array / engine bits) from s_getreg."""
+    devs = gpu[0:1].cu_partitions(parts)
+    ncu = gpu.device(0).compute_units
+    groups = 8192
+    seen = []
+    for p in range(parts):
+        cr = ck.ClNumberCruncher(devs[p], WHERE_SRC)
+        assert cr.error_code() == 0, cr.error_message()
+        out = ck.ClArray(np.full(2 * groups, -1, np.int32))
+        out.read = False
+        out.elements_per_group = 2
+        spin = ck.ClArray(np.array([2000], np.int32))
+        spin.write = False
+        out.next_param(spin).compute(cr, 1, "where", groups * 64, 64)
+        xcc = out.array[0::2]
+        cu = (out.array[1::2] >> 8) & 0xFF  # CU_ID / SH_ID / SE_ID bits of HW_ID
+        assert (xcc >= 0).all()
+        where = set(zip(xcc.tolist(), cu.tolist()))
+        seen.append(where)
+        assert len(set(xcc.tolist())) == 8, sorted(set(xcc.tolist()))  # every XCD
+        assert len(where) <= ncu // parts, (p, len(where))
+        cr.dispose()
+    for p in range(parts):
+        for q in range(p + 1, parts):
+            assert not (seen[p] & seen[q]), (p, q)

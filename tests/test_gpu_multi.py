@@ -205,11 +205,11 @@ def test_gemm_over_every_gpu_verified(gpus):
     g = GemmBf16(2048, 2048, 2048, devices=_all(gpus), tile="256x256pb")
     for _ in range(3):
         g.run(resident=True)
-    assert g.verify() < 5e-3
+    assert g.verify() < 1e-4
     assert all(r > 0 for r in g.cr.ranges(1)), g.cr.ranges(1)
     g.run(resident=False)
     c, ref = g.result(download=False), g.reference()
-    assert np.abs(c - ref).max() < 5e-3 * np.abs(ref).max()
+    assert np.abs(c - ref).max() < 1e-4 * np.abs(ref).max()
     g.cr.dispose()
 
 

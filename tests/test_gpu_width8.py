@@ -182,5 +182,5 @@ def test_gemm_over_8_logical_devices_verified():
         g.run(compute_id=1, resident=True)
     r = cr.ranges(1)
     assert len(r) == W and all(x > 0 for x in r) and sum(r) == g.global_range
-    assert g.verify(compute_id=1, tiles_per_device=4) < 5e-3
+    assert g.verify(compute_id=1, tiles_per_device=4) < 1e-4
     cr.dispose()

@@ -267,3 +267,67 @@ def test_round_robin_rotates_tasks(fine):
         np.testing.assert_array_equal(x.array, float(i))
     assert pool.device_task_counts() == [8, 5, 4]
     pool.dispose()
+
+
+@pytest.mark.parametrize("fine", [False, True])
+def test_round_robin_group_with_barrier_flags(fine):
+    """a serial group whose BEGIN carries a global barrier
+    (its own flag, or inherited from the previous task's SYNC_LAST) and whose
+    END carries one too must still take one rotation slot as a whole, stay in
+    order on its device, and release the rotation afterwards."""
+    cpu = ck.ClPlatforms.all().cpus(True)
+    D = 3
+    pool = ClDevicePool(ClDevicePoolType.DEVICE_ROUND_ROBIN, SRC, fine, 3)
+    pool.add_device(cpu + cpu + cpu)
+    tp = ClTaskPool()
+    before = []
+    for i in range(2):  # slots 0, 1; the second one's SYNC_LAST is inherited by the group's BEGIN
+        x, t = _task("fill", 256, float(i))
+        if i == 1:
+            t.type = ClTaskType.TASK_MESSAGE_GLOBAL_SYNCHRONIZATION_LAST
+        tp.feed(t)
+        before.append(t)
+    shared = ck.ClArray(np.zeros(128, np.float32))
+    group = []
+    for k in range(5):  # slot 2 -> device 2, as a whole
+        _, t = _task("add", 128, 1.0, shared)
+        if k == 0:
+            t.type = ClTaskType.TASK_MESSAGE_SERIAL_MODE_BEGIN | ClTaskType.TASK_MESSAGE_GLOBAL_SYNCHRONIZATION_FIRST
+        elif k == 4:
+            t.type = ClTaskType.TASK_MESSAGE_SERIAL_MODE_END | ClTaskType.TASK_MESSAGE_GLOBAL_SYNCHRONIZATION_FIRST
+        tp.feed(t)
+        group.append(t)
+    after = []
+    for i in range(4):  # slots 3.. -> devices 0, 1, 2, 0: the rotation was released
+        _, t = _task("fill", 256, 5.0)
+        tp.feed(t)
+        after.append(t)
+    pool.enqueue_task_pool(tp)
+    pool.finish()
+    assert [t.device_index for t in before] == [0, 1]
+    assert {t.device_index for t in group} == {2}
+    np.testing.assert_array_equal(shared.array, 5.0)
+    assert [t.device_index for t in after] == [i % D for i in range(3, 7)]
+    pool.dispose()
+
+
+def test_task_with_kernel_list():
+    """ClTask kernels given as a list of names (accepted by
+    the cruncher's name splitter) also go through the pool's template key."""
+    cpu = ck.ClPlatforms.all().cpus(True)
+    pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, False, 2)
+    pool.add_device(cpu + cpu)
+    tp = ClTaskPool()
+    arrays = []
+    for i in range(4):
+        x = ck.ClArray(np.zeros(256, np.float32))
+        v = ck.ClArray(np.array([float(i)], np.float32))
+        v.write = False
+        t = x.next_param(v).task(1, ["fill", "add"], 256, 64)
+        tp.feed(t)
+        arrays.append(x)
+    pool.enqueue_task_pool(tp)
+    pool.finish()
+    for i, x in enumerate(arrays):
+        np.testing.assert_array_equal(x.array, 2.0 * i)
+    pool.dispose()

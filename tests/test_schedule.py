@@ -104,3 +104,54 @@ def test_explicit_blob_bounds_validated():
     with pytest.raises(Exception):
         x.next_param(y).compute(cr, 1, "k", 256, 64, 0, True, ck.PIPELINE_EVENT, [0, 100, 256])
     cr.dispose()
+
+
+@pytest.mark.parametrize("hwq,want", [("4", 4), ("2", 2), ("", 4), ("64", 16)])
+def test_queue_concurrency_follows_hw_queues(monkeypatch, hwq, want):
+    """the default async / driver-pipeline queue count is
+    the GPU's hardware queue count (GPU_MAX_HW_QUEUES, 4 by default), and the
+    driver pipeline maps blob k to queue k mod that count."""
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", hwq)
+    cpu = ck.ClPlatforms.all().cpus(True)
+    cr = ck.ClNumberCruncher(cpu, SRC)
+    assert cr.compute_queue_concurrency == want
+    cr.dispose()
+    blobs = 8
+    sched = _record(cpu, ck.PIPELINE_DRIVER, blobs)
+    kern = [o for o in sched if o[1] == "kernel"]
+    assert len(kern) == blobs  # one kernel op per blob
+    assert [o[2] for o in kern] == [1 + (k % want) for k in range(len(kern))]
+    assert check_pipeline_schedule(sched) == len(kern)
+    # an explicit count still wins
+    cr = ck.ClNumberCruncher(cpu, SRC, queue_concurrency=16)
+    assert cr.compute_queue_concurrency == 16
+    cr.dispose()
+
+
+@pytest.mark.parametrize("reads_main", [True, False])
+def test_explicit_blobs_order_every_earlier_upload(reads_main):
+    """with explicit blobs, blob q's kernels may read
+    panels uploaded by earlier blobs of the other half-pipeline.  Whatever
+    the read-stream setting, every blob's kernels are ordered after every
+    earlier blob's uploads."""
+    src = """__global__ void k(const float* x, const float* w, float* y) {
+      long long i = get_global_id(0); y[i] = x[i] * 2.0f + w[i % 64]; }"""
+    cpu = ck.ClPlatforms.all().cpus(True)
+    cr = ck.ClNumberCruncher(cpu, src)
+    cr.cores.record_schedule = True
+    cr.cores.pipeline_reads_on_main_stream = reads_main
+    bounds = [0, 64, 256, 576, 1024]
+    n = bounds[-1]
+    x = ck.ClArray(np.arange(n, dtype=np.float32))
+    x.partial_read = True
+    x.write = False
+    w = ck.ClArray(np.arange(256, dtype=np.float32))
+    w.partial_read = True
+    w.write = False
+    w.blob_slices = [(64 * k, 64) for k in range(4)]
+    y = ck.ClArray(np.zeros(n, np.float32))
+    y.read = False
+    x.next_param(w, y).compute(cr, 1, "k", n, 64, 0, True, ck.PIPELINE_EVENT, bounds)
+    np.testing.assert_array_equal(y.array, 2 * x.array + w.array[np.arange(n) % 64])
+    assert check_pipeline_schedule(cr.cores.schedule(), prefix_uploads=True) == 4
+    cr.dispose()
