@@ -621,10 +621,13 @@ def write_detail(full: dict, world: int, path=None, gpu: bool = True) -> str:
 
 
 def _r(x, nd=3):
-    """Round a number for the summary line (None and non-numbers pass)."""
-    if isinstance(x, bool) or not isinstance(x, (int, float)):
+    """Round a number for the summary line: ints and non-numbers pass, small
+    magnitudes (errors) keep 3 significant digits."""
+    if isinstance(x, (bool, int)) or not isinstance(x, float):
         return x
-    return round(float(x), nd)
+    if x != 0 and abs(x) < 0.1:
+        return float(f"{x:.3g}")
+    return round(x, nd)
 
 
 def _pick(d, keys, nd=3):

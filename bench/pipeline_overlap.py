@@ -15,9 +15,9 @@ exactly that case and runs it through ``compute()`` three ways:
 
 The kernel is a user kernel string (hiprtc), one uint32 in and one out per
 work item, with ``iters`` LCG steps per element.  ``iters`` is calibrated at
-start so the kernel alone takes as long as the mean of the upload alone and
-the download alone (each measured through ``compute()`` with the other
-transfer switched off).  Every timed call's output is checked EXACTLY
+start so the kernel alone takes as long as the mean of the upload and the
+download (the upload timed alone through ``compute()``, the download as the
+difference of upload + download and upload alone).  Every timed call's output is checked EXACTLY
 against the closed form of the iterated LCG (``v -> a^n v + c(a^n-1)/(a-1)``
 mod 2^32), so no mode can skip work.
 
@@ -110,16 +110,19 @@ def main():
         sync()
         return (time.perf_counter() - t) * 1e3 / calls
 
-    # ---- calibration: upload alone, download alone, kernel per LCG step ----
+    # ---- calibration: upload alone, upload + download, kernel per LCG step ----
+    # (the download's share is the difference of the first two, both through
+    # the same 3-phase path the baseline config runs)
     id_up, id_down, id_k = next(cid), next(cid), next(cid)
     it.array[0] = 0
     y.write = False
     call(cr, id_up)  # first upload also creates the buffers
     up_ms = statistics.median(med_ms(lambda: call(cr, id_up), 3) for _ in range(3))
-    x.read = False  # x stays on the device; only y comes down
     y.write = True
     call(cr, id_down)
-    down_ms = statistics.median(med_ms(lambda: call(cr, id_down), 3) for _ in range(3))
+    both_ms = statistics.median(med_ms(lambda: call(cr, id_down), 3) for _ in range(3))
+    down_ms = max(0.0, both_ms - up_ms)
+    x.read = x.partial_read = False  # x stays on the device (a partial read uploads whatever .read says)
     y.write = False
     probe = 256
     it.array[0] = probe
@@ -131,7 +134,7 @@ def main():
     iters = a.iters or max(1, int(round(((up_ms + down_ms) / 2 - zero_ms) / per_step)))
     it.array[0] = iters
     kernel_ms = statistics.median(med_ms(lambda: call(cr, id_k), 3) for _ in range(3))
-    x.read = True
+    x.read = x.partial_read = True
     y.write = True
     want = expected(x.array, iters)
 
@@ -146,7 +149,7 @@ def main():
     ids = {name: next(cid) for name, _, _ in configs}
     times = {name: [] for name, _, _ in configs}
     exact = {name: True for name, _, _ in configs}
-    piped = {}
+    piped, moved = {}, {}
 
     def run(name, fn, layout):
         c = crs["q16"] if layout else None
@@ -163,7 +166,9 @@ def main():
         run(name, fn, layout)
         exact[name] &= bool(np.array_equal(y.array, want))
         c = crs["q16"] if ("q16" in name or layout) else crs["q4"]
-        piped[name] = bool(c.last_record()["pipelined"])
+        rec = c.last_record()
+        piped[name] = bool(rec["pipelined"])
+        moved[name] = [int(rec["h2d_bytes"]), int(rec["d2h_bytes"])]
     for _ in range(a.rounds):
         for name, fn, layout in configs:
             y.array[:] = 0
@@ -183,6 +188,9 @@ def main():
         "ideal_speedup_sum_over_max": round(sum(parts) / max(parts), 3),
         "ms": res,
         "pipelined": piped,
+        # H2D / D2H bytes of one call per config: every config moves the same data
+        "same_bytes_every_config": len({tuple(v) for v in moved.values()}) == 1,
+        "h2d_d2h_bytes_per_call": moved.get("3phase"),
         "outputs_exact": all(exact.values()),
         "best_event": ev, "best_event_4streams": ev4, "best_driver_q4": dq4, "best_driver_q16": dq16,
         "pipeline_speedup_event": round(base / min(res[ev], res[ev4]), 3),

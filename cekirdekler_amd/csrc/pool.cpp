@@ -207,6 +207,7 @@ void DevicePool::consumer(int dev) {
   const bool async = max_in_flight_ > 1;
   if (async) cr.fine_grained = true;  // a marker word after every compute
   std::vector<Inflight> inflight;
+  int idle_polls = 0;
   for (;;) {
     if (!inflight.empty()) retire(dev, inflight);
     Item it;
@@ -235,9 +236,15 @@ void DevicePool::consumer(int dev) {
       continue;
     }
     if (!got) {  // only in-flight tasks: poll their marker words
-      std::this_thread::sleep_for(std::chrono::microseconds(10));
+      // a short yielding spin first: a sleep, however short it is asked to
+      // be, costs tens of µs on Linux, longer than many tasks
+      if (++idle_polls < 64)
+        std::this_thread::yield();
+      else
+        std::this_thread::sleep_for(std::chrono::microseconds(10));
       continue;
     }
+    idle_polls = 0;
     const double t0 = now_ms();
     const PoolTask& t = it.task;
     if (t.call.kernels.empty()) {  // a pure barrier / message task

@@ -128,6 +128,8 @@ Worker::Worker(const DeviceInfo& dev, std::shared_ptr<Program> prog, int queue_c
     bool pinned = false;
     marker_words_ = static_cast<uint64_t*>(host_alloc(32 * sizeof(uint64_t), 4096, &pinned));
     std::memset(marker_words_, 0, 32 * sizeof(uint64_t));
+    // one lookup here instead of a runtime call (under HIP's lock) per marker
+    marker_dev_ = static_cast<uint64_t*>(host_device_ptr(marker_words_));
   } else {
     pool_.reset(new CpuPool(dev_.cpu_threads > 0 ? dev_.cpu_threads : 1));
   }
@@ -380,6 +382,11 @@ hipStream_t Worker::main_stream() {
 
 hipStream_t Worker::compute_stream(int i) {
   if (!gpu()) return nullptr;
+  // one queue: the main stream itself.  A separate stream would cost a
+  // hardware queue more for no concurrency — and a CU-masked stream (a
+  // partitioned device) owns a hardware queue of its own, so 8 partitions
+  // x 2 streams oversubscribe the GPU's queue slots
+  if (qconc_ == 1) return main_stream();
   i %= 16;
   if (!cq_[i]) cq_[i] = new_stream(false);
   return cq_[i];
@@ -691,7 +698,7 @@ void Worker::add_marker(hipStream_t s) {
   uint64_t v = ++marker_issued_per_slot_[slot];
   last_slot_ = slot;
   last_value_ = v;
-  CEK_HIP(hipStreamWriteValue64(s, host_device_ptr(&marker_words_[slot]), v, 0));
+  CEK_HIP(hipStreamWriteValue64(s, marker_dev_ + slot, v, 0));
 }
 
 uint64_t Worker::marker_word(int slot) const {

@@ -242,6 +242,7 @@ class Worker {
 
   // markers: one 64-bit word per stream slot in pinned host memory
   uint64_t* marker_words_ = nullptr;
+  uint64_t* marker_dev_ = nullptr;  // device address of marker_words_ (looked up once)
   std::vector<uint64_t> marker_issued_per_slot_;
   long long markers_issued_ = 0;
   int last_slot_ = -1;

@@ -7,12 +7,21 @@ to a :class:`ClTaskPool` (FIFO); pools are enqueued into a
 :class:`ClDevicePool`, whose scheduler is native (``cek.DevicePool``,
 ``csrc/pool.cpp``): one C++ consumer thread per device takes the next task
 the moment its device has room ("compute at will", the reference's greedy
-default), with no Python and no GIL per task.  Each device keeps up to
-``max_queues_per_device`` tasks in flight on its own HIP streams (enqueue
-mode + round-robin queues) and retires them through stream-written marker
-words (``hipStreamWriteValue64``), the µs-cheap counterpart of the
-reference's 150–300 µs marker callbacks (Cores.cs:447).  User callbacks run
-on a dispatcher thread as completions arrive.
+default), with no Python and no GIL per task.  With fine-grained queue
+control each device keeps several tasks in flight — the reference's
+adaptive per-device limit (N/10 … N/50 tasks over the devices, at most 16,
+ClPipeline.cs:4178-4236) — spread over ``max_queues_per_device`` HIP
+streams (enqueue mode + round-robin queues), and retires them through
+stream-written marker words (``hipStreamWriteValue64``), the µs-cheap
+counterpart of the reference's 150–300 µs marker callbacks (Cores.cs:447).
+The in-flight depth is not tied to the stream count: tasks queued in order
+on one stream still keep the device busy while the host prepares the next.
+A CU-partitioned device (``ClDevices.cu_partitions``) gets one stream: each
+CU-masked stream owns a hardware queue, and 8 partitions × several streams
+oversubscribe the GPU's queue slots (measured: 4096 one-work-group tasks
+over 8 partitions ran at 38 k tasks/s with 4 streams per partition against
+95 k with one; profiles/r5/task_pool_partitions.md).  User callbacks run on
+a dispatcher thread as completions arrive.
 
 Task type flags (ClTaskType, :3247-3321): DEVICE_SELECT_BEGIN/END and
 SERIAL_MODE_BEGIN/END pin a group of tasks to one device (in order),
@@ -198,6 +207,9 @@ class ClDevicePool:
         self.kernel_source = kernel_source
         self.prebuilt = prebuilt
         self.max_queues = max(1, min(16, int(max_queues_per_device))) if fine_grained_queue_control else 1
+        # tasks in flight per device: the adaptive limit decides, up to 16
+        # (without fine-grained control: one at a time, synchronously)
+        self.max_in_flight = 16 if fine_grained_queue_control else 1
         self.crunchers: List[ClNumberCruncher] = []
         self._native = None
         self._counts_base: List[int] = []
@@ -213,8 +225,9 @@ class ClDevicePool:
     def add_device(self, devices: ClDevices) -> None:
         """Adds each device (the same device may be added several times)."""
         for i in range(len(devices)):
+            part = devices.device(i).cu_partition is not None
             cr = ClNumberCruncher(devices[i], self.kernel_source, prebuilt=self.prebuilt,
-                                  queue_concurrency=max(1, self.max_queues))
+                                  queue_concurrency=1 if part else max(1, self.max_queues))
             if cr.error_code():
                 raise RuntimeError(cr.error_message())
             self.crunchers.append(cr)
@@ -230,7 +243,7 @@ class ClDevicePool:
                 counts[i] = c
             self._native.close()
         self._counts_base = counts
-        self._native = cek.DevicePool([c.cores for c in self.crunchers], self.max_queues, int(self.pool_type))
+        self._native = cek.DevicePool([c.cores for c in self.crunchers], self.max_in_flight, int(self.pool_type))
         if self._dispatcher is None:
             self._dispatcher = threading.Thread(target=self._dispatch_loop, daemon=True)
             self._dispatcher.start()
@@ -362,7 +375,7 @@ class ClDevicePool:
     def queue_limit(self) -> int:
         """Current per-device queue-depth limit: follows the head pool's
         progress (N/10 → N/20 → N/33 → N/50 → 2 → 1 tasks, over the device
-        count, within ``max_queues_per_device``)."""
+        count, at most 16)."""
         return int(self._native.queue_limit()) if self._native is not None else 0
 
     def queue_limit_history(self) -> List[int]:
