@@ -12,6 +12,7 @@
 #include "jit.h"
 #include "memory.h"
 #include "pool.h"
+#include "probe.h"
 #include "xgmi.h"
 
 namespace py = pybind11;
@@ -345,6 +346,23 @@ PYBIND11_MODULE(_cek, m) {
       .def("allreduce_sum_f32", [](RcclComm& c, uint64_t p, uint64_t n, uint64_t stream) {
         c.allreduce_sum_f32(reinterpret_cast<void*>(p), n, reinterpret_cast<hipStream_t>(stream));
       }, py::call_guard<py::gil_scoped_release>());
+
+  m.def("launch_rate_probe", [](int ordinal, const std::string& co, const std::string& kernel, int threads,
+                                int launches) {
+        LaunchRate r;
+        {
+          py::gil_scoped_release rel;
+          r = launch_rate_probe(ordinal, co, kernel, threads, launches);
+        }
+        py::dict d;
+        d["threads"] = r.threads;
+        d["launches_per_thread"] = r.launches;
+        d["host_ms"] = r.host_ms;
+        d["drain_ms"] = r.drain_ms;
+        d["launches_per_s"] = r.launches_per_s;
+        d["per_thread_ms"] = r.per_thread_ms;
+        return d;
+      }, py::arg("ordinal"), py::arg("code_object"), py::arg("kernel"), py::arg("threads"), py::arg("launches"));
 
   m.def("allgatherv_plan", [](int rank, int world, const std::vector<uint64_t>& offsets,
                               const std::vector<uint64_t>& sizes) {

@@ -457,6 +457,37 @@ class GemmBf16:
             worst = max(worst, float(np.abs(c[r:r + 256, q:q + 256] - ref).max() / max(np.abs(ref).max(), 1e-30)))
         return worst
 
+    def verify_shells_full(self, panels: int = 8, device=None) -> tuple:
+        """Every element of :meth:`shells_result` against a float64 product
+        computed by torch on ``device``: ``(max_rel_err, blocks_checked)``,
+        the error per BM×BN block relative to that block's ``max |ref|``."""
+        import torch
+
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else (
+                torch.device("cpu"))
+        c = torch.from_numpy(self.shells_result(panels)).to(device)
+        ref = self._reference_t(device)
+        ntm, ntn = self.M // self.BM, self.N // self.BN
+        got = c.view(ntm, self.BM, ntn, self.BN).double()
+        want = ref.view(ntm, self.BM, ntn, self.BN)
+        err = (got - want).abs().amax(dim=(1, 3)) / want.abs().amax(dim=(1, 3)).clamp_min(1e-30)
+        return float(err.max()), ntm * ntn
+
+    def _reference_t(self, device):
+        """C = A·Bᵀ in float64 on a torch device (row-major [M][N])."""
+        import torch
+
+        def operand(arr, rows):
+            x = arr.array
+            if x.dtype == np.uint16:  # bf16 bit patterns
+                t = torch.from_numpy(x.view(np.int16)).to(device).view(torch.bfloat16)
+            else:
+                t = torch.from_numpy(x).to(device)
+            return t.reshape(rows, self.K).double()
+
+        return operand(self.A, self.M) @ operand(self.B, self.N).T
+
     def result(self, download: bool = True) -> np.ndarray:
         """Row-major fp32 C (downloads every device's slice when resident)."""
         if download:
@@ -549,18 +580,9 @@ class GemmBf16:
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else (
                 torch.device("cpu"))
-        M, N, K, BM, BN = self.M, self.N, self.K, self.BM, self.BN
+        M, N, BM, BN = self.M, self.N, self.BM, self.BN
         ntm, ntn = M // BM, N // BN
-
-        def operand(arr, rows):
-            x = arr.array
-            if x.dtype == np.uint16:  # bf16 bit patterns
-                t = torch.from_numpy(x.view(np.int16)).to(device).view(torch.bfloat16)
-            else:
-                t = torch.from_numpy(x).to(device)
-            return t.reshape(rows, K).double()
-
-        ref = operand(self.A, M) @ operand(self.B, N).T  # [M][N] float64
+        ref = self._reference_t(device)  # [M][N] float64
         ref_tiles = ref.view(ntm, BM, ntn, BN).permute(0, 2, 1, 3)  # [ntm][ntn][BM][BN]
         del ref
         ranges = self.cr.ranges(compute_id)

@@ -123,3 +123,30 @@ def test_verify_full_checks_every_tile(cls, tile):
     err, _ = g.verify_full(1, host=True, device="cpu")
     assert err > 1e-4
     cr.dispose()
+
+
+def test_verify_shells_full_checks_every_block(cpu_cr):
+    """The native shell stream's host C (shell layout) checked whole."""
+    from cekirdekler_amd.ops.gemm import rows_to_tile, untile  # noqa: F401
+
+    g = GemmBf16(1024, 1024, 256, cruncher=cpu_cr, tile="256x256pb", group_m=2)
+    P = 2
+    ref = g.reference().astype(np.float32)
+    pm, pn = g.M // P, g.N // P
+    parts = []
+    for s in range(P):  # R_s then C_s, each tile-major in grouped order
+        for rows, cols in (((s * pm, (s + 1) * pm), (0, (s + 1) * pn)),
+                           ((0, s * pm), (s * pn, (s + 1) * pn))):
+            m, n = rows[1] - rows[0], cols[1] - cols[0]
+            if m == 0:
+                continue
+            blk = ref[rows[0]:rows[1], cols[0]:cols[1]]
+            tm, tn = tile_coords(np.arange((m // 256) * (n // 256)), m, n, 256, 256, g.group_m)
+            tiles = np.stack([blk[r * 256:(r + 1) * 256, c * 256:(c + 1) * 256] for r, c in zip(tm, tn)])
+            parts.append(rows_to_tile(tiles, g.geom).ravel())
+    g.C.array[:] = np.concatenate(parts)
+    np.testing.assert_array_equal(g.shells_result(P), ref)
+    err, blocks = g.verify_shells_full(P, device="cpu")
+    assert blocks == 16 and err < 1e-6
+    g.C.array[5] += 1.0
+    assert g.verify_shells_full(P, device="cpu")[0] > 1e-4

@@ -1,18 +1,22 @@
 """Where the device pool's host time per task goes.
 
-Dispatch rate of ClDevicePool on tiny tasks (one 256-thread work-group
-each), for D logical devices of GPU 0, whole-GPU or CU-partitioned, with 1
-or 3 queues per device.  Then the raw launch rate of the same kernel from D
-host threads, each on its own cruncher in enqueue mode (no pool, no markers):
-if that rate also falls as D grows on one GPU, the cost is the HIP runtime
-serialising launches to one device, not the pool's hand-off.
+Three measurements on GPU 0:
+
+* ``hip_launch_threads``: raw HIP launch rate from T native threads, each on
+  its own stream of the one device (``cek.launch_rate_probe``: no runtime,
+  no pool, no sync) — the ceiling any fan-out over logical devices of one
+  GPU can reach;
+* ``fanout_us_per_compute``: host µs per enqueue-mode compute() of one
+  cruncher over D logical devices (worker hand-off + D launches);
+* ``pool``: ClDevicePool dispatch rate on tiny tasks (one 256-thread
+  work-group each) for D logical devices, whole-GPU or CU-partitioned, with
+  1 or 3 queues per device.
 
     python tools/pool_dispatch_probe.py > gpurun_out/pool_dispatch.json
 """
 import json
 import os
 import sys
-import threading
 import time
 
 import numpy as np
@@ -66,51 +70,45 @@ def pool_rate(d, part, queues):
     return round(rate)
 
 
-def raw_rate(d, part):
-    """D host threads, each launching TASKS/D computes on its own
-    single-device cruncher in enqueue mode (one drain at the end)."""
-    devs = devices(d, part)
-    crs = [ck.ClNumberCruncher(devs[i], SRC, queue_concurrency=1) for i in range(d)]
+def fanout_us(d, calls=400):
+    """One cruncher over D logical devices of GPU 0, enqueue mode: host µs
+    per compute() of a tiny kernel split over the D devices (the runtime's
+    worker hand-off plus D launches)."""
+    cr = ck.ClNumberCruncher(devices(d, 0), SRC)
     v = ck.ClArray(np.array([1.0], np.float32))
+    x = ck.ClArray(np.zeros(256 * d, np.float32))
     v.write = False
-    xs = [ck.ClArray(np.zeros(256, np.float32)) for _ in range(d)]
-    for i, cr in enumerate(crs):
-        xs[i].read = xs[i].write = False
-        cr.upload(v)
-        cr.upload(xs[i])
-    v.read = False
-    for i, cr in enumerate(crs):
-        xs[i].next_param(v).compute(cr, 1, "add", 256, 256)
-    per = TASKS // d
-    barrier = threading.Barrier(d + 1)
-
-    def run(i):
-        cr, x = crs[i], xs[i]
-        barrier.wait()
-        cr.enqueue_mode = True
-        for _ in range(per):
-            x.next_param(v).compute(cr, 1, "add", 256, 256)
-        cr.enqueue_mode = False
-
-    th = [threading.Thread(target=run, args=(i,)) for i in range(d)]
-    for t in th:
-        t.start()
-    barrier.wait()
+    x.write = False
+    x.next_param(v).compute(cr, 1, "add", 256 * d, 256)
+    v.read = x.read = False
+    cr.enqueue_mode = True
+    for _ in range(50):
+        x.next_param(v).compute(cr, 1, "add", 256 * d, 256)
+    cr.enqueue_mode = False
+    cr.enqueue_mode = True
     t0 = time.perf_counter()
-    for t in th:
-        t.join()
-    rate = per * d / (time.perf_counter() - t0)
-    for cr in crs:
-        cr.dispose()
-    return round(rate)
+    for _ in range(calls):
+        x.next_param(v).compute(cr, 1, "add", 256 * d, 256)
+    host = (time.perf_counter() - t0) * 1e6 / calls
+    cr.enqueue_mode = False
+    cr.dispose()
+    return round(host, 2)
 
 
-out = {"tasks": TASKS, "pool": {}, "raw_threads": {}}
+from cekirdekler_amd._native import cek  # noqa: E402
+from cekirdekler_amd.ops.library import code_object  # noqa: E402
+
+out = {"tasks": TASKS, "pool": {}, "hip_launch_threads": {}, "fanout_us_per_compute": {}}
+for t in (1, 2, 4, 8):
+    r = cek.launch_rate_probe(0, code_object("stream"), "cek_copy_u8", t, 4000)
+    out["hip_launch_threads"][f"t{t}"] = {"launches_per_s": round(r["launches_per_s"]),
+                                          "us_per_launch_per_thread": round(1e3 * r["host_ms"] / 4000, 3)}
+for d in (1, 2, 4, 8):
+    out["fanout_us_per_compute"][f"d{d}"] = fanout_us(d)
 for d in (1, 2, 4, 8):
     for part in (0, 1):
         if d == 1 and part:
             continue
         for q in (1, 3):
             out["pool"][f"d{d}_part{part}_q{q}"] = pool_rate(d, part, q)
-        out["raw_threads"][f"d{d}_part{part}"] = raw_rate(d, part)
 print(json.dumps(out), flush=True)
