@@ -1157,6 +1157,15 @@ static bool writes_host_memory(const ComputeCall& c) {
   return std::any_of(c.arrays.begin(), c.arrays.end(), [](const ArraySpec& a) { return a.zc && !a.ro; });
 }
 
+// A marker after this compute must release host-memory writes (system
+// scope): kernels stored into zero-copy memory, or results were downloaded
+// (a blit-kernel D2H into hipHostMalloc pages is a kernel store to host
+// memory).  Device-resident computes get a fence-less marker.
+static bool marker_needs_release(const ComputeCall& c) {
+  return std::any_of(c.arrays.begin(), c.arrays.end(),
+                     [](const ArraySpec& a) { return (a.zc && !a.ro) || (!a.zc && (a.write || a.write_all)); });
+}
+
 void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref, long long range,
                        uint64_t* h2d, uint64_t* d2h) {
   hipStream_t s = nullptr;
@@ -1253,7 +1262,7 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
   }
   span_end(wk, s);
   if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(s);
-  if (fine_grained) wk.add_marker(s);
+  if (fine_grained) wk.add_marker(s, marker_needs_release(c));
   if (!enqueue_mode_ && wk.gpu()) wk.wait_stream(s, sleep_waits);
 }
 
@@ -1407,7 +1416,7 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
   }
   span_end(wk, m);
   if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(m);
-  if (fine_grained) wk.add_marker(m);
+  if (fine_grained) wk.add_marker(m, marker_needs_release(c));
   if (wk.gpu()) wk.wait_stream(m, sleep_waits);
 }
 
@@ -1477,7 +1486,7 @@ void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long
   }
   span_end(wk, m);
   if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(m);
-  if (fine_grained) wk.add_marker(m);
+  if (fine_grained) wk.add_marker(m, marker_needs_release(c));
   if (wk.gpu()) wk.wait_stream(m, sleep_waits);
 }
 

@@ -272,7 +272,7 @@ class Cores {
   long long markers_reached();
   long long markers_issued();
   std::pair<int, uint64_t> last_marker(int dev) const { return workers_.at(dev)->last_marker(); }
-  uint64_t marker_word(int dev, int slot) const { return workers_.at(dev)->marker_word(slot); }
+  uint64_t marker_word(int dev, int slot) { return workers_.at(dev)->marker_word(slot); }
   void finish();  // synchronise every stream of every device
   void release_array(uint64_t uid);
   uint64_t device_bytes(int i) const { return workers_.at(i)->bytes_allocated(); }

@@ -207,9 +207,9 @@ void DevicePool::consumer(int dev) {
   const bool async = max_in_flight_ > 1;
   if (async) cr.fine_grained = true;  // a marker word after every compute
   std::vector<Inflight> inflight;
-  int idle_polls = 0;
+  double last_progress = now_ms();
   for (;;) {
-    if (!inflight.empty()) retire(dev, inflight);
+    if (!inflight.empty() && retire(dev, inflight) > 0) last_progress = now_ms();
     Item it;
     bool got = false, idle = false, stop = false;
     {
@@ -235,16 +235,20 @@ void DevicePool::consumer(int dev) {
       work_cv_.wait_for(lk, std::chrono::milliseconds(5));
       continue;
     }
-    if (!got) {  // only in-flight tasks: poll their marker words
-      // a short yielding spin first: a sleep, however short it is asked to
-      // be, costs tens of µs on Linux, longer than many tasks
-      if (++idle_polls < 64)
+    if (!got) {  // only in-flight tasks: poll their markers
+      // yield-spin while tasks keep retiring: a sleep, however short it is
+      // asked to be, costs ~60 µs on Linux — longer than most tasks on a
+      // partition, and a late retirement leaves the device idle (median
+      // 40-60 µs gaps between a queue's kernels in a rocprofv3 trace of the
+      // 256-task pool, profiles/r5/README.md).  Only after 2 ms without a
+      // retirement does the consumer fall back to short sleeps.
+      if (now_ms() - last_progress < 2.0)
         std::this_thread::yield();
       else
         std::this_thread::sleep_for(std::chrono::microseconds(10));
       continue;
     }
-    idle_polls = 0;
+    last_progress = now_ms();
     const double t0 = now_ms();
     const PoolTask& t = it.task;
     if (t.call.kernels.empty()) {  // a pure barrier / message task

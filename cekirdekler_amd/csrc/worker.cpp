@@ -122,6 +122,8 @@ Worker::Worker(const DeviceInfo& dev, std::shared_ptr<Program> prog, int queue_c
       no_pipelining_(no_pipelining) {
   cq_.assign(16, nullptr);
   marker_issued_per_slot_.assign(32, 0);
+  rings_.resize(32);
+  if (const char* e = std::getenv("CEK_MARKERS")) write_value_markers_ = std::string(e) == "writevalue";
   if (gpu()) {
     set_device();
     apply_sync_mode(dev_.ordinal);
@@ -164,6 +166,11 @@ Worker::~Worker() {
       for (auto s : h)
         if (s) (void)hipStreamDestroy(s);
     host_free(marker_words_);
+    for (auto& r : rings_) {
+      for (auto& e : r.pending) (void)hipEventDestroy(e.first);
+      for (auto e : r.spare) (void)hipEventDestroy(e);
+      for (auto e : r.spare_fenced) (void)hipEventDestroy(e);
+    }
   }
 }
 
@@ -687,7 +694,7 @@ int Worker::device_enqueue_errors() {
   return total;
 }
 
-void Worker::add_marker(hipStream_t s) {
+void Worker::add_marker(hipStream_t s, bool release) {
   ++markers_issued_;
   if (!gpu()) {
     last_slot_ = -1;
@@ -698,18 +705,52 @@ void Worker::add_marker(hipStream_t s) {
   uint64_t v = ++marker_issued_per_slot_[slot];
   last_slot_ = slot;
   last_value_ = v;
-  CEK_HIP(hipStreamWriteValue64(s, marker_dev_ + slot, v, 0));
+  if (write_value_markers_) {
+    CEK_HIP(hipStreamWriteValue64(s, marker_dev_ + slot, v, 0));
+    return;
+  }
+  std::lock_guard<std::mutex> g(marker_mu_);
+  MarkerRing& r = rings_[slot];
+  auto& spare = release ? r.spare_fenced : r.spare;
+  hipEvent_t e = nullptr;
+  if (!spare.empty()) {
+    e = spare.front();
+    spare.pop_front();
+  } else {
+    set_device();
+    // no timing; no system-scope release unless host memory was written: a
+    // completion signal only
+    CEK_HIP(hipEventCreateWithFlags(&e, release ? hipEventDisableTiming
+                                                : (hipEventDisableTiming | hipEventDisableSystemFence)));
+  }
+  CEK_HIP(hipEventRecord(e, s));
+  r.pending.emplace_back(e, release);
 }
 
-uint64_t Worker::marker_word(int slot) const {
+uint64_t Worker::marker_word(int slot) {
   if (!gpu() || slot < 0) return static_cast<uint64_t>(markers_issued_);
-  return __atomic_load_n(&marker_words_[slot], __ATOMIC_ACQUIRE);
+  if (write_value_markers_) return __atomic_load_n(&marker_words_[slot], __ATOMIC_ACQUIRE);
+  std::lock_guard<std::mutex> g(marker_mu_);
+  MarkerRing& r = rings_[slot];
+  while (!r.pending.empty()) {
+    const auto front = r.pending.front();
+    const hipError_t q = hipEventQuery(front.first);
+    if (q == hipErrorNotReady) break;
+    if (q != hipSuccess) {
+      (void)hipGetLastError();
+      throw Error("marker event query failed on " + dev_.name);
+    }
+    (front.second ? r.spare_fenced : r.spare).push_back(front.first);
+    r.pending.pop_front();
+    ++r.done;
+  }
+  return r.done;
 }
 
 long long Worker::markers_reached() {
   if (!gpu()) return markers_issued_;
   long long r = 0;
-  for (int i = 0; i < 32; ++i) r += static_cast<long long>(__atomic_load_n(&marker_words_[i], __ATOMIC_ACQUIRE));
+  for (int i = 0; i < 32; ++i) r += static_cast<long long>(marker_word(i));
   return r;
 }
 

@@ -168,12 +168,14 @@ class Worker {
   int device_enqueue_errors();
 
   // --- markers (fine-grained queue control, ClCommandQueue.cs:103-112) ---
-  void add_marker(hipStream_t s);
+  // release: the marker also makes earlier writes to HOST memory visible
+  // (a system-scope release; set when the compute downloaded results)
+  void add_marker(hipStream_t s, bool release = false);
   long long markers_reached();
   // (slot, value) of the newest marker; a marker is reached once
   // marker_word(slot) >= value.  CPU device: slot -1 (always reached).
   std::pair<int, uint64_t> last_marker() const { return {last_slot_, last_value_}; }
-  uint64_t marker_word(int slot) const;
+  uint64_t marker_word(int slot);
   long long markers_issued() const { return markers_issued_; }
 
   // --- user-event gating (ClUserEvent.cs:102-117) -------------------------
@@ -244,6 +246,20 @@ class Worker {
   uint64_t* marker_words_ = nullptr;
   uint64_t* marker_dev_ = nullptr;  // device address of marker_words_ (looked up once)
   std::vector<uint64_t> marker_issued_per_slot_;
+  // Event markers (the default): per stream slot, the recorded events not
+  // yet seen complete (in issue order: a stream completes them in order),
+  // spare events, and how many have completed.  A marker is a barrier packet
+  // with a completion signal; hipStreamWriteValue64 runs as a blit kernel
+  // (__amd_rocclr_streamOpsWrite) — a kernel dispatch per marker, ~10× the
+  // host cost under 8 submitting threads (profiles/r5/task_pool_partitions.md).
+  struct MarkerRing {
+    std::deque<std::pair<hipEvent_t, bool>> pending;  // (event, system-scope release)
+    std::deque<hipEvent_t> spare, spare_fenced;
+    uint64_t done = 0;
+  };
+  std::vector<MarkerRing> rings_;
+  std::mutex marker_mu_;
+  bool write_value_markers_ = false;  // CEK_MARKERS=writevalue: the old path
   long long markers_issued_ = 0;
   int last_slot_ = -1;
   uint64_t last_value_ = 0;

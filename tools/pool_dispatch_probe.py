@@ -70,11 +70,14 @@ def pool_rate(d, part, queues):
     return round(rate)
 
 
-def fanout_us(d, calls=400):
+def fanout_us(d, calls=400, spans=True):
     """One cruncher over D logical devices of GPU 0, enqueue mode: host µs
     per compute() of a tiny kernel split over the D devices (the runtime's
-    worker hand-off plus D launches)."""
+    worker hand-off plus D launches).  Logical devices of one GPU record a
+    begin/end event pair per compute and device (``spans``); distinct GPUs
+    record one span per enqueued batch, so ``spans=False`` is their case."""
     cr = ck.ClNumberCruncher(devices(d, 0), SRC)
+    cr.cores.device_spans = spans
     v = ck.ClArray(np.array([1.0], np.float32))
     x = ck.ClArray(np.zeros(256 * d, np.float32))
     v.write = False
@@ -105,6 +108,7 @@ for t in (1, 2, 4, 8):
                                           "us_per_launch_per_thread": round(1e3 * r["host_ms"] / 4000, 3)}
 for d in (1, 2, 4, 8):
     out["fanout_us_per_compute"][f"d{d}"] = fanout_us(d)
+    out["fanout_us_per_compute"][f"d{d}_no_spans"] = fanout_us(d, spans=False)
 for d in (1, 2, 4, 8):
     for part in (0, 1):
         if d == 1 and part:
