@@ -509,47 +509,3 @@ extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8u_f32(const 
                                                                         int2* out, CEK_HIDDEN) {
   mandel_blk8m<32, 32, true, true>(view, size, out, __cek_off);
 }
-
-// blk8u with P blocks per wave ("blk8v": 2, "blk8w": 4), assigned
-// boustrophedon over the launch's centre-out block sequence: with T = P·nw
-// blocks in the launch, wave k takes blocks k, 2nw−1−k, 2nw+k, 4nw−1−k, …
-// — a heavy block from the centre bands paired with a light one from the
-// edge.  Every wave then carries comparable work, the launch has P× fewer
-// waves to dispatch and to start (argument loads, prologue), and the last
-// waves to start are not a run of short exterior waves that the wave
-// dispatcher cannot launch fast enough to keep the SIMDs busy.  Device
-// ranges and pipeline chunks stay whole bands of the launch (every write
-// stays in the launch's rows).
-template <int P>
-__device__ __forceinline__ void mandel_blk8_multi(const float* view, const int* size, int2* out, long long off) {
-  const int W = size[0], max_iter = size[2];
-  const int bpb = W >> 4;  // blocks per band
-  const int nw = (int)gridDim.x;
-  const int b0 = __builtin_amdgcn_readfirstlane((int)(((off >> 6) * P) / bpb));
-  const int nbl = P * nw / bpb;  // bands in this launch
-  const int c = nbl >> 1;
-  const int l = threadIdx.x;
-  const int r = l >> 3, c2 = (l & 7) * 2;
-  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
-  const int k = (int)blockIdx.x;
-#pragma unroll 1
-  for (int h = 0; h < P; ++h) {
-    const int j = (h & 1) ? (h + 1) * nw - 1 - k : h * nw + k;
-    const int kb = j / bpb, blk = j - kb * bpb;
-    const int band = b0 + ((kb & 1) ? c - ((kb + 1) >> 1) : c + (kb >> 1));
-    const float ci = y0 + (float)(band * 8 + r) * dy;
-    const float crx = x0 + (float)(blk * 16 + c2) * dx;
-    const f32x2 cr = {crx, crx + dx}, civ = {ci, ci};
-    out[((long long)band * 4 * W + blk * 8) + r * (W >> 1) + (l & 7)] = mandel_blk8_core<32, 32, true>(cr, civ, max_iter);
-  }
-}
-
-extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8v_f32(const float* view, const int* size,
-                                                                        int2* out, CEK_HIDDEN) {
-  mandel_blk8_multi<2>(view, size, out, __cek_off);
-}
-
-extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8w_f32(const float* view, const int* size,
-                                                                        int2* out, CEK_HIDDEN) {
-  mandel_blk8_multi<4>(view, size, out, __cek_off);
-}

@@ -20,8 +20,7 @@ FLOP_PER_ITER = 8
 
 # kernel variants; the band kernels additionally need device and pipeline
 # chunk ranges made of whole 16-row bands (see kernels/mandelbrot.hip)
-BAND_ROWS = {"blk8": 8, "blk8h": 8, "blk8k": 8, "blk8m": 8, "blk8t": 8, "blk8u": 8, "blk8v": 8,
-             "blk8w": 8}  # rows per band
+BAND_ROWS = {"blk8": 8, "blk8h": 8, "blk8k": 8, "blk8m": 8, "blk8t": 8, "blk8u": 8}  # rows per band
 BAND_KERNELS = set(BAND_ROWS)
 KERNELS = {
     # name: (library kernel, pixels per work item, work-group size)
@@ -45,10 +44,6 @@ KERNELS = {
     # blk8t with each launch's bands in centre-out order (longest first for
     # views centred on the set)
     "blk8u": ("cek_mandelbrot_blk8u_f32", 2, 64),
-    # blk8u with 2 / 4 blocks per wave, a centre block paired with an edge
-    # block (fewer, evenly loaded waves; 4 / 8 pixels per work item)
-    "blk8v": ("cek_mandelbrot_blk8v_f32", 4, 64),
-    "blk8w": ("cek_mandelbrot_blk8w_f32", 8, 64),
 }
 
 
