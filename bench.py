@@ -698,7 +698,7 @@ def compact_extra(full: dict, detail: str) -> dict:
     tp = full.get("task_pool")
     if isinstance(tp, dict):
         t = _pick(tp, ["tasks", "pool_devices", "cu_partitioned", "makespan_ms", "ideal_ms_sum_over_devices",
-                       "makespan_over_ideal", "dispatch_tasks_per_s", "host_us_per_task", "median_task_device_us",
+                       "makespan_over_ideal", "makespan_over_ideal_cu_partitioned", "dispatch_tasks_per_s", "host_us_per_task", "median_task_device_us",
                        "serial_group_in_order", "gemm_task_max_rel_err", "reduce_task_rel_err"])
         rr = tp.get("round_robin")
         if isinstance(rr, dict):

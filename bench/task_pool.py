@@ -292,6 +292,7 @@ emit({"config": "task_pool_256", "tasks": ntasks, "gpus": ng, "logical_devices":
       "ideal_basis": ("hipEvent device time per task, alone on one CU partition; sum / partitions" if partitioned
                       else "hipEvent device time per task, alone on one GPU; sum / GPUs"),
       "makespan_over_ideal": makespan / ideal, "tasks_per_s": ntasks / (makespan * 1e-3),
+      **({"makespan_over_ideal_cu_partitioned": makespan / ideal} if partitioned else {}),
       # the pool's host cost per task (one producer, D consumers) against
       # the device time one task feeds: the pool keeps up when it is below
       "host_us_per_task": round(1e6 / dispatch, 2),
