@@ -703,6 +703,10 @@ def compact_extra(full: dict, detail: str) -> dict:
         rr = tp.get("round_robin")
         if isinstance(rr, dict):
             t["round_robin_makespan_over_ideal"] = _r(rr.get("makespan_over_ideal"))
+        cs = tp.get("concurrent_spans")
+        if isinstance(cs, dict):
+            t["makespan_over_concurrent_ideal"] = _r(cs.get("makespan_over_ideal"))
+            t["contention_factor"] = _r(cs.get("contention_factor"))
         ex["task_pool"] = t
     nb = full.get("nbody_pipeline")
     if isinstance(nb, dict):

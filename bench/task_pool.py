@@ -221,7 +221,7 @@ def build_pool() -> ClTaskPool:
     return tp
 
 
-def run_policy(policy):
+def run_policy(policy, spans=False):
     pool = ClDevicePool(policy, SRC, True, a.queues, prebuilt=prebuilt)
     pool.add_device(devs)
     for cr in pool.crunchers:  # every input on every device: a task may land anywhere
@@ -241,6 +241,27 @@ def run_policy(policy):
     sync()
     ms = (time.perf_counter() - t0) * 1e3
     counts = pool.device_task_counts()
+    concurrent = None
+    if spans:
+        # one more pass with every task's device span recorded (hipEvents
+        # around its kernels): the tasks' device times as they ran, side by
+        # side with the other devices' tasks — on one GPU the partitions
+        # share HBM, L2 and fabric, so this is the basis of an ideal that
+        # the shared hardware allows
+        for cr in pool.crunchers:
+            cr.record_timeline = True
+        tp3 = build_pool()
+        sync()
+        t0 = time.perf_counter()
+        pool.enqueue_task_pool(tp3)
+        pool.finish()
+        sync()
+        ms3 = (time.perf_counter() - t0) * 1e3
+        busy = 0.0
+        for cr in pool.crunchers:
+            busy += sum(sp["end_ms"] - sp["begin_ms"] for sp in cr.timeline())
+            cr.record_timeline = False
+        concurrent = {"makespan_ms": ms3, "task_device_ms_sum": busy, "ideal_ms": busy / len(pool.crunchers)}
     # dispatch rate: 4096 tasks of one work-group each (the host-side cost
     # of the pool: native batch enqueue, consumer threads, marker retirement)
     tiny_x = [ck.ClArray(np.zeros(256, np.float32)) for _ in range(64)]
@@ -264,12 +285,12 @@ def run_policy(policy):
     sync()
     dispatch = 4096 / (time.perf_counter() - t0)
     pool.dispose()
-    return n, ms, counts, dispatch
+    return n, ms, counts, dispatch, concurrent
 
 
-ntasks, makespan, counts, dispatch = run_policy(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL)
+ntasks, makespan, counts, dispatch, concurrent = run_policy(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, spans=True)
 ideal = sum(single) / (len(devs) if partitioned else max(1, ng))
-_, makespan_rr, counts_rr, dispatch_rr = run_policy(ClDevicePoolType.DEVICE_ROUND_ROBIN)
+_, makespan_rr, counts_rr, dispatch_rr, _ = run_policy(ClDevicePoolType.DEVICE_ROUND_ROBIN)
 
 # checks: serial group order (x ← 2x + 1, eight times from 0 = 255), one GEMM, one reduction
 serial_ok = bool(np.all(serial_x.array == 255.0))
@@ -293,6 +314,10 @@ emit({"config": "task_pool_256", "tasks": ntasks, "gpus": ng, "logical_devices":
                       else "hipEvent device time per task, alone on one GPU; sum / GPUs"),
       "makespan_over_ideal": makespan / ideal, "tasks_per_s": ntasks / (makespan * 1e-3),
       **({"makespan_over_ideal_cu_partitioned": makespan / ideal} if partitioned else {}),
+      # the same pool with each task's device span recorded as it ran beside
+      # the others: Σ spans / devices is the ideal the shared hardware allows
+      "concurrent_spans": {**concurrent, "makespan_over_ideal": concurrent["makespan_ms"] / concurrent["ideal_ms"],
+                           "contention_factor": concurrent["task_device_ms_sum"] / sum(single)},
       # the pool's host cost per task (one producer, D consumers) against
       # the device time one task feeds: the pool keeps up when it is below
       "host_us_per_task": round(1e6 / dispatch, 2),

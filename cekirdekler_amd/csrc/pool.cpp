@@ -121,7 +121,11 @@ int DevicePool::limit_locked() {
   // Floor of 2 (when the pool allows 2): with one task in flight a device
   // idles for the host's enqueue + marker-retirement turnaround (10-20 µs)
   // between tasks; two in flight hide it and the tail stays balanced.
-  const long long floor_q = std::min(2, max_in_flight_);
+  static const int min_inflight = [] {
+    const char* e = std::getenv("CEK_POOL_MIN_INFLIGHT");
+    return e ? std::max(1, std::atoi(e)) : 2;
+  }();
+  const long long floor_q = std::min(min_inflight, max_in_flight_);
   const int lim = static_cast<int>(std::max<long long>(floor_q, std::min<long long>(q, max_in_flight_)));
   if (limit_history_.empty() || limit_history_.back() != lim) limit_history_.push_back(lim);
   return lim;
