@@ -707,6 +707,7 @@ def compact_extra(full: dict, detail: str) -> dict:
         if isinstance(cs, dict):
             t["makespan_over_concurrent_ideal"] = _r(cs.get("makespan_over_ideal"))
             t["contention_factor"] = _r(cs.get("contention_factor"))
+        t["makespan_over_greedy_sim"] = _r(tp.get("makespan_over_greedy_sim"))
         ex["task_pool"] = t
     nb = full.get("nbody_pipeline")
     if isinstance(nb, dict):

@@ -290,6 +290,27 @@ def run_policy(policy, spans=False):
 
 ntasks, makespan, counts, dispatch, concurrent = run_policy(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, spans=True)
 ideal = sum(single) / (len(devs) if partitioned else max(1, ng))
+
+
+def greedy_fifo_ms(times, ndev, barrier_at):
+    """Makespan of the reference's own policy with zero overhead: tasks in
+    FIFO order, each to the device that frees first (compute at will,
+    ClPipeline.cs:4132-4312), every device drained at the global barrier.
+    Σ/D is a bound no FIFO-greedy schedule of these tasks reaches (one
+    device may take several of the 0.7 ms N-body tasks before the barrier)."""
+    free = [0.0] * ndev
+    for i, t in enumerate(times):
+        if i == barrier_at:
+            free = [max(free)] * ndev
+        d = min(range(ndev), key=free.__getitem__)
+        free[d] += t
+    return max(free)
+
+
+contention = concurrent["task_device_ms_sum"] / sum(single)
+greedy_ms = greedy_fifo_ms(single, len(devs) if partitioned else max(1, ng), len(work) // 2)
+greedy_ms_contended = greedy_fifo_ms([t * contention for t in single], len(devs) if partitioned else max(1, ng),
+                                     len(work) // 2)
 _, makespan_rr, counts_rr, dispatch_rr, _ = run_policy(ClDevicePoolType.DEVICE_ROUND_ROBIN)
 
 # checks: serial group order (x ← 2x + 1, eight times from 0 = 255), one GEMM, one reduction
@@ -317,7 +338,11 @@ emit({"config": "task_pool_256", "tasks": ntasks, "gpus": ng, "logical_devices":
       # the same pool with each task's device span recorded as it ran beside
       # the others: Σ spans / devices is the ideal the shared hardware allows
       "concurrent_spans": {**concurrent, "makespan_over_ideal": concurrent["makespan_ms"] / concurrent["ideal_ms"],
-                           "contention_factor": concurrent["task_device_ms_sum"] / sum(single)},
+                           "contention_factor": contention},
+      # the reference's FIFO greedy policy simulated with zero overhead on
+      # the measured task times (alone, and scaled by the contention factor)
+      "greedy_fifo_sim_ms": greedy_ms, "greedy_fifo_sim_contended_ms": greedy_ms_contended,
+      "makespan_over_greedy_sim": makespan / greedy_ms_contended,
       # the pool's host cost per task (one producer, D consumers) against
       # the device time one task feeds: the pool keeps up when it is below
       "host_us_per_task": round(1e6 / dispatch, 2),
