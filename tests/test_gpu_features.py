@@ -720,3 +720,55 @@ def test_cu_partition_runs_on_its_own_cus(gpu, parts):
     for p in range(parts):
         for q in range(p + 1, parts):
             assert not (seen[p] & seen[q]), (p, q)
+
+
+@pytest.mark.parametrize("policy", [0, 1])
+def test_task_pool_on_cu_partitions(gpu, policy):
+    """The device pool over 4 CU partitions of one GPU (one CU-masked stream
+    each, event markers): a serial group runs in order on one partition,
+    a global barrier orders two phases, every task's downloaded output is
+    right (the marker after a download carries a system-scope release), and
+    the device-resident tasks' markers (fence-less) all retire."""
+    from cekirdekler_amd.parallel.pool import ClDevicePool, ClDevicePoolType, ClTask, ClTaskPool, ClTaskType
+
+    src = """__global__ void fill(float* x, float* v) { x[get_global_id(0)] = v[0]; }
+    __global__ void add(float* x, const float* v) { long long i = get_global_id(0); x[i] = x[i] * 2.0f + v[0]; }"""
+    pool = ClDevicePool(ClDevicePoolType(policy), src, True, 3)
+    pool.add_device(gpu[0:1].cu_partitions(4))
+    assert all(cr.compute_queue_concurrency == 1 for cr in pool.crunchers)
+    tp = ClTaskPool()
+    arrays, order = [], []
+    lock = threading.Lock()
+    for i in range(48):
+        if i == 24:
+            tp.feed(ClTask.global_barrier())
+        x = ck.ClArray(np.zeros(1 << 14, np.float32))
+        v = ck.ClArray(np.array([float(i)], np.float32))
+        v.write = False
+        t = x.next_param(v).task(1, "fill", 1 << 14, 256)
+        t.set_callback(lambda i=i: (lock.acquire(), order.append(i), lock.release()))
+        tp.feed(t)
+        arrays.append(x)
+    shared = ck.ClArray(np.zeros(4096, np.float32))
+    one = ck.ClArray(np.array([1.0], np.float32))
+    one.write = False
+    group = []
+    for k in range(6):
+        shared.read = k == 0
+        shared.write = k == 5
+        t = shared.next_param(one).task(2, "add", 4096, 256)
+        t.type = (ClTaskType.TASK_MESSAGE_SERIAL_MODE_BEGIN if k == 0 else
+                  ClTaskType.TASK_MESSAGE_SERIAL_MODE_END if k == 5 else ClTaskType.TASK_MESSAGE_DEFAULT)
+        tp.feed(t)
+        group.append(t)
+    pool.enqueue_task_pool(tp)
+    pool.finish()
+    for i, x in enumerate(arrays):
+        np.testing.assert_array_equal(x.array, float(i))
+    assert set(order[:24]) == set(range(24))  # the barrier ordered the phases
+    np.testing.assert_array_equal(shared.array, 63.0)  # x <- 2x + 1, six times from 0, in order
+    assert len({t.device_index for t in group}) == 1
+    assert sum(pool.device_task_counts()) == 48 + 1 + 6
+    for cr in pool.crunchers:
+        assert cr.count_markers_remaining() == 0
+    pool.dispose()
