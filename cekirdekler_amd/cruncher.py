@@ -466,6 +466,29 @@ class ClNumberCruncher:
         return [{"device": d, "compute_id": cid, "begin_ms": b, "end_ms": e, "abs_begin_ms": ab, "abs_end_ms": ae}
                 for d, cid, b, e, ab, ae in self._cores.timeline()]
 
+    @property
+    def record_kernel_times(self) -> bool:
+        """Kernel profiling timestamps (OpenCL's CL_PROFILING_COMMAND_START /
+        END): while on, every kernel launch carries a start and a stop event
+        stamped by the dispatch itself (``hipExtModuleLaunchKernel``), so
+        :meth:`kernel_times` gives each kernel's own execution time — without
+        the gap between back-to-back launches that stream events and host
+        clocks include."""
+        return bool(self._cores.kernel_times_on) if self._cores else False
+
+    @record_kernel_times.setter
+    def record_kernel_times(self, on: bool) -> None:
+        self._cores.kernel_times_on = bool(on)
+
+    def kernel_times(self, device: int = 0) -> List[tuple]:
+        """(kernel name, ms) of every launch on local ``device`` recorded
+        while :attr:`record_kernel_times` was on, in launch order; waits for
+        them and clears the list."""
+        return [(k, float(ms)) for k, ms in self._cores.kernel_times(device)]
+
+    recordKernelTimes = record_kernel_times
+    kernelTimes = kernel_times
+
     def last_record(self) -> dict:
         """Structured record of the last compute (observability)."""
         r = self._cores.last_record()

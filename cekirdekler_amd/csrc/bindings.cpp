@@ -504,6 +504,8 @@ PYBIND11_MODULE(_cek, m) {
       .def_property("debug_checks", &Cores::debug_checks, &Cores::set_debug_checks)
       .def("gemm_host_shells", &Cores::gemm_host_shells, py::call_guard<py::gil_scoped_release>())
       .def_property("kernel_d2h", &Cores::kernel_d2h, &Cores::set_kernel_d2h)
+      .def_property("kernel_times_on", &Cores::kernel_times_on, &Cores::set_kernel_times)
+      .def("kernel_times", &Cores::kernel_times, py::arg("device"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("kernel_d2h_bytes", &Cores::kernel_d2h_bytes)
       .def("device_enqueue_errors", &Cores::device_enqueue_errors, py::call_guard<py::gil_scoped_release>())
       .def("timeline",

@@ -229,6 +229,12 @@ class Cores {
     for (auto& w : workers_) w->kernel_d2h = on;
   }
   bool kernel_d2h() const { return !workers_.empty() && workers_[0]->kernel_d2h.load(); }
+  // kernel profiling timestamps (Worker::kernel_times_on)
+  void set_kernel_times(bool on) {
+    for (auto& w : workers_) w->kernel_times_on = on;
+  }
+  bool kernel_times_on() const { return !workers_.empty() && workers_[0]->kernel_times_on.load(); }
+  std::vector<std::pair<std::string, double>> kernel_times(int dev) { return workers_.at(dev)->kernel_times(); }
   // CUs reserved per GPU for copy kernels (Worker::set_cu_reserve); drains
   // and re-creates the streams
   void set_copy_cus(int n) {

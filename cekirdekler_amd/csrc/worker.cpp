@@ -6,6 +6,16 @@
 
 #include "memory.h"
 
+// hip/hip_ext.h declares this AMD launch (kernel start/stop events stamped by
+// the dispatch) next to a template that needs the device-compiler headers;
+// the host build takes the C declaration alone
+extern "C" hipError_t hipExtModuleLaunchKernel(hipFunction_t f, uint32_t globalWorkSizeX, uint32_t globalWorkSizeY,
+                                               uint32_t globalWorkSizeZ, uint32_t localWorkSizeX,
+                                               uint32_t localWorkSizeY, uint32_t localWorkSizeZ,
+                                               size_t sharedMemBytes, hipStream_t hStream, void** kernelParams,
+                                               void** extra, hipEvent_t startEvent, hipEvent_t stopEvent,
+                                               uint32_t flags);
+
 namespace cek {
 
 // ----------------------------------------------------------------- CpuPool --
@@ -166,6 +176,11 @@ Worker::~Worker() {
       for (auto s : h)
         if (s) (void)hipStreamDestroy(s);
     host_free(marker_words_);
+    for (auto& k : kstamps_) {
+      (void)hipEventDestroy(k.start);
+      (void)hipEventDestroy(k.stop);
+    }
+    for (auto e : kstamp_spare_) (void)hipEventDestroy(e);
     for (auto& r : rings_) {
       for (auto& e : r.pending) (void)hipEventDestroy(e.first);
       for (auto e : r.spare) (void)hipEventDestroy(e);
@@ -605,8 +620,16 @@ void Worker::launch(hipStream_t s, const std::string& kernel, const std::vector<
       CEK_HIP(hipMemsetAsync(q, 0, 8 * sizeof(int), s));
     }
     unsigned grid = static_cast<unsigned>(count / local);
-    CEK_HIP(hipModuleLaunchKernel(f, grid, 1, 1, static_cast<unsigned>(local), 1, 1, dyn_lds_, s,
-                                  params.data(), nullptr));
+    if (kernel_times_on.load(std::memory_order_relaxed)) {
+      hipEvent_t a = kstamp_event(), b = kstamp_event();
+      CEK_HIP(hipExtModuleLaunchKernel(f, grid * static_cast<unsigned>(local), 1, 1, static_cast<unsigned>(local),
+                                       1, 1, dyn_lds_, s, params.data(), nullptr, a, b, 0));
+      std::lock_guard<std::mutex> g(kstamp_mu_);
+      kstamps_.push_back({kernel, a, b});
+    } else {
+      CEK_HIP(hipModuleLaunchKernel(f, grid, 1, 1, static_cast<unsigned>(local), 1, 1, dyn_lds_, s,
+                                    params.data(), nullptr));
+    }
     if (dyn && prog_->has_dispatcher(kernel)) {
       // one launch per child level, same stream: level L's records were
       // written by level L-1's kernel, which the stream has completed
@@ -633,6 +656,43 @@ void Worker::launch(hipStream_t s, const std::string& kernel, const std::vector<
       fn(argv, offset, gsize, offset + g0 * local, (g1 - g0) * local, local);
     });
   }
+}
+
+hipEvent_t Worker::kstamp_event() {
+  {
+    std::lock_guard<std::mutex> g(kstamp_mu_);
+    if (!kstamp_spare_.empty()) {
+      hipEvent_t e = kstamp_spare_.back();
+      kstamp_spare_.pop_back();
+      return e;
+    }
+  }
+  set_device();
+  hipEvent_t e = nullptr;
+  CEK_HIP(hipEventCreate(&e));  // timing enabled
+  return e;
+}
+
+std::vector<std::pair<std::string, double>> Worker::kernel_times() {
+  std::vector<KernelStamp> st;
+  {
+    std::lock_guard<std::mutex> g(kstamp_mu_);
+    st.swap(kstamps_);
+  }
+  std::vector<std::pair<std::string, double>> out;
+  out.reserve(st.size());
+  for (auto& k : st) {
+    CEK_HIP(hipEventSynchronize(k.stop));
+    float ms = 0.f;
+    CEK_HIP(hipEventElapsedTime(&ms, k.start, k.stop));
+    out.emplace_back(k.kernel, ms);
+  }
+  std::lock_guard<std::mutex> g(kstamp_mu_);
+  for (auto& k : st) {
+    kstamp_spare_.push_back(k.start);
+    kstamp_spare_.push_back(k.stop);
+  }
+  return out;
 }
 
 void Worker::check_guards(hipStream_t s, const std::string& kernel, const std::vector<ArraySpec>& arrs) {

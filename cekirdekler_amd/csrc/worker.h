@@ -163,6 +163,14 @@ class Worker {
   // aligned ends: keeps downloads off the SDMA rings the uploads use, so a
   // download gated on a kernel never blocks an upload queued behind it
   std::atomic<bool> kernel_d2h{false};
+  // Kernel profiling timestamps (the counterpart of OpenCL's
+  // CL_PROFILING_COMMAND_START / END): while on, every launch goes through
+  // hipExtModuleLaunchKernel with a start and a stop event that the runtime
+  // stamps from the dispatch itself — the kernel's own execution time,
+  // without the gap between back-to-back launches that stream events or a
+  // host clock include.  kernel_times() drains them: (kernel, ms) in launch order.
+  std::atomic<bool> kernel_times_on{false};
+  std::vector<std::pair<std::string, double>> kernel_times();
   static constexpr uint64_t kKernelD2HMinBytes = 1ull << 20;
   uint64_t kernel_d2h_bytes() const { return kernel_d2h_bytes_; }
   int device_enqueue_errors();
@@ -258,6 +266,14 @@ class Worker {
     uint64_t done = 0;
   };
   std::vector<MarkerRing> rings_;
+  struct KernelStamp {
+    std::string kernel;
+    hipEvent_t start, stop;
+  };
+  std::vector<KernelStamp> kstamps_;
+  std::vector<hipEvent_t> kstamp_spare_;
+  std::mutex kstamp_mu_;
+  hipEvent_t kstamp_event();
   std::mutex marker_mu_;
   bool write_value_markers_ = false;  // CEK_MARKERS=writevalue: the old path
   long long markers_issued_ = 0;

@@ -772,3 +772,33 @@ def test_task_pool_on_cu_partitions(gpu, policy):
     for cr in pool.crunchers:
         assert cr.count_markers_remaining() == 0
     pool.dispose()
+
+
+def test_kernel_profiling_timestamps(gpu):
+    """record_kernel_times: every launch carries dispatch-stamped start/stop
+    events; kernel_times() returns one positive duration per launch, in
+    launch order, each no longer than the host wall of the whole batch."""
+    import time
+
+    src = """__global__ void spin(float* x, const int* it) {
+      long long i = get_global_id(0); float v = x[i];
+      for (int k = 0; k < it[0]; ++k) v = v * 0.999f + 1.0f; x[i] = v; }"""
+    cr = ck.ClNumberCruncher(gpu[0], src)
+    x = ck.ClArray(np.zeros(1 << 20, np.float32))
+    it = ck.ClArray(np.array([4000], np.int32))
+    x.read = x.write = False
+    it.write = False
+    x.next_param(it).compute(cr, 1, "spin", 1 << 20, 256)
+    cr.record_kernel_times = True
+    cr.enqueue_mode = True
+    t0 = time.perf_counter()
+    for _ in range(5):
+        x.next_param(it).compute(cr, 1, "spin", 1 << 20, 256)
+    cr.enqueue_mode = False
+    wall = (time.perf_counter() - t0) * 1e3
+    cr.record_kernel_times = False
+    kt = cr.kernel_times(0)
+    assert [k for k, _ in kt] == ["spin"] * 5
+    assert all(0 < ms < wall for _, ms in kt), (kt, wall)
+    assert cr.kernel_times(0) == []  # drained
+    cr.dispose()
