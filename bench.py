@@ -163,6 +163,17 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
                enter=lambda: setattr(cr, "enqueue_mode", True),
                leave=lambda: setattr(cr, "enqueue_mode", False))
     ranges = cr.ranges(1)
+    # the same computes once more with dispatch-stamped kernel times: the
+    # GEMM kernel alone, without the gap between back-to-back launches that
+    # the per-step time includes (informative; not the headline)
+    cr.record_kernel_times = True
+    cr.enqueue_mode = True
+    for _ in range(steps):
+        step()
+    cr.enqueue_mode = False
+    cr.record_kernel_times = False
+    kt = sorted(t for name, t in cr.kernel_times(0) if name.startswith("cek_sgemm"))
+    kernel_ms = _max_over_ranks(ctx, kt[len(kt) // 2] if kt else 0.0)
     # the benchmarked output itself: EVERY tile of this rank's C replica
     # against a float64 product on its GPU (before the host-resident run
     # below re-splits compute id 2 and overwrites the host copy)
@@ -282,6 +293,7 @@ def bench_sgemm(ctx, steps, warmup, size=8192, tile=None):
             "host_resident_native_shells_ms": ms_native_shells, "host_resident_shells_copy_cus_ms": ms_shells_cu,
             "ranges": ranges, "max_rel_err": max(err, err_async, err_host), "max_rel_err_host_resident": err_host,
             "tiles_checked": tiles_checked, "tiles_total": g.tiles,
+            "kernel_ms": kernel_ms, "kernel_gflops": g.flops / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None,
             "handover_fallbacks": fallbacks, "device": "gpu"}
 
 
@@ -758,6 +770,7 @@ def compact_extra(full: dict, detail: str) -> dict:
     ex["sgemm"] = {
         "gflops_single_queue": _r(sq.get("gflops"), 1), "gflops_async_queues": _r(aq.get("gflops"), 1),
         "gflops_sync_per_step": _r(sg.get("sync_per_step_gflops"), 1),
+        "kernel_ms": _r(sg.get("kernel_ms"), 4), "gflops_kernel_timestamps": _r(sg.get("kernel_gflops"), 1),
         "tile": sg.get("tile"), "ranges": sg.get("ranges"),
         "ranges_identical_on_all_ranks": all(r == all_ranges[0] for r in all_ranges),
         "balancer_setup_calls": sg.get("balancer_setup_calls"),
