@@ -562,6 +562,35 @@ def bench_lb_iters():
 ROOT = os.path.dirname(os.path.abspath(__file__))
 
 
+def _child_env() -> dict:
+    """This environment without the rank variables: a child program is a
+    job of its own (or starts its own torchrun)."""
+    return {k: v for k, v in os.environ.items()
+            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                         "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+
+
+def _run_child(cmd, env, timeout: float) -> dict:
+    """Run one bench/ program as a child process in its own session and
+    return the last JSON line it printed; a failure or a timeout (which
+    kills the whole process group, torchrun's ranks too) is reported in the
+    returned dict instead."""
+    p = subprocess.Popen(cmd, cwd=os.path.join(ROOT, "bench"), env=env, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        so, se = p.communicate(timeout=timeout)
+        lines = [ln for ln in so.splitlines() if ln.startswith("{")]
+        return json.loads(lines[-1]) if (p.returncode == 0 and lines) else {
+            "error": f"exit {p.returncode}: {(se or so)[-300:]}"}
+    except Exception as e:  # timeout or parse failure
+        try:
+            os.killpg(p.pid, 9)
+        except OSError:
+            pass
+        p.communicate()
+        return {"error": repr(e)[:300]}
+
+
 def bench_node_configs(world: int) -> dict:
     """BASELINE configs 4 and 5 on this job's GPUs (0 .. world-1), run by
     rank 0 after every other rank has left: the N-body 3-stage
@@ -571,9 +600,7 @@ def bench_node_configs(world: int) -> dict:
     single-process programs (the reference's model), so each runs as a child
     process with its own time limit; a failure is reported in its field and
     cannot stop the headline."""
-    env = {k: v for k, v in os.environ.items()
-           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
-                        "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    env = _child_env()
     out = {}
     rccl = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
             "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "rccl_gemm.py",
@@ -607,26 +634,13 @@ def bench_node_configs(world: int) -> dict:
         if left < 30:
             out[name] = {"skipped": f"node-config time budget ({NODE_CONFIGS_BUDGET_S} s) spent"}
             continue
-        # own session: a timeout kills the whole process group (torchrun's ranks too)
-        p = subprocess.Popen(cmd, cwd=os.path.join(ROOT, "bench"), env=env, stdout=subprocess.PIPE,
-                             stderr=subprocess.PIPE, text=True, start_new_session=True)
-        try:
-            so, se = p.communicate(timeout=min(180, left))
-            lines = [ln for ln in so.splitlines() if ln.startswith("{")]
-            out[name] = json.loads(lines[-1]) if (p.returncode == 0 and lines) else {
-                "error": f"exit {p.returncode}: {(se or so)[-300:]}"}
-        except Exception as e:  # timeout or parse failure
-            try:
-                os.killpg(p.pid, 9)
-            except OSError:
-                pass
-            p.communicate()
-            out[name] = {"error": repr(e)[:300]}
+        out[name] = _run_child(cmd, env, min(180, left))
     return out
 
 
 MAX_REL_ERR = 1e-4  # bf16 inputs, fp32 accumulation: measured ~1.5e-6 relative to max |ref| per tile
 NODE_CONFIGS_BUDGET_S = 360  # all of bench_node_configs' child processes together
+PEER_TOPOLOGY_TIMEOUT_S = 90
 HOST_RESIDENT_BLOBS = 8
 HOST_RESIDENT_PANELS = 16
 HOST_RESIDENT_COPY_CUS = 8
@@ -678,7 +692,9 @@ def compact_extra(full: dict, detail: str) -> dict:
     next #1).  ``full`` is what :func:`write_detail` writes."""
     ex = {"detail_file": detail}
     peers = full.get("peer_topology") or {}
-    if peers:
+    if "error" in peers:
+        ex["peer"] = _pick(peers, [])
+    elif peers:
         bw = peers.get("bandwidth") or {}
         same = (bw.get("same_gpu") or {}).get("sdma") or {}
         pairs = bw.get("pairs") or []
@@ -786,22 +802,11 @@ def compact_extra(full: dict, detail: str) -> dict:
 
 
 def _peer_topology(world: int) -> dict:
-    """hipDeviceCanAccessPeer among this job's GPUs, the device-to-device path
-    the runtime takes between them, and measured copy bandwidth by engine
-    (SDMA vs copy kernel; a few pairs, every pair at once, inside GPU 0),
-    every copy checked byte for byte (utils/multigpu.peer_bandwidth_report)."""
-    from cekirdekler_amd._native import cek
-    from cekirdekler_amd.utils.multigpu import peer_bandwidth_report
-
-    full = cek.can_access_peer_matrix()
-    ngpu = min(world, len(full))  # ranks may share a GPU (one-GPU rehearsals)
-    m = [row[:ngpu] for row in full[:ngpu]]
-    out = {"gpus_visible": len(full), "job_gpus": world, "can_access_peer": m, "path": cek.peer_path(m)}
-    try:  # an extra: a failure is reported in its field
-        out["bandwidth"] = peer_bandwidth_report(list(range(ngpu)))
-    except Exception as e:  # pragma: no cover
-        out["bandwidth"] = {"error": repr(e)[:300]}
-    return out
+    """hipDeviceCanAccessPeer among this job's GPUs, the device-to-device
+    path between them and measured copy bandwidth by engine
+    (``bench/peer_topology.py``), in a child process with its own time limit
+    so that the peer paths cannot hold the headline line back."""
+    return _run_child([sys.executable, "peer_topology.py", "--gpus", str(world)], _child_env(), PEER_TOPOLOGY_TIMEOUT_S)
 
 
 def _free_port() -> int:
