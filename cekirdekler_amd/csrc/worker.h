@@ -259,7 +259,7 @@ class Worker {
   // spare events, and how many have completed.  A marker is a barrier packet
   // with a completion signal; hipStreamWriteValue64 runs as a blit kernel
   // (__amd_rocclr_streamOpsWrite) — a kernel dispatch per marker, ~10× the
-  // host cost under 8 submitting threads (profiles/r5/task_pool_partitions.md).
+  // host cost under 8 submitting threads (profiles/r5/README.md).
   struct MarkerRing {
     std::deque<std::pair<hipEvent_t, bool>> pending;  // (event, system-scope release)
     std::deque<hipEvent_t> spare, spare_fenced;

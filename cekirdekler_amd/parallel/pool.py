@@ -12,15 +12,16 @@ control each device keeps several tasks in flight — the reference's
 adaptive per-device limit (N/10 … N/50 tasks over the devices, at most 16,
 ClPipeline.cs:4178-4236) — spread over ``max_queues_per_device`` HIP
 streams (enqueue mode + round-robin queues), and retires them through
-stream-written marker words (``hipStreamWriteValue64``), the µs-cheap
-counterpart of the reference's 150–300 µs marker callbacks (Cores.cs:447).
+stream markers (fence-less events, recorded after each task and polled with
+``hipEventQuery``), the µs-cheap counterpart of the reference's 150–300 µs
+marker callbacks (Cores.cs:447).
 The in-flight depth is not tied to the stream count: tasks queued in order
 on one stream still keep the device busy while the host prepares the next.
 A CU-partitioned device (``ClDevices.cu_partitions``) gets one stream: each
 CU-masked stream owns a hardware queue, and 8 partitions × several streams
 oversubscribe the GPU's queue slots (measured: 4096 one-work-group tasks
 over 8 partitions ran at 38 k tasks/s with 4 streams per partition against
-95 k with one; profiles/r5/task_pool_partitions.md).  User callbacks run on
+95 k with one; profiles/r5/README.md).  User callbacks run on
 a dispatcher thread as completions arrive.
 
 Task type flags (ClTaskType, :3247-3321): DEVICE_SELECT_BEGIN/END and
