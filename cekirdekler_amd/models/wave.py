@@ -107,12 +107,15 @@ class WaveSurface:
         # instead of a D2H copy after the kernel (0.0399 vs 0.0498 ms per
         # GPU frame, tools/wave_zc_probe.py).
         self.xyzo.zero_copy = bool(zero_copy_output)
-        # the 256-byte argument block, uploaded every frame, in pinned memory
-        # (a pageable copy is staged through a blit kernel)
+        # the 256-byte argument block, new every frame, in pinned memory that
+        # GPU kernels read in place (zero-copy): no copy command in the
+        # frame's stream (0.0360 vs 0.0389 ms per GPU frame with a per-frame
+        # upload, tools/wave_args_probe.py, profiles/r5/wave_args_s23.json)
         self.arguments = ClArray(64, np.float32)
         self.arguments.array[:] = 0
         self.arguments.write = False
         self.arguments.partial_read = False
+        self.arguments.zero_copy = True
         self.t = 0.0
         self.ctr = 0.0
 
