@@ -468,12 +468,34 @@ __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ
 // interior waves sharing a few SIMDs.  The order stays inside the launch's
 // own bands (device ranges and pipeline chunks are whole bands), so every
 // write stays in the launch's range.
-template <int BIG, int S, bool ASM, bool CENTER = false>
+// FASTPRO: a shorter serial prologue per wave.  The view and size loads
+// are issued together (one wait instead of two dependent ones), and a
+// power-of-two blocks-per-band count (any width 16·2^k, e.g. 4096) maps the
+// work-group index with shifts instead of three scalar integer divisions
+// (~100 dependent SALU instructions per wave in the compiler's expansion);
+// other widths keep the division.
+template <int BIG, int S, bool ASM, bool CENTER = false, bool FASTPRO = false>
 __device__ __forceinline__ void mandel_blk8m(const float* view, const int* size, int2* out, long long off) {
   const int W = size[0], max_iter = size[2];
+  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
+  if constexpr (FASTPRO) asm volatile("" ::"s"(W), "s"(max_iter), "s"(x0), "s"(y0), "s"(dx), "s"(dy));
   const int bpb = W >> 4;  // blocks per band
   int band, blk;
-  if constexpr (CENTER) {
+  if (FASTPRO && (bpb & (bpb - 1)) == 0) {
+    const int sh = __builtin_ctz((unsigned)bpb);
+    if constexpr (CENTER) {
+      const int b0 = (int)(off >> (6 + sh));
+      const int nbl = (int)gridDim.x >> sh;  // bands in this launch
+      const int kb = (int)blockIdx.x >> sh;
+      blk = (int)blockIdx.x & (bpb - 1);
+      const int c = nbl >> 1;
+      band = b0 + ((kb & 1) ? c - ((kb + 1) >> 1) : c + (kb >> 1));
+    } else {
+      const int wv = (int)(((long long)blockIdx.x * 64 + off) >> 6);
+      band = wv >> sh;
+      blk = wv & (bpb - 1);
+    }
+  } else if constexpr (CENTER) {
     const int b0 = __builtin_amdgcn_readfirstlane((int)((off >> 6) / bpb));
     const int nbl = (int)gridDim.x / bpb;  // bands in this launch
     const int kb = (int)blockIdx.x / bpb;
@@ -487,7 +509,6 @@ __device__ __forceinline__ void mandel_blk8m(const float* view, const int* size,
   }
   const int l = threadIdx.x;
   const int r = l >> 3, c2 = (l & 7) * 2;
-  const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
   const float ci = y0 + (float)(band * 8 + r) * dy;
   const float crx = x0 + (float)(blk * 16 + c2) * dx;
   const f32x2 cr = {crx, crx + dx}, civ = {ci, ci};
@@ -508,4 +529,10 @@ extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8t_f32(const 
 extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8u_f32(const float* view, const int* size,
                                                                         int2* out, CEK_HIDDEN) {
   mandel_blk8m<32, 32, true, true>(view, size, out, __cek_off);
+}
+
+// blk8u with the short prologue (FASTPRO)
+extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8r_f32(const float* view, const int* size,
+                                                                        int2* out, CEK_HIDDEN) {
+  mandel_blk8m<32, 32, true, true, true>(view, size, out, __cek_off);
 }

@@ -181,7 +181,7 @@ def test_gemm_wave_granularity_two_logical_devices():
     assert GemmBf16(256, 256, 64, devices=g0, tile="256x256pb").granularity() == 512  # < 1 wave: per tile
 
 
-@pytest.mark.parametrize("kernel", ["quad", "blk8", "blk8h", "blk8k", "blk8m", "blk8t", "blk8u"])
+@pytest.mark.parametrize("kernel", ["quad", "blk8", "blk8h", "blk8k", "blk8m", "blk8t", "blk8u", "blk8r"])
 def test_mandelbrot_event_pipeline_matches_numpy(kernel):
     from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
 
@@ -192,12 +192,15 @@ def test_mandelbrot_event_pipeline_matches_numpy(kernel):
     assert mism < 0.01, mism
 
 
-@pytest.mark.parametrize("kernel", ["blk8h", "blk8k", "blk8m", "blk8t", "blk8u"])
-@pytest.mark.parametrize("shape", [(1024, 1024, 256), (512, 256, 60), (256, 128, 5), (512, 256, 100)])
+@pytest.mark.parametrize("kernel", ["blk8h", "blk8k", "blk8m", "blk8t", "blk8u", "blk8r"])
+@pytest.mark.parametrize("shape", [(1024, 1024, 256), (512, 256, 60), (256, 128, 5), (512, 256, 100),
+                                   (768, 128, 60)])
 def test_mandelbrot_blk8k_matches_numpy(shape, kernel):
     """blk8k's exactly counted first block, early-exit waves, the 4-op
     iteration and the skipped counting pass (max_iter a multiple of 8, not
-    a multiple, and below one block) against the float32 numpy reference."""
+    a multiple, and below one block) against the float32 numpy reference;
+    width 768 (48 blocks per band, not a power of two) takes blk8r's
+    division path."""
     from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
 
     w, h, it = shape
@@ -371,7 +374,7 @@ def test_mandelbrot_two_frames_in_flight_async_enqueue():
     from cekirdekler_amd.ops.library import library
 
     cr = ck.ClNumberCruncher(_gpu()[0], "", prebuilt=library("mandelbrot"), queue_concurrency=2)
-    ms = [MandelbrotRenderer(1024, 512, max_iter=100, cruncher=cr, kernel="blk8u") for _ in range(2)]
+    ms = [MandelbrotRenderer(1024, 512, max_iter=100, cruncher=cr, kernel="blk8r") for _ in range(2)]
     for i, m in enumerate(ms):
         m.render(i + 1, pipeline=False)
         m.out.write = False

@@ -10,7 +10,7 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES" \
            "SQ_ACTIVE_INST_VALU SQ_INSTS_SALU"; do
   i=$((i+1))
-  timeout -k 10 120 rocprofv3 --kernel-trace --pmc $set -d gpurun_out/mandel_pmc$i -o run --output-format csv \
+  timeout -k 10 120 rocprofv3 --pmc $set -d gpurun_out/mandel_pmc$i -o run --output-format csv \
       -- python3 tools/valu_pmc.py > gpurun_out/mandel_pmc$i.log 2>&1
   rc=$?
   echo "pass $i rc=$rc"
