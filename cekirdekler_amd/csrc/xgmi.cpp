@@ -42,6 +42,30 @@ hipFunction_t copy_fn(int ordinal) {
   return p->gpu_fn("cek_copy16_d2d");
 }
 
+std::map<std::pair<int, int>, bool> g_access;  // (accessing GPU, owning GPU) -> peer access on
+
+// Whether a kernel on GPU `a` may dereference memory of GPU `b`: peer access
+// enabled (once per pair).  A copy kernel that touched another GPU's memory
+// without it would fault, and a fault can reset every GPU of the node.
+bool kernel_can_reach(int a, int b) {
+  if (a == b) return true;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = g_access.find({a, b});
+    if (it != g_access.end()) return it->second;
+  }
+  const auto m = enable_peer_access_among({a, b});
+  const bool ok = m[0][1] != 0;
+  std::lock_guard<std::mutex> g(g_mu);
+  g_access[{a, b}] = ok;
+  g_access[{b, a}] = m[1][0] != 0;
+  return ok;
+}
+
+bool kernel_engine_ok(int ordinal, int src_dev, int dst_dev) {
+  return kernel_can_reach(ordinal, src_dev) && kernel_can_reach(ordinal, dst_dev);
+}
+
 void launch_copy(int ordinal, void* dst, const void* src, uint64_t bytes, hipStream_t s) {
   // whole 16-byte vectors by the kernel, a ragged tail (if any) by SDMA
   const uint64_t body = bytes & ~uint64_t(15);
@@ -101,7 +125,9 @@ struct DevBuf {
 int peer_copy(void* dst, int dst_dev, const void* src, int src_dev, uint64_t bytes, hipStream_t s,
               int stream_ordinal) {
   if (!bytes) return kCopySdma;
-  const int e = choose_engine(src_dev, dst_dev, bytes);
+  int e = choose_engine(src_dev, dst_dev, bytes);
+  // the kernel runs on the stream's GPU and dereferences both ends
+  if (e == kCopyKernel && !kernel_engine_ok(stream_ordinal, src_dev, dst_dev)) e = kCopySdma;
   if (e == kCopyKernel)
     launch_copy(stream_ordinal, dst, src, bytes, s);
   else
@@ -116,6 +142,9 @@ CopyMeasure measure_copy(int src, int dst, uint64_t bytes, int engine, int reps,
   (void)hipGetDevice(&cur);
   if (src != dst) enable_peer_access_among({src, dst});
   const int so = stream_ordinal >= 0 ? stream_ordinal : dst;
+  if (engine == kCopyKernel && !kernel_engine_ok(so, src, dst))
+    throw Error("measure_copy: no peer access for a copy kernel on GPU " + std::to_string(so) + " between GPUs " +
+                std::to_string(src) + " and " + std::to_string(dst));
   CopyMeasure m;
   m.src = src;
   m.dst = dst;
@@ -173,6 +202,10 @@ ConcurrentMeasure measure_all_pairs(const std::vector<int>& ords, uint64_t bytes
   (void)hipGetDevice(&cur);
   enable_peer_access_among(ords);
   const int n = static_cast<int>(ords.size());
+  if (engine == kCopyKernel)
+    for (int d = 0; d < n; ++d)
+      for (int s = 0; s < n; ++s)
+        if (!kernel_can_reach(ords[d], ords[s])) return cm;  // not measurable: verified stays false
   reps = std::max(1, reps);
   std::vector<std::unique_ptr<DevBuf>> src(n);
   std::vector<std::vector<std::unique_ptr<DevBuf>>> dst(n);
@@ -249,8 +282,13 @@ void calibrate(const std::vector<int>& ords, const std::vector<uint64_t>& sizes,
     for (int d : ords)
       for (uint64_t b : sizes) {
         const CopyMeasure a = measure_copy(s, d, b, kCopySdma, reps);
+        if (!a.verified) throw Error("calibrate: a measured copy did not verify");
+        if (!kernel_engine_ok(d, s, d)) {  // no peer access: SDMA only
+          t[{s, d}][b] = kCopySdma;
+          continue;
+        }
         const CopyMeasure k = measure_copy(s, d, b, kCopyKernel, reps);
-        if (!a.verified || !k.verified) throw Error("calibrate: a measured copy did not verify");
+        if (!k.verified) throw Error("calibrate: a measured copy did not verify");
         t[{s, d}][b] = k.gbps > a.gbps ? kCopyKernel : kCopySdma;
       }
   std::lock_guard<std::mutex> g(g_mu);
