@@ -316,6 +316,32 @@ __device__ __forceinline__ void mandel_steps_asm(f32x2& zr, f32x2& zi, const f32
                  : "+v"(zr), "+v"(zi), "=&v"(a), "=&v"(t) : "v"(cr), "v"(civ));
 }
 
+// N steps from (sr, si) into (dr, di), leaving (sr, si) intact: the first
+// step reads the source pair and writes the destination pair, the other
+// N − 1 run in place on the destination (same hand order and spacing as
+// above).  The all-bounded fast path ping-pongs between two pairs with it, so
+// the block's start z stays available as the checkpoint without a copy.
+#define CEK_MANDEL_STEP_FROM                                               \
+  "v_pk_fma_f32 %2, %6, %6, %4\n\t"                                       \
+  "v_pk_mul_f32 %3, %6, %7\n\t"                                           \
+  "v_pk_fma_f32 %0, %7, %7, %2 neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"         \
+  "v_pk_fma_f32 %1, %3, 2.0, %5 op_sel_hi:[1,0,1]\n\t"
+#define CEK_MANDEL_STEP2 CEK_MANDEL_STEP CEK_MANDEL_STEP
+#define CEK_MANDEL_STEP7 CEK_MANDEL_STEP4 CEK_MANDEL_STEP2 CEK_MANDEL_STEP
+template <int N>
+__device__ __forceinline__ void mandel_steps_from_asm(const f32x2 sr, const f32x2 si, f32x2& dr, f32x2& di,
+                                                      const f32x2 cr, const f32x2 civ) {
+  static_assert(N == 8 || N == 32, "8 or 32 steps");
+  f32x2 a, t;
+  if constexpr (N == 8)
+    asm volatile("s_nop 0\n\t" CEK_MANDEL_STEP_FROM CEK_MANDEL_STEP7 "s_nop 0"
+                 : "=&v"(dr), "=&v"(di), "=&v"(a), "=&v"(t) : "v"(cr), "v"(civ), "v"(sr), "v"(si));
+  else
+    asm volatile("s_nop 0\n\t" CEK_MANDEL_STEP_FROM CEK_MANDEL_STEP7 CEK_MANDEL_STEP4 CEK_MANDEL_STEP4
+                 CEK_MANDEL_STEP4 CEK_MANDEL_STEP4 CEK_MANDEL_STEP4 CEK_MANDEL_STEP4 "s_nop 0"
+                 : "=&v"(dr), "=&v"(di), "=&v"(a), "=&v"(t) : "v"(cr), "v"(civ), "v"(sr), "v"(si));
+}
+
 // N counted iterations (|z|² checked and counted every step), ordered so
 // that every result is read at least two instructions after it is written:
 //   q = zi·zi; t = zr·zi; m = zr·zr + q; a = zr·zr + cr; tc = clamp(m·nbig + cbig);
@@ -348,9 +374,10 @@ __device__ __forceinline__ void mandel_counted_asm(f32x2& zr, f32x2& zi, f32x2& 
 #undef CEK_MANDEL_COUNT_ARGS
 }
 
-template <int BIG, int S, bool ASM>
+template <int BIG, int S, bool ASM, bool FAST = false>
 __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ, const int max_iter) {
   static_assert(BIG % 8 == 0 && S % 8 == 0 && S >= 8, "block lengths are multiples of 8");
+  static_assert(!FAST || ASM, "the all-bounded fast path uses the hand-ordered blocks");
   const f32x2 two = {2.f, 2.f};
   const f32x2 nbig = {-1048576.f, -1048576.f}, cbig = {4194304.f, 4194304.f};
   f32x2 zr = {0.f, 0.f}, zi = {0.f, 0.f}, cnt = {0.f, 0.f}, tc = {1.f, 1.f};
@@ -421,6 +448,72 @@ __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ
   };
   int it = 8;
   bool live = true;
+  if constexpr (FAST) {
+    // While EVERY lane is still bounded (set-interior waves: ~90 % of the
+    // work on views centred on the set) no lane needs a checkpoint of its
+    // own: the blocks alternate between two z pairs, so the block's start z
+    // is the checkpoint without a copy, and the block start is every lane's
+    // last bounded iteration.  Per block that is |z|² and two compares
+    // instead of |z|², two compares, a move and six selects.  The first
+    // escape hands per-lane checkpoints to the general loops below, which go
+    // on from the same block boundary.
+    if ((ballot(dx1) | ballot(dy1)) == 0) {
+      // the loop carries (ar, ai) only; (br, bi) lives between its halves
+      f32x2 ar = zr, ai = zi, br, bi;
+      bool rem = false, second = false;
+      for (;;) {
+        int L = it < S ? 8 : BIG;
+        if (it + L > max_iter) {
+          rem = true;
+          break;
+        }
+        if (L == 8)
+          mandel_steps_from_asm<8>(ar, ai, br, bi, cr, civ);
+        else
+          mandel_steps_from_asm<BIG>(ar, ai, br, bi, cr, civ);
+        f32x2 m = __builtin_elementwise_fma(br, br, bi * bi);
+        it += L;
+        if (!all_lanes(ballot(m.x <= 4.f) & ballot(m.y <= 4.f))) break;
+        L = it < S ? 8 : BIG;
+        if (it + L > max_iter) {
+          rem = second = true;
+          break;
+        }
+        if (L == 8)
+          mandel_steps_from_asm<8>(br, bi, ar, ai, cr, civ);
+        else
+          mandel_steps_from_asm<BIG>(br, bi, ar, ai, cr, civ);
+        m = __builtin_elementwise_fma(ar, ar, ai * ai);
+        it += L;
+        if (!all_lanes(ballot(m.x <= 4.f) & ballot(m.y <= 4.f))) {
+          second = true;
+          break;
+        }
+      }
+      // `second`: the last block ran from (br, bi) into (ar, ai)
+      const f32x2 sr = second ? br : ar, si = second ? bi : ai;  // the block's start z
+      const f32x2 dr = second ? ar : br, di = second ? ai : bi;  // its end z
+      if (rem) {  // every lane bounded at `it` (= the block start here); the rest is counted below
+        fr = zr = second ? br : ar;  // the z every lane has at `it`
+        fi = zi = second ? bi : ai;
+        ex = ey = it;
+        live = false;
+      } else {  // the first escapes: per-lane checkpoints from here on
+        const int L = (it - 8) < S ? 8 : BIG;  // the length of the block that just ran
+        const f32x2 m = __builtin_elementwise_fma(dr, dr, di * di);
+        const bool kx = m.x <= 4.f, ky = m.y <= 4.f;
+        fr.x = kx ? dr.x : sr.x;
+        fi.x = kx ? di.x : si.x;
+        ex = kx ? it : it - L;
+        fr.y = ky ? dr.y : sr.y;
+        fi.y = ky ? di.y : si.y;
+        ey = ky ? it : it - L;
+        zr = dr;
+        zi = di;
+        live = (ballot(kx) | ballot(ky)) != 0;
+      }
+    }
+  }
   for (; live && it < S && it + 8 <= max_iter; it += 8) {
     if constexpr (ASM) {
       mandel_steps_asm<8>(zr, zi, cr, civ);
@@ -474,7 +567,7 @@ __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ
 // work-group index with shifts instead of three scalar integer divisions
 // (~100 dependent SALU instructions per wave in the compiler's expansion);
 // other widths keep the division.
-template <int BIG, int S, bool ASM, bool CENTER = false, bool FASTPRO = false>
+template <int BIG, int S, bool ASM, bool CENTER = false, bool FASTPRO = false, bool FAST = false>
 __device__ __forceinline__ void mandel_blk8m(const float* view, const int* size, int2* out, long long off) {
   const int W = size[0], max_iter = size[2];
   const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
@@ -512,7 +605,7 @@ __device__ __forceinline__ void mandel_blk8m(const float* view, const int* size,
   const float ci = y0 + (float)(band * 8 + r) * dy;
   const float crx = x0 + (float)(blk * 16 + c2) * dx;
   const f32x2 cr = {crx, crx + dx}, civ = {ci, ci};
-  out[((long long)band * 4 * W + blk * 8) + r * (W >> 1) + (l & 7)] = mandel_blk8_core<BIG, S, ASM>(cr, civ, max_iter);
+  out[((long long)band * 4 * W + blk * 8) + r * (W >> 1) + (l & 7)] = mandel_blk8_core<BIG, S, ASM, FAST>(cr, civ, max_iter);
 }
 
 extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8m_f32(const float* view, const int* size,
@@ -535,4 +628,10 @@ extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8u_f32(const 
 extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8r_f32(const float* view, const int* size,
                                                                         int2* out, CEK_HIDDEN) {
   mandel_blk8m<32, 32, true, true, true>(view, size, out, __cek_off);
+}
+
+// blk8r with the all-bounded fast path (FAST)
+extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8y_f32(const float* view, const int* size,
+                                                                        int2* out, CEK_HIDDEN) {
+  mandel_blk8m<32, 32, true, true, true, true>(view, size, out, __cek_off);
 }

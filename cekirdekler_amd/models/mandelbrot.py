@@ -20,7 +20,7 @@ FLOP_PER_ITER = 8
 
 # kernel variants; the band kernels additionally need device and pipeline
 # chunk ranges made of whole 16-row bands (see kernels/mandelbrot.hip)
-BAND_ROWS = {"blk8": 8, "blk8h": 8, "blk8k": 8, "blk8m": 8, "blk8t": 8, "blk8u": 8, "blk8r": 8}  # rows per band
+BAND_ROWS = {"blk8": 8, "blk8h": 8, "blk8k": 8, "blk8m": 8, "blk8t": 8, "blk8u": 8, "blk8r": 8, "blk8y": 8}  # rows per band
 BAND_KERNELS = set(BAND_ROWS)
 KERNELS = {
     # name: (library kernel, pixels per work item, work-group size)
@@ -45,10 +45,13 @@ KERNELS = {
     # views centred on the set)
     "blk8u": ("cek_mandelbrot_blk8u_f32", 2, 64),
     # blk8u with a shorter per-wave prologue (loads issued together, shifts
-    # instead of scalar divisions for power-of-two widths): the fastest,
-    # bench.py's kernel-only number (51.2-51.7 % vs 49.8 % of FP32 peak on
-    # one stream, profiles/r5/README.md)
+    # instead of scalar divisions for power-of-two widths): 51.2-51.7 % vs
+    # 49.8 % of FP32 peak on one stream (profiles/r5/README.md)
     "blk8r": ("cek_mandelbrot_blk8r_f32", 2, 64),
+    # blk8r without per-lane checkpoints while every lane is bounded (two z
+    # pairs ping-ponged; bit-identical images): the fastest, bench.py's
+    # kernel-only number (53.6-53.8 % vs 52.5-52.8 % for blk8r)
+    "blk8y": ("cek_mandelbrot_blk8y_f32", 2, 64),
 }
 
 

@@ -29,7 +29,8 @@ LIBRARY = {
                   "cek_sgemm_f32_256x256g8q"],
     "mandelbrot": ["cek_mandelbrot_f32", "cek_mandelbrot_blk8_f32", "cek_mandelbrot_blk8h_f32",
                    "cek_mandelbrot_blk8k_f32", "cek_mandelbrot_blk8m_f32", "cek_mandelbrot_blk8t_f32",
-                   "cek_mandelbrot_blk8u_f32", "cek_mandelbrot_blk8r_f32"],
+                   "cek_mandelbrot_blk8u_f32", "cek_mandelbrot_blk8r_f32",
+                   "cek_mandelbrot_blk8y_f32"],
     "nbody": ["cek_nbody_f32_b2", "cek_nbody_integrate_f32_b2", "cek_nbody_energy_f32_b2",
               "cek_nbody_f32_b4", "cek_nbody_integrate_f32_b4", "cek_nbody_energy_f32_b4"],
     "reduce": ["cek_reduce_sum_f32", "cek_reduce_sum_f32_x32", "cek_reduce_sum_f32_final"],

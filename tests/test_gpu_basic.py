@@ -181,7 +181,7 @@ def test_gemm_wave_granularity_two_logical_devices():
     assert GemmBf16(256, 256, 64, devices=g0, tile="256x256pb").granularity() == 512  # < 1 wave: per tile
 
 
-@pytest.mark.parametrize("kernel", ["quad", "blk8", "blk8h", "blk8k", "blk8m", "blk8t", "blk8u", "blk8r"])
+@pytest.mark.parametrize("kernel", ["quad", "blk8", "blk8h", "blk8k", "blk8m", "blk8t", "blk8u", "blk8r", "blk8y"])
 def test_mandelbrot_event_pipeline_matches_numpy(kernel):
     from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
 
@@ -192,7 +192,7 @@ def test_mandelbrot_event_pipeline_matches_numpy(kernel):
     assert mism < 0.01, mism
 
 
-@pytest.mark.parametrize("kernel", ["blk8h", "blk8k", "blk8m", "blk8t", "blk8u", "blk8r"])
+@pytest.mark.parametrize("kernel", ["blk8h", "blk8k", "blk8m", "blk8t", "blk8u", "blk8r", "blk8y"])
 @pytest.mark.parametrize("shape", [(1024, 1024, 256), (512, 256, 60), (256, 128, 5), (512, 256, 100),
                                    (768, 128, 60)])
 def test_mandelbrot_blk8k_matches_numpy(shape, kernel):
@@ -209,6 +209,25 @@ def test_mandelbrot_blk8k_matches_numpy(shape, kernel):
     ref = m.reference()
     assert np.mean(img != ref) < 2e-3, np.mean(img != ref)
     m.cr.dispose()
+
+
+@pytest.mark.parametrize("shape", [(1024, 1024, 256), (1024, 512, 100), (512, 512, 60), (768, 256, 200)])
+@pytest.mark.parametrize("view", [(-2.0, -1.5, 3.0, 3.0), (-0.8, -0.2, 0.4, 0.4)])
+def test_mandelbrot_fast_path_equals_general(shape, view):
+    """blk8y (no per-lane checkpoints while every lane is bounded, z pairs
+    ping-ponged) computes the same z sequence and checkpoints as blk8r:
+    images bit-identical, on the default view and on a zoom that is mostly
+    set interior, with max_iter a multiple of the block, not one, and below
+    the first 32-step block."""
+    from cekirdekler_amd.models.mandelbrot import MandelbrotRenderer
+
+    w, h, it = shape
+    imgs = []
+    for k in ("blk8r", "blk8y"):
+        m = MandelbrotRenderer(w, h, max_iter=it, view=view, devices=_gpu()[0], kernel=k)
+        imgs.append(m.render(pipeline=False).copy())
+        m.cr.dispose()
+    assert np.array_equal(imgs[0], imgs[1]), int((imgs[0] != imgs[1]).sum())
 
 
 @pytest.mark.parametrize("kernel,per_item", [("cek_reduce_sum_f32", 8), ("cek_reduce_sum_f32_x32", 32)])
@@ -374,7 +393,7 @@ def test_mandelbrot_two_frames_in_flight_async_enqueue():
     from cekirdekler_amd.ops.library import library
 
     cr = ck.ClNumberCruncher(_gpu()[0], "", prebuilt=library("mandelbrot"), queue_concurrency=2)
-    ms = [MandelbrotRenderer(1024, 512, max_iter=100, cruncher=cr, kernel="blk8r") for _ in range(2)]
+    ms = [MandelbrotRenderer(1024, 512, max_iter=100, cruncher=cr, kernel="blk8y") for _ in range(2)]
     for i, m in enumerate(ms):
         m.render(i + 1, pipeline=False)
         m.out.write = False

@@ -25,7 +25,7 @@ rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 7
 frames = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 gpu = ck.ClPlatforms.all().gpus()[0]
 cr = ck.ClNumberCruncher(gpu, "", prebuilt=library("mandelbrot"), queue_concurrency=2)
-ms = [MandelbrotRenderer(4096, 4096, 256, cruncher=cr, kernel="blk8r") for _ in range(2)]
+ms = [MandelbrotRenderer(4096, 4096, 256, cruncher=cr, kernel="blk8y") for _ in range(2)]
 for i, m in enumerate(ms):
     m.render(i + 1, pipeline=False)
 flops = ms[0].flops()
