@@ -374,7 +374,9 @@ __device__ __forceinline__ void mandel_counted_asm(f32x2& zr, f32x2& zi, f32x2& 
 #undef CEK_MANDEL_COUNT_ARGS
 }
 
-template <int BIG, int S, bool ASM, bool FAST = false>
+// FAST: 0 = per-lane checkpoints after every block; 1 = none while every
+// lane is bounded (blk8y)
+template <int BIG, int S, bool ASM, int FAST = 0>
 __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ, const int max_iter) {
   static_assert(BIG % 8 == 0 && S % 8 == 0 && S >= 8, "block lengths are multiples of 8");
   static_assert(!FAST || ASM, "the all-bounded fast path uses the hand-ordered blocks");
@@ -448,7 +450,7 @@ __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ
   };
   int it = 8;
   bool live = true;
-  if constexpr (FAST) {
+  if constexpr (FAST == 1) {
     // While EVERY lane is still bounded (set-interior waves: ~90 % of the
     // work on views centred on the set) no lane needs a checkpoint of its
     // own: the blocks alternate between two z pairs, so the block's start z
@@ -567,7 +569,7 @@ __device__ __forceinline__ int2 mandel_blk8_core(const f32x2 cr, const f32x2 civ
 // work-group index with shifts instead of three scalar integer divisions
 // (~100 dependent SALU instructions per wave in the compiler's expansion);
 // other widths keep the division.
-template <int BIG, int S, bool ASM, bool CENTER = false, bool FASTPRO = false, bool FAST = false>
+template <int BIG, int S, bool ASM, bool CENTER = false, bool FASTPRO = false, int FAST = 0>
 __device__ __forceinline__ void mandel_blk8m(const float* view, const int* size, int2* out, long long off) {
   const int W = size[0], max_iter = size[2];
   const float x0 = view[0], y0 = view[1], dx = view[2], dy = view[3];
@@ -633,5 +635,6 @@ extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8r_f32(const 
 // blk8r with the all-bounded fast path (FAST)
 extern "C" __global__ __launch_bounds__(64) void cek_mandelbrot_blk8y_f32(const float* view, const int* size,
                                                                         int2* out, CEK_HIDDEN) {
-  mandel_blk8m<32, 32, true, true, true, true>(view, size, out, __cek_off);
+  mandel_blk8m<32, 32, true, true, true, 1>(view, size, out, __cek_off);
 }
+
