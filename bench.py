@@ -735,8 +735,8 @@ def compact_extra(full: dict, detail: str) -> dict:
         ex["pipeline_overlap"] = p
     bt = full.get("broadcast_threshold")
     if isinstance(bt, dict):
-        ex["broadcast_threshold"] = _pick(bt, ["devices", "logical", "crossover_bytes", "sizes", "direct_ms",
-                                               "staged_ms", "exact"], 4)
+        ex["broadcast_threshold"] = _pick(bt, ["devices", "logical", "crossover_bytes", "runtime_adopted_min_bytes",
+                                               "sizes", "direct_ms", "staged_ms", "exact"], 4)
     tp = full.get("task_pool")
     if isinstance(tp, dict):
         t = _pick(tp, ["tasks", "pool_devices", "cu_partitioned", "makespan_ms", "ideal_ms_sum_over_devices",

@@ -573,6 +573,34 @@ class ClNumberCruncher:
     def peer_read_min_bytes(self, n: int) -> None:
         self._cores.peer_read_min_bytes = int(n)
 
+    def calibrate_peer_reads(self, sizes=None, calls: int = 5, cached: bool = True) -> dict:
+        """Measure where the xGMI read fan-out starts to beat per-GPU uploads
+        on this cruncher's GPUs and set :attr:`peer_read_min_bytes` to it
+        (the broadcast / per-GPU upload choice by a
+        measured size threshold; the built-in 1 MiB is only the default).
+        The measurement runs on a temporary cruncher over the same devices
+        (``utils.multigpu.measure_peer_read_threshold``); the result is kept
+        per device set for the process (``cached``).  Fewer than two GPUs:
+        nothing to choose, the threshold is left as it is.  A fan-out that
+        never wins sets the threshold past every measured size."""
+        from .utils import multigpu
+
+        gpus = [d for d in self.devices if d.is_gpu]
+        if len(gpus) < 2:
+            return {"skipped": "fewer than two GPU devices", "peer_read_min_bytes": self.peer_read_min_bytes}
+        key = multigpu.device_set_key(gpus)
+        res = multigpu._PEER_READ_CACHE.get(key) if cached else None
+        if res is None:
+            res = multigpu.measure_peer_read_threshold(ClDevices(gpus), sizes or multigpu.PEER_READ_SIZES, calls)
+            if not res["exact"]:
+                raise RuntimeError("calibrate_peer_reads: a measured call produced a wrong output")
+            multigpu._PEER_READ_CACHE[key] = res
+        cross = res["crossover_bytes"]
+        self.peer_read_min_bytes = int(cross) if cross is not None else 2 * max(res["sizes"])
+        return {**res, "peer_read_min_bytes": self.peer_read_min_bytes}
+
+    calibratePeerReads = calibrate_peer_reads
+
     # ------------------------------------------------------------ compute
     def _validate(self, group: ClParameterGroup, names, G, L, pipeline, blobs) -> None:
         D = self.number_of_devices

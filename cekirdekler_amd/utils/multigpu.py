@@ -115,3 +115,91 @@ def peer_bandwidth_report(ordinals: Sequence[int], pair_bytes: int = 256 << 20, 
     if out["pairs"]:
         out["min_pair_gbps"] = min(max(r[k]["gbps"] for k in ENGINES) for r in out["pairs"])
     return out
+
+
+# --------------------------------------------- broadcast vs per-GPU upload threshold
+PEER_READ_SIZES = (65536, 262144, 1 << 20, 4 << 20, 16 << 20, 64 << 20, 256 << 20)
+_TOUCH_SRC = """
+__global__ void cek_touch(const float* x, float* y) {
+    long long i = get_global_id(0);
+    y[i] = x[i] * 2.0f + 1.0f;
+}
+"""
+# measured thresholds per device set (ordinals, CU partitions), for the process
+_PEER_READ_CACHE: dict = {}
+
+
+def pick_crossover(sizes: Sequence[int], direct_ms: Sequence[float], staged_ms: Sequence[float]) -> Optional[int]:
+    """The smallest size from which the staged fan-out stays faster than the
+    direct uploads at every larger size measured (None: never)."""
+    for i in range(len(sizes)):
+        if all(s < d for s, d in zip(staged_ms[i:], direct_ms[i:])):
+            return int(sizes[i])
+    return None
+
+
+def measure_peer_read_threshold(devices, sizes: Sequence[int] = PEER_READ_SIZES, calls: int = 5) -> dict:
+    """Time the two ways a full ``read`` array reaches every GPU of
+    ``devices`` ("choose by size threshold, measured"):
+    ``direct`` — every GPU uploads the whole array over its own PCIe link
+    (the reference, Worker.cs:833-860) — and ``staged`` — 1/D uploaded per
+    GPU, the rest pulled from the peers' replicas over xGMI
+    (``Cores::stage_peer_reads``).  A tiny kernel reads the array on every
+    GPU, so a call's time is the transfer; modes interleaved, median of
+    ``calls``, every output checked.  Returns the sizes, both timings,
+    ``crossover_bytes`` (:func:`pick_crossover`) and ``exact``."""
+    import statistics
+    import time
+
+    import numpy as np
+
+    from ..arrays import ClArray
+    from ..cruncher import ClNumberCruncher
+
+    cr = ClNumberCruncher(devices, _TOUCH_SRC)
+    if cr.error_code():
+        raise RuntimeError(cr.error_message())
+    D = cr.number_of_devices
+    try:
+        cr.peer_read_min_bytes = 0
+        G = 256 * D * 4
+        y = ClArray(np.zeros(G, np.float32))
+        y.read = False
+        out = {"devices": D, "calls": int(calls), "sizes": [], "direct_ms": [], "staged_ms": [],
+               "staged_path": [], "exact": True}
+        cid = 1
+        for size in sizes:
+            n = max(G, int(size) // 4)
+            x = ClArray(n, np.float32)
+            x.array[:] = np.arange(n, dtype=np.float32) % 1000
+            x.write = False
+            want = x.array[:G] * 2.0 + 1.0
+            times = {"direct": [], "staged": []}
+            for mode in ("direct", "staged"):  # untimed first calls: buffers, balancer state
+                cr.peer_reads = mode == "staged"
+                x.next_param(y).compute(cr, cid + (mode == "staged"), "cek_touch", G, 256)
+            for _ in range(max(1, int(calls))):
+                for mode in ("direct", "staged"):
+                    cr.peer_reads = mode == "staged"
+                    y.array[:] = 0
+                    t0 = time.perf_counter()
+                    x.next_param(y).compute(cr, cid + (mode == "staged"), "cek_touch", G, 256)
+                    times[mode].append((time.perf_counter() - t0) * 1e3)
+                    out["exact"] &= bool(np.array_equal(y.array, want))
+            out["sizes"].append(4 * n)
+            out["direct_ms"].append(round(statistics.median(times["direct"]), 4))
+            out["staged_ms"].append(round(statistics.median(times["staged"]), 4))
+            out["staged_path"].append(cr.last_record()["p2p_path"])
+            x.dispose()
+            cid += 2
+        y.dispose()
+    finally:
+        cr.dispose()
+    out["crossover_bytes"] = pick_crossover(out["sizes"], out["direct_ms"], out["staged_ms"])
+    return out
+
+
+def device_set_key(devices) -> tuple:
+    """(ordinal, CU partition) of every GPU in ``devices``: the cache key of a
+    measured threshold."""
+    return tuple((d.info.ordinal, d.cu_partition) for d in devices if d.is_gpu)

@@ -44,3 +44,25 @@ def test_cu_partitions_keep_cpu_devices():
     cpu = ck.ClPlatforms.all().cpus(True)
     assert len(cpu.cu_partitions(4)) == len(cpu)
     assert cpu.cu_partitions(4).device(0).cu_partition is None
+
+
+def test_pick_crossover():
+    """The measured broadcast / per-GPU upload threshold (SURVEY §5.8 item
+    3): the smallest size from which the staged fan-out stays faster."""
+    from cekirdekler_amd.utils.multigpu import pick_crossover
+
+    sizes = [1, 2, 4, 8]
+    assert pick_crossover(sizes, [1, 1, 1, 1], [2, 0.5, 0.5, 0.5]) == 2
+    assert pick_crossover(sizes, [1, 1, 1, 1], [0.5, 2, 0.5, 0.5]) == 4  # must STAY faster
+    assert pick_crossover(sizes, [1, 1, 1, 1], [0.5] * 4) == 1
+    assert pick_crossover(sizes, [1, 1, 1, 1], [2, 2, 2, 2]) is None
+
+
+def test_calibrate_peer_reads_needs_two_gpus():
+    import cekirdekler_amd as ck
+
+    cr = ck.ClNumberCruncher(ck.ClPlatforms.all().cpus(True), "__global__ void k(float* a) {}")
+    before = cr.peer_read_min_bytes
+    out = cr.calibrate_peer_reads()
+    assert "skipped" in out and cr.peer_read_min_bytes == before
+    cr.dispose()

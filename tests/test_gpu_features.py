@@ -802,3 +802,22 @@ def test_kernel_profiling_timestamps(gpu):
     assert all(0 < ms < wall for _, ms in kt), (kt, wall)
     assert cr.kernel_times(0) == []  # drained
     cr.dispose()
+
+
+@pytest.mark.gpu
+def test_calibrate_peer_reads_sets_measured_threshold():
+    """ClNumberCruncher.calibrate_peer_reads measures direct vs staged reads
+    by size on its GPUs (here two logical devices of GPU 0), checks every
+    output and adopts the crossover as peer_read_min_bytes."""
+    import cekirdekler_amd as ck
+    from cekirdekler_amd.utils import multigpu
+
+    g = ck.ClPlatforms.all().gpus()
+    cr = ck.ClNumberCruncher(g[0] + g[0], "__global__ void k(float* a) {}")
+    sizes = [65536, 1 << 20, 8 << 20]
+    out = cr.calibrate_peer_reads(sizes=sizes, calls=2, cached=False)
+    assert out["exact"] and len(out["direct_ms"]) == len(sizes) == len(out["staged_ms"])
+    want = out["crossover_bytes"] if out["crossover_bytes"] is not None else 2 * max(out["sizes"])
+    assert cr.peer_read_min_bytes == want
+    assert multigpu.device_set_key([d for d in cr.devices]) in multigpu._PEER_READ_CACHE
+    cr.dispose()
