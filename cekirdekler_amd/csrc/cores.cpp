@@ -46,6 +46,7 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
   global_devices_ = static_cast<int>(workers_.size());
   spans_.resize(workers_.size());
   if (const char* e = std::getenv("CEK_DEVICE_SPANS")) device_spans = std::string(e) != "0";
+  if (const char* e = std::getenv("CEK_SINGLE_DEVICE_SPANS")) single_device_spans = std::string(e) == "1";
   if (const char* e = std::getenv("CEK_KERNEL_D2H")) set_kernel_d2h(std::string(e) != "0");
   if (const char* e = std::getenv("CEK_ZC_RELEASE")) zc_release = std::string(e) != "0";
   // CEK_SLEEP_WAITS=1: GPU workers wait for their streams by sleeping on a
@@ -873,7 +874,11 @@ void Cores::launch_kernels_body(Worker& wk, hipStream_t s, const ComputeCall& c,
 // Enqueue mode with one device in the whole job: nothing to balance, so no
 // span events between the back-to-back computes (the host clock times the
 // enqueued batch when the mode is left).
-bool Cores::spans_on() const { return device_spans && !(enqueue_mode_ && global_devices_ == 1); }
+// One device in the whole job: there is no split to balance, so its compute
+// time is the host's stopwatch (the reference's clock, Worker.cs:779-807)
+// and no span events go into its streams (two event records and an elapsed-
+// time query per synchronous compute).  CEK_SINGLE_DEVICE_SPANS=1 keeps them.
+bool Cores::spans_on() const { return device_spans && (global_devices_ > 1 || single_device_spans); }
 
 // An enqueued batch gets one span per device (opened by its first compute,
 // closed when the mode is left) when no two local devices share a GPU: one
@@ -938,7 +943,7 @@ void Cores::span_end(Worker& wk, hipStream_t s) {
 
 double Cores::span_ms(int w) {
   DevSpans& d = spans_[w];
-  if (!device_spans || d.pool.empty()) return -1.0;
+  if (!spans_on() || d.pool.empty()) return -1.0;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, d.pool[0].first, d.pool[0].second) != hipSuccess) {
     (void)hipGetLastError();

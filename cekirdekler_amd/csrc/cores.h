@@ -484,6 +484,7 @@ class Cores {
   std::vector<DevSpans> spans_;
  public:
   bool device_spans = true;  // CEK_DEVICE_SPANS=0: host wall clock instead
+  bool single_device_spans = false;  // spans with one device in the job too (CEK_SINGLE_DEVICE_SPANS=1)
   // a system-scope release marker after kernels that may store into
   // zero-copy host memory (per compute in sync mode, once per batch when
   // enqueue mode is left); CEK_ZC_RELEASE=0 turns it off
