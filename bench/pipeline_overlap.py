@@ -92,11 +92,16 @@ def main():
     y = ck.ClArray(n, np.uint32)
     y.read = False
 
-    crs = {"q4": ck.ClNumberCruncher(dev, SRC), "q16": ck.ClNumberCruncher(dev, SRC, queue_concurrency=16)}
+    # the default compute-stream count (hardware queues minus the main
+    # stream's, hardware.async_queue_count), one per hardware queue (4) and
+    # the reference's 16
+    crs = {"qd": ck.ClNumberCruncher(dev, SRC), "q4": ck.ClNumberCruncher(dev, SRC, queue_concurrency=4),
+           "q16": ck.ClNumberCruncher(dev, SRC, queue_concurrency=16)}
     for cr in crs.values():
         if cr.error_code():
             raise SystemExit(cr.error_message())
-    cr = crs["q4"]
+    cr = crs["qd"]
+    qd = cr.compute_queue_concurrency
     cid = iter(range(1, 1000))
 
     def call(c, compute_id, pipeline=False, ptype=ck.PIPELINE_EVENT, nb=1):
@@ -139,11 +144,12 @@ def main():
     want = expected(x.array, iters)
 
     # ---- configs --------------------------------------------------------------
-    configs = [("3phase", lambda c, i: call(crs["q4"], i), None)]
+    configs = [("3phase", lambda c, i: call(crs["qd"], i), None)]
     for b in blobs:
-        configs.append((f"event_b{b}", lambda c, i, b=b: call(crs["q4"], i, True, ck.PIPELINE_EVENT, b), None))
+        configs.append((f"event_b{b}", lambda c, i, b=b: call(crs["qd"], i, True, ck.PIPELINE_EVENT, b), None))
         configs.append((f"event_b{b}_4streams", lambda c, i, b=b: call(crs["q16"], i, True, ck.PIPELINE_EVENT, b),
                         "writes_one_stream"))
+        configs.append((f"driver_b{b}_qd", lambda c, i, b=b: call(crs["qd"], i, True, ck.PIPELINE_DRIVER, b), None))
         configs.append((f"driver_b{b}_q4", lambda c, i, b=b: call(crs["q4"], i, True, ck.PIPELINE_DRIVER, b), None))
         configs.append((f"driver_b{b}_q16", lambda c, i, b=b: call(crs["q16"], i, True, ck.PIPELINE_DRIVER, b), None))
     ids = {name: next(cid) for name, _, _ in configs}
@@ -165,7 +171,7 @@ def main():
         y.array[:] = 0
         run(name, fn, layout)
         exact[name] &= bool(np.array_equal(y.array, want))
-        c = crs["q16"] if ("q16" in name or layout) else crs["q4"]
+        c = crs["q16"] if ("q16" in name or layout) else (crs["q4"] if name.endswith("_q4") else crs["qd"])
         rec = c.last_record()
         piped[name] = bool(rec["pipelined"])
         moved[name] = [int(rec["h2d_bytes"]), int(rec["d2h_bytes"])]
@@ -178,7 +184,8 @@ def main():
     base = res["3phase"]
     ev = min((k for k in res if k.startswith("event_") and not k.endswith("4streams")), key=res.get)
     ev4 = min((k for k in res if k.endswith("4streams")), key=res.get)
-    dq4 = min((k for k in res if k.startswith("driver_") and k.endswith("q4")), key=res.get)
+    dqd = min((k for k in res if k.startswith("driver_") and k.endswith("_qd")), key=res.get)
+    dq4 = min((k for k in res if k.startswith("driver_") and k.endswith("_q4")), key=res.get)
     dq16 = min((k for k in res if k.endswith("q16")), key=res.get)
     parts = [up_ms, kernel_ms, down_ms]
     out = {
@@ -192,11 +199,13 @@ def main():
         "same_bytes_every_config": len({tuple(v) for v in moved.values()}) == 1,
         "h2d_d2h_bytes_per_call": moved.get("3phase"),
         "outputs_exact": all(exact.values()),
-        "best_event": ev, "best_event_4streams": ev4, "best_driver_q4": dq4, "best_driver_q16": dq16,
+        "default_compute_streams": qd,
+        "best_event": ev, "best_event_4streams": ev4, "best_driver_default": dqd, "best_driver_q4": dq4,
+        "best_driver_q16": dq16,
         "pipeline_speedup_event": round(base / min(res[ev], res[ev4]), 3),
-        "pipeline_speedup_driver": round(base / min(res[dq4], res[dq16]), 3),
+        "pipeline_speedup_driver": round(base / min(res[dqd], res[dq4], res[dq16]), 3),
         "event_5_vs_4_streams": [res[ev], res[ev4]],
-        "driver_q4_vs_q16": [res[dq4], res[dq16]],
+        "driver_default_q4_q16": [res[dqd], res[dq4], res[dq16]],
         "timing": f"median of {a.rounds} interleaved rounds of {a.calls} calls per config",
     }
     for c in crs.values():

@@ -22,7 +22,7 @@ import numpy as np
 
 from ._native import cek, kernel_dir
 from .arrays import ClArray, ClParameterGroup, _register_cores, as_clarray
-from .hardware import ClDevices, ClPlatforms, hw_queue_count
+from .hardware import ClDevices, ClPlatforms, async_queue_count
 
 PIPELINE_EVENT = True    # Cores.PIPELINE_EVENT (Cores.cs:416-423)
 PIPELINE_DRIVER = False  # Cores.PIPELINE_DRIVER
@@ -167,9 +167,10 @@ class ClNumberCruncher:
                 "(GPU-resident child levels, see ClNumberCruncher.device_enqueue_errors)")
         cfg = cek.CoresConfig()
         # async-enqueue / driver-pipeline streams per device: one per hardware
-        # queue unless asked (the reference's fixed 16 aliases onto 4 queues)
+        # queue the main stream leaves free, unless asked (the reference's
+        # fixed 16 aliases onto 4 queues; hardware.async_queue_count)
         if queue_concurrency is None:
-            queue_concurrency = hw_queue_count()
+            queue_concurrency = async_queue_count()
         cfg.queue_concurrency = int(queue_concurrency)
         self._queue_concurrency = max(1, min(16, int(queue_concurrency)))
         cfg.no_pipelining = bool(no_pipelining)

@@ -446,6 +446,7 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("serial", &Cores::serial)
       .def_readwrite("peer_reads", &Cores::peer_reads)
       .def_readwrite("device_spans", &Cores::device_spans)
+      .def_readwrite("deferred_downloads", &Cores::deferred_downloads)
       .def_readwrite("zc_release", &Cores::zc_release)
       .def_property("copy_cus", &Cores::copy_cus, &Cores::set_copy_cus)
       .def_readwrite("pipeline_writes_on_compute_stream", &Cores::pipeline_writes_on_compute_stream)

@@ -45,8 +45,11 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
   }
   global_devices_ = static_cast<int>(workers_.size());
   spans_.resize(workers_.size());
+  pending_d2h_.resize(workers_.size());
+  pending_span_end_.resize(workers_.size());
   if (const char* e = std::getenv("CEK_DEVICE_SPANS")) device_spans = std::string(e) != "0";
   if (const char* e = std::getenv("CEK_SINGLE_DEVICE_SPANS")) single_device_spans = std::string(e) == "1";
+  if (const char* e = std::getenv("CEK_DEFER_DOWNLOADS")) deferred_downloads = std::string(e) != "0";
   if (const char* e = std::getenv("CEK_KERNEL_D2H")) set_kernel_d2h(std::string(e) != "0");
   if (const char* e = std::getenv("CEK_ZC_RELEASE")) zc_release = std::string(e) != "0";
   // CEK_SLEEP_WAITS=1: GPU workers wait for their streams by sleeping on a
@@ -494,6 +497,7 @@ void Cores::capture_begin() {
   if (debug_checks_) throw Error("compute graphs cannot be captured with debug checks on (they synchronise)");
   for (auto& w : workers_) {
     w->wait();
+    flush_downloads(*w);
     w->sync_all();
   }
   cap_saved_ = {device_spans, peer_reads, async_enqueue, fine_grained, enqueue_mode_, record_timeline,
@@ -623,6 +627,7 @@ void Cores::finish() {
   if (capturing_) throw Error("finish() during a graph capture (end the capture first)");
   for (auto& w : workers_) {
     w->wait();
+    flush_downloads(*w);
     w->sync_all();
   }
   gather_pending_ = false;  // every gather copy (on the main streams) is done
@@ -642,6 +647,7 @@ void Cores::upload(int i, const ArraySpec& a) {
   std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   Worker& w = *workers_.at(i);
   w.set_device();
+  flush_downloads(w);
   hipStream_t s = w.main_stream();
   wait_gather(w, s);
   w.h2d(s, a, 0, a.bytes / a.elem_size);
@@ -652,6 +658,7 @@ void Cores::download(int i, const ArraySpec& a) {
   std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
   Worker& w = *workers_.at(i);
   w.set_device();
+  flush_downloads(w);
   hipStream_t s = w.main_stream();
   wait_gather(w, s);
   w.d2h(s, a, 0, a.bytes / a.elem_size);
@@ -874,11 +881,16 @@ void Cores::launch_kernels_body(Worker& wk, hipStream_t s, const ComputeCall& c,
 // Enqueue mode with one device in the whole job: nothing to balance, so no
 // span events between the back-to-back computes (the host clock times the
 // enqueued batch when the mode is left).
-// One device in the whole job: there is no split to balance, so its compute
-// time is the host's stopwatch (the reference's clock, Worker.cs:779-807)
-// and no span events go into its streams (two event records and an elapsed-
-// time query per synchronous compute).  CEK_SINGLE_DEVICE_SPANS=1 keeps them.
-bool Cores::spans_on() const { return device_spans && (global_devices_ > 1 || single_device_spans); }
+// Device-time span events only where they are read: every local device a
+// GPU (with a CPU device in the set all devices share the host clock, see
+// run_device_body) and more than one device in the whole job.  With one
+// device there is no split to balance, so its compute time is the host's
+// stopwatch (the reference's clock, Worker.cs:779-807) and no span events go
+// into its streams (two event records and an elapsed-time query per
+// synchronous compute).  CEK_SINGLE_DEVICE_SPANS=1 keeps them there.
+bool Cores::spans_on() const {
+  return device_spans && all_gpu_ && (global_devices_ > 1 || single_device_spans);
+}
 
 // An enqueued batch gets one span per device (opened by its first compute,
 // closed when the mode is left) when no two local devices share a GPU: one
@@ -1171,11 +1183,36 @@ static bool marker_needs_release(const ComputeCall& c) {
                      [](const ArraySpec& a) { return (a.zc && !a.ro) || (!a.zc && (a.write || a.write_all)); });
 }
 
+bool Cores::defer_downloads(const Worker& wk) const {
+  // not with markers (a task's marker must follow its own download, and a
+  // deferred one would wait for the next task), collectives, phase barriers
+  // or a graph capture
+  return deferred_downloads && wk.gpu() && enqueue_mode_ && async_enqueue && !fine_grained && !capturing_ &&
+         !phase_ && !comm_;
+}
+
+void Cores::flush_downloads(Worker& wk) {
+  const int w = worker_index(wk);
+  if (w < 0 || w >= static_cast<int>(pending_d2h_.size())) return;
+  auto& pd = pending_d2h_[w];
+  auto& ps = pending_span_end_[w];
+  if (pd.empty() && ps.empty()) return;
+  wk.set_device();
+  for (const auto& p : pd) wk.d2h(p.s, p.a, p.begin, p.count);
+  pd.clear();
+  DevSpans& d = spans_[w];
+  for (const auto& p : ps)
+    if (p.index >= 0 && p.index < static_cast<int>(d.pool.size())) CEK_HIP(hipEventRecord(d.pool[p.index].second, p.s));
+  ps.clear();
+}
+
 void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref, long long range,
                        uint64_t* h2d, uint64_t* d2h) {
   hipStream_t s = nullptr;
   if (wk.gpu())
     s = (enqueue_mode_ && async_enqueue) ? wk.compute_stream(wk.next_compute_queue()) : wk.main_stream();
+  const bool defer = defer_downloads(wk);
+  if (!defer) flush_downloads(wk);  // a compute that does not defer runs after every earlier download
   if (wk.gpu() && s != wk.main_stream()) wait_gather(wk, s);
   span_begin(wk, s);
   // across ranks: written slices all-gathered by RCCL (every written array
@@ -1202,6 +1239,9 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
     }
   }
   full_reads(wk, s, c, h2d);
+  // the earlier computes' downloads go into the copy queues after this
+  // compute's uploads
+  if (defer) flush_downloads(wk);
   // phase 2: kernels
   launch_kernels(wk, s, c, ref, range);
   if (call_gathers_ && wk.gpu()) {  // in-process gather: this device's kernels are enqueued
@@ -1246,26 +1286,41 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
       ds->gap = true;
     }
   }
-  // phase 3: device → host
+  // phase 3: device → host (deferred in async enqueue mode, see PendingD2H)
+  const int wi = defer ? worker_index(wk) : -1;
+  auto download = [&](const ArraySpec& a, uint64_t b, uint64_t n) {
+    if (wi >= 0)
+      pending_d2h_[wi].push_back({s, a, b, n});
+    else
+      wk.d2h(s, a, b, n);
+  };
+  bool deferred_any = false;
   for (size_t i = 0; i < c.arrays.size(); ++i) {
     const auto& a = c.arrays[i];
     if (a.zc || !a.write) continue;
+    deferred_any = wi >= 0;
     if (a.write_all) {
       if (static_cast<int>(i % global_devices_) == gidx) {
-        wk.d2h(s, a, 0, a.bytes / a.elem_size);
+        download(a, 0, a.bytes / a.elem_size);
         *d2h += a.bytes;
       }
     } else if (gathered(a)) {  // the replica holds every rank's slice
-      wk.d2h(s, a, 0, a.bytes / a.elem_size);
+      download(a, 0, a.bytes / a.elem_size);
       *d2h += a.bytes;
     } else {
       uint64_t b, n;
       a.slice(ref, range, c.local_range, b, n);
-      wk.d2h(s, a, b, n);
+      download(a, b, n);
       *d2h += n * a.elem_size;
     }
   }
-  span_end(wk, s);
+  if (deferred_any && wk.gpu() && spans_on()) {
+    // the span closes after the deferred download too
+    const DevSpans& d = spans_[wi];
+    pending_span_end_[wi].push_back({s, d.used - 1});
+  } else {
+    span_end(wk, s);
+  }
   if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(s);
   if (fine_grained) wk.add_marker(s, marker_needs_release(c));
   if (!enqueue_mode_ && wk.gpu()) wk.wait_stream(s, sleep_waits);
@@ -1526,6 +1581,7 @@ void Cores::run_device_body(int w, const ComputeCall& c, long long ref, long lon
   }
   if (range > 0) {
     wk.set_device();
+    if (pipelined) flush_downloads(wk);  // the pipelines' copies follow every earlier download
     if (!pipelined)
       run_3phase(wk, gidx, c, ref, range, h2d, d2h);
     else if (c.pipeline_event)

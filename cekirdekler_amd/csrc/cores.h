@@ -484,6 +484,9 @@ class Cores {
   std::vector<DevSpans> spans_;
  public:
   bool device_spans = true;  // CEK_DEVICE_SPANS=0: host wall clock instead
+  // async enqueue computes' downloads after the next compute's uploads
+  // (CEK_DEFER_DOWNLOADS=0: in each compute's own order)
+  bool deferred_downloads = true;
   bool single_device_spans = false;  // spans with one device in the job too (CEK_SINGLE_DEVICE_SPANS=1)
   // a system-scope release marker after kernels that may store into
   // zero-copy host memory (per compute in sync mode, once per batch when
@@ -497,6 +500,25 @@ class Cores {
   void span_end(Worker& wk, hipStream_t s);
   double span_ms(int w);              // sync mode: the last span (stream drained)
   double enqueue_spans_ms(int w);     // enqueue mode: union of the spans so far
+  // Async enqueue mode: a compute's downloads are issued after the NEXT
+  // compute's uploads (or when the batch ends).  A stream's copies go to an
+  // SDMA queue that other streams share and that runs in submission order:
+  // a download, which waits for its kernel, would hold back every later
+  // compute's upload behind it, and the computes would run one after the
+  // other instead of side by side (rocprofv3 trace, profiles/r5/README.md).
+  struct PendingD2H {
+    hipStream_t s;
+    ArraySpec a;
+    uint64_t begin, count;
+  };
+  struct PendingSpanEnd {
+    hipStream_t s;
+    int index;
+  };
+  std::vector<std::vector<PendingD2H>> pending_d2h_;          // per local device
+  std::vector<std::vector<PendingSpanEnd>> pending_span_end_;  // per local device
+  bool defer_downloads(const Worker& wk) const;
+  void flush_downloads(Worker& wk);
   ComputeRecord last_record_;
   CoresConfig cfg_;
 

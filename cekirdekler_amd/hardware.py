@@ -69,6 +69,23 @@ def hw_queue_count() -> int:
     return max(1, min(16, n))
 
 
+def async_queue_count() -> int:
+    """Default async-enqueue / driver-pipeline compute streams per device:
+    one per hardware queue the device's main stream leaves free,
+    ``hw_queue_count() - 1`` (at least 1).
+
+    HIP binds each new stream to a hardware queue: a new queue while the
+    pool has fewer than GPU_MAX_HW_QUEUES, afterwards an existing one.  The
+    main stream takes one, so with 4 queues a fourth compute stream lands on
+    the queue of a busy compute stream and the computes on those two run one
+    after the other — measured on MI355X (``tools/queue_map_probe.py``,
+    ``profiles/r5/README.md``): with 4 compute streams the computes on
+    streams 2 and 3 serialise, with 3 every consecutive pair runs side by
+    side, and a two-stage DevicePipeline overlaps its stages in every
+    window instead of in none."""
+    return max(1, hw_queue_count() - 1)
+
+
 class ClDevice:
     """One selectable device plus its selection flags."""
 

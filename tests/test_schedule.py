@@ -106,11 +106,13 @@ def test_explicit_blob_bounds_validated():
     cr.dispose()
 
 
-@pytest.mark.parametrize("hwq,want", [("4", 4), ("2", 2), ("", 4), ("64", 16)])
+@pytest.mark.parametrize("hwq,want", [("4", 3), ("2", 1), ("1", 1), ("", 3), ("64", 15)])
 def test_queue_concurrency_follows_hw_queues(monkeypatch, hwq, want):
-    """the default async / driver-pipeline queue count is
-    the GPU's hardware queue count (GPU_MAX_HW_QUEUES, 4 by default), and the
-    driver pipeline maps blob k to queue k mod that count."""
+    """the default async / driver-pipeline queue count
+    follows the GPU's hardware queue count (GPU_MAX_HW_QUEUES, 4 by default):
+    one compute stream per queue the main stream leaves free, so no two
+    compute streams share a queue (hardware.async_queue_count); the driver
+    pipeline maps blob k to queue k mod that count."""
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", hwq)
     cpu = ck.ClPlatforms.all().cpus(True)
     cr = ck.ClNumberCruncher(cpu, SRC)
