@@ -821,3 +821,44 @@ def test_calibrate_peer_reads_sets_measured_threshold():
     assert cr.peer_read_min_bytes == want
     assert multigpu.device_set_key([d for d in cr.devices]) in multigpu._PEER_READ_CACHE
     cr.dispose()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("defer", [True, False])
+def test_async_enqueue_deferred_downloads_correct(defer):
+    """Async enqueue mode issues a compute's downloads after the next
+    compute's uploads (Cores::flush_downloads): every result still reaches
+    its host array by the time the mode is left, for consecutive computes
+    on the rotating streams, a sync compute after the batch and an explicit
+    cr.download."""
+    import cekirdekler_amd as ck
+
+    g = ck.ClPlatforms.all().gpus()
+    src = "__global__ void k(const float* x, float* y) { long long i = get_global_id(0); y[i] = x[i] * 3.0f + 1.0f; }"
+    cr = ck.ClNumberCruncher(g[0], src)
+    cr.cores.deferred_downloads = defer
+    n = 1 << 16
+    xs = [ck.ClArray(np.arange(n, dtype=np.float32) + k) for k in range(5)]
+    ys = [ck.ClArray(np.zeros(n, np.float32)) for _ in range(5)]
+    for y in ys:
+        y.read = False
+    cr.enqueue_mode = True
+    cr.enqueue_mode_async_enable = True
+    for rep in range(2):
+        for k in range(5):
+            xs[k].array[:] = np.arange(n, dtype=np.float32) + k + 10 * rep
+            xs[k].next_param(ys[k]).compute(cr, 1 + k, "k", n, 256)
+    cr.enqueue_mode = False
+    cr.enqueue_mode_async_enable = False
+    for k in range(5):
+        np.testing.assert_array_equal(ys[k].array, (np.arange(n, dtype=np.float32) + k + 10) * 3.0 + 1.0)
+    # a synchronous compute right after an async batch
+    cr.enqueue_mode = True
+    cr.enqueue_mode_async_enable = True
+    xs[0].next_param(ys[0]).compute(cr, 1, "k", n, 256)
+    cr.enqueue_mode_async_enable = False
+    xs[1].next_param(ys[1]).compute(cr, 2, "k", n, 256)
+    cr.enqueue_mode = False
+    np.testing.assert_array_equal(ys[0].array, (np.arange(n, dtype=np.float32) + 10) * 3.0 + 1.0)
+    np.testing.assert_array_equal(ys[1].array, (np.arange(n, dtype=np.float32) + 11) * 3.0 + 1.0)
+    cr.dispose()
