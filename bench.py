@@ -624,6 +624,9 @@ def bench_node_configs(world: int) -> dict:
     configs.append(("hetero_stream", [sys.executable, "hetero_stream.py"]))
     # the reference's read/compute/write overlap claim on a balanced workload
     configs.append(("pipeline_overlap", [sys.executable, "pipeline_overlap.py"]))
+    # the reference's async-queue timeline: four independent computes on the
+    # async enqueue queues against one at a time
+    configs.append(("async_queues", [sys.executable, "async_queues.py"]))
     # xGMI fan-out vs per-GPU uploads of read arrays, by size
     configs.append(("broadcast_threshold", [sys.executable, "broadcast_threshold.py", "--gpus", str(world)]))
     t_start = time.monotonic()
@@ -734,6 +737,10 @@ def compact_extra(full: dict, detail: str) -> dict:
         if isinstance(po.get("ms"), dict):
             p["3phase_ms"] = po["ms"].get("3phase")
         ex["pipeline_overlap"] = p
+    aq = full.get("async_queues")
+    if isinstance(aq, dict):
+        ex["async_queues"] = _pick(aq, ["compute_streams", "ms_per_round_of_4", "async_speedup_over_sync",
+                                        "deferred_vs_inorder", "outputs_checked"])
     bt = full.get("broadcast_threshold")
     if isinstance(bt, dict):
         ex["broadcast_threshold"] = _pick(bt, ["devices", "logical", "crossover_bytes", "runtime_adopted_min_bytes",
