@@ -243,9 +243,10 @@ def test_device_pipeline_timeline_overlap_gpu(gpu):
         dp.add_stage(st)
     for _ in range(18):  # warm-up: both buffer parities and the first use of all 16 compute streams
         dp.feed()
-    # Streams share the process's 4 hardware queues; two stages whose streams
-    # land on one queue run back to back for that feed.  Take the best of a
-    # few measurement windows (the stages rotate over the 16 streams).
+    # The async compute streams get a hardware queue each (GPU_MAX_HW_QUEUES
+    # - 1 of them) and a stage's download is issued after the next stage's
+    # upload (the streams share an SDMA queue): the stages overlap in every
+    # window, first pipeline of a process included.  Best of a few windows.
     par, per_stage = 0.0, [0.0, 0.0]
     for _ in range(4):
         dp.record_timeline = True
