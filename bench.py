@@ -439,7 +439,7 @@ def _row_major_comparison(steps: int) -> dict:
     return out
 
 
-def _mandelbrot_kernel_only(kernel: str = "blk8y", reps: int = 20) -> dict:
+def _mandelbrot_kernel_only(kernel: str = "blk8y", reps: int = 40) -> dict:
     """The fastest Mandelbrot kernel alone on this rank's GPU (image left in
     device memory, no D2H, calls enqueued back to back in enqueue mode):
     BASELINE's "kernel >= 50 % of FP32 peak" target.
