@@ -100,3 +100,40 @@ def test_compact_line_fits_with_a_real_gpu_run(world):
     assert out["pipeline_overlap"]["pipeline_speedup_event"] == 2.1
     assert out["hetero_stream"]["iters_1"]["x_cpu"] > 1
     assert list(out)[-3:] == ["load_balance_iters", "mandelbrot_4k", "sgemm"]
+
+
+def test_run_child_reports_errors_and_kills_hung_children(tmp_path):
+    """The node configs and the peer topology run as children with their own
+    time limit: a child that fails or hangs becomes an ``error`` field (the
+    headline line is still printed), a hung child's whole process group is
+    killed, and the last JSON line of a good child is returned."""
+    bench = _bench_module()
+    env = bench._child_env()
+    good = bench._run_child([sys.executable, "-c", "print('noise'); print('{\"a\": 1}')"], env, 30)
+    assert good == {"a": 1}
+    bad = bench._run_child([sys.executable, "-c", "import sys; sys.exit(3)"], env, 30)
+    assert "exit 3" in bad["error"]
+    pidfile = tmp_path / "grandchild.pid"
+    hung = [sys.executable, "-c",
+            "import subprocess, sys, time; "
+            f"p = subprocess.Popen([sys.executable, '-c', 'import time; time.sleep(60)']); "
+            f"open({str(pidfile)!r}, 'w').write(str(p.pid)); time.sleep(60)"]
+    out = bench._run_child(hung, env, 3)
+    assert "error" in out and "Timeout" in out["error"]
+    pid = int(pidfile.read_text())
+    # the grandchild was in the child's session: killed with it
+    import time
+
+    def alive(p):
+        try:
+            with open(f"/proc/{p}/status") as f:  # a killed, not yet reaped process is a zombie
+                return not any(ln.startswith("State:") and "Z" in ln.split()[1] for ln in f)
+        except FileNotFoundError:
+            return False
+
+    for _ in range(50):
+        if not alive(pid):
+            break
+        time.sleep(0.1)
+    else:
+        pytest.fail("the hung child's grandchild survived")
