@@ -118,6 +118,13 @@ class WaveSurface:
         self.arguments.zero_copy = True
         self.t = 0.0
         self.ctr = 0.0
+        # the per-frame constants (Kamera.cs:256-264) go in once; a frame
+        # writes only ctr and t
+        args = self.arguments.array
+        args[2], args[3] = self.base["x"][0], self.base["y"][0]
+        args[4] = self.n
+        self._group = self.xyz.next_param(self.xyzn, self.xyzo, self.arguments)
+        self._first = True
 
     def update(self, compute_id: int = 1) -> np.ndarray:
         """One frame (Kamera.cs:199-275); returns the displaced vertices."""
@@ -126,12 +133,11 @@ class WaveSurface:
         self.t += 0.001
         args = self.arguments.array
         args[0], args[1] = self.ctr, self.t
-        args[2], args[3] = self.base["x"][0], self.base["y"][0]
-        args[4] = self.n
-        self.xyz.next_param(self.xyzn, self.xyzo, self.arguments).compute(
-            self.cr, compute_id, "waveEquation", self.range, self.local)
-        self.xyzn.read = False
-        self.xyz.read = False
+        self._group.compute(self.cr, compute_id, "waveEquation", self.range, self.local)
+        if self._first:  # base vertices and normals stay on the devices (Kamera.cs:271-272)
+            self.xyzn.read = False
+            self.xyz.read = False
+            self._first = False
         return self.vertices[:self.n]
 
     def reference(self) -> np.ndarray:
