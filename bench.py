@@ -529,34 +529,20 @@ def _mandelbrot_kernel_only(kernel: str = "blk8y", reps: int = 40) -> dict:
 
 
 def bench_lb_iters():
-    """Computes until every device share is within 5% of steady state, on two
-    logical devices of this GPU with an injected 2:1 slowdown (the reference
-    law converges as 0.7^k)."""
+    """Computes until device 0's share stays within 5% of its steady state
+    (the median of the last 10 of 40 calls), on two logical devices of this
+    GPU with an injected 2:1 slowdown (the reference law converges as 0.7^k;
+    SURVEY §7.4 item 3).  Run by rank 0 alone after the other ranks have
+    left, so no other process shares the host or the GPU
+    (``parallel.balancer.measure_lb_convergence``; the whole trajectory goes
+    to the detail file)."""
     import cekirdekler_amd as ck
+    from cekirdekler_amd.parallel.balancer import measure_lb_convergence
 
     plats = ck.ClPlatforms.all()
     gpus = plats.gpus()
     devs = (gpus[0] + gpus[0]) if len(gpus) else (plats.cpus(True) + plats.cpus(True))
-    # compute-heavy kernel so a device's time is proportional to its range
-    # (fixed launch/sync overheads would otherwise bias the steady state)
-    src = """__global__ void k(float* x){ long long i = get_global_id(0); float v = x[i];
-        for (int j = 0; j < 2048; ++j) v = v * 0.999f + 1.0f; x[i] = v; }"""
-    cr = ck.ClNumberCruncher(devs, src)
-    cr.cores.serial = True  # logical devices share one GPU: time them in isolation
-    cr.set_time_scale(1, 2.0)
-    n = 1 << 22
-    x = ck.ClArray(n, np.float32)
-    x.read = False
-    x.write = False
-    shares = []
-    for _ in range(40):
-        x.compute(cr, 7, "k", n, 256)
-        r = cr.ranges(7)
-        shares.append(r[0] / sum(r))
-    steady = shares[-1]
-    it = next(i for i in range(len(shares)) if all(abs(s - steady) <= 0.05 * steady for s in shares[i:]))
-    cr.dispose()
-    return {"iters": it + 1, "steady_share_dev0": steady}
+    return measure_lb_convergence(devs, calls=40, slow_device=1, slowdown=2.0)
 
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -871,7 +857,6 @@ def main(argv=None) -> int:
         sg = bench_sgemm_cpu(ctx, args.steps, args.warmup, min(args.size, 512))
     all_ranges = _all_ranges(ctx, sg["ranges"])
     mb = {} if (args.skip_mandelbrot or not use_gpu) else bench_mandelbrot(ctx, args.steps, args.warmup)
-    lb = bench_lb_iters() if (ctx.rank == 0 and use_gpu) else {}
     rowc = {}
     if ctx.rank == 0 and use_gpu and args.size == 8192:
         try:  # an extra: a failure is reported in its field
@@ -883,6 +868,7 @@ def main(argv=None) -> int:
 
         dist.barrier()
         dist.destroy_process_group()  # the other ranks exit here; rank 0 goes on alone
+    lb = bench_lb_iters() if (ctx.rank == 0 and use_gpu) else {}
     node = {} if (ctx.rank != 0 or args.skip_node_configs or not use_gpu) else bench_node_configs(ctx.world)
     peers = _peer_topology(ctx.world) if (ctx.rank == 0 and use_gpu) else {}
     ok = sg["max_rel_err"] <= MAX_REL_ERR

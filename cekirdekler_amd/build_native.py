@@ -28,7 +28,8 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("CEK_ARCH", "gfx950")
 
 SOURCES = ["device.cpp", "jit.cpp", "memory.cpp", "balancer.cpp", "worker.cpp", "dist.cpp",
-           "cores.cpp", "pool.cpp", "copy_engine.cpp", "shell_gemm.cpp", "xgmi.cpp", "probe.cpp", "bindings.cpp"]
+           "cores.cpp", "pool.cpp", "copy_engine.cpp", "shell_gemm.cpp", "xgmi.cpp", "probe.cpp", "refloops.cpp",
+           "bindings.cpp"]
 
 
 def ext_path() -> str:

@@ -22,7 +22,7 @@ import numpy as np
 
 from ._native import cek, kernel_dir
 from .arrays import ClArray, ClParameterGroup, _register_cores, as_clarray
-from .hardware import ClDevices, ClPlatforms, async_queue_count
+from .hardware import ClDevices, ClPlatforms, async_queue_count, mixed_cpu_policy
 
 PIPELINE_EVENT = True    # Cores.PIPELINE_EVENT (Cores.cs:416-423)
 PIPELINE_DRIVER = False  # Cores.PIPELINE_DRIVER
@@ -186,7 +186,15 @@ class ClNumberCruncher:
         if len(devices) == 0:
             self._error_code, self._error_message = 1, "no device selected"
             return
-        self._cores = cek.Cores([d.native_info() for d in devices], self.kernel_source, cfg)
+        # A CPU device next to GPUs shares the host with the GPU workers'
+        # threads: see mixed_cpu_policy
+        n_gpu = sum(1 for d in devices if d.is_gpu)
+        policy = mixed_cpu_policy() if (n_gpu and any(d.is_cpu for d in devices)) else "none"
+        reserve = n_gpu if policy in ("reserve", "both") else 0
+        self.mixed_cpu_policy = policy
+        self._cores = cek.Cores([d.native_info(reserve_threads=reserve) for d in devices], self.kernel_source, cfg)
+        if policy in ("sleep", "both"):
+            self._cores.sleep_waits = True
         self._error_code = self._cores.error_code
         self._error_message = self._cores.error_message
         if self._error_code:

@@ -13,6 +13,7 @@
 #include "memory.h"
 #include "pool.h"
 #include "probe.h"
+#include "refloops.h"
 #include "xgmi.h"
 
 namespace py = pybind11;
@@ -202,6 +203,12 @@ PYBIND11_MODULE(_cek, m) {
     py::gil_scoped_release r;
     copy_memory(reinterpret_cast<void*>(d), reinterpret_cast<const void*>(s), n);
   });
+
+  m.def("wave_reference_scalar", [](uint64_t base, uint64_t normals, uint64_t out, long long n, float ctr, float t) {
+    py::gil_scoped_release r;
+    wave_reference_scalar(reinterpret_cast<const float*>(base), reinterpret_cast<const float*>(normals),
+                          reinterpret_cast<float*>(out), n, ctr, t);
+  }, "the reference wave example's single-threaded scalar CPU loop (Kamera.cs:208-218); pointers to packed xyz floats");
 
   m.def("load_balance", [](std::vector<double> bench, bool smooth, std::vector<std::vector<double>> history,
                            long long total, std::vector<long long> ranges, long long step) {

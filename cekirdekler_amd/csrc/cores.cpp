@@ -47,6 +47,7 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
   spans_.resize(workers_.size());
   pending_d2h_.resize(workers_.size());
   pending_span_end_.resize(workers_.size());
+  order_events_.resize(workers_.size());
   if (const char* e = std::getenv("CEK_DEVICE_SPANS")) device_spans = std::string(e) != "0";
   if (const char* e = std::getenv("CEK_SINGLE_DEVICE_SPANS")) single_device_spans = std::string(e) == "1";
   if (const char* e = std::getenv("CEK_DEFER_DOWNLOADS")) deferred_downloads = std::string(e) != "0";
@@ -269,6 +270,8 @@ Cores::~Cores() {
     }
     if (spans_[w].gap_a) (void)hipEventDestroy(spans_[w].gap_a);
     if (spans_[w].gap_b) (void)hipEventDestroy(spans_[w].gap_b);
+    if (w < order_events_.size())
+      for (hipEvent_t e : order_events_[w]) (void)hipEventDestroy(e);
   }
   for (size_t w = 0; w < shell_dims_.size() && w < workers_.size(); ++w)
     if (shell_dims_[w]) {
@@ -501,7 +504,8 @@ void Cores::capture_begin() {
     w->sync_all();
   }
   cap_saved_ = {device_spans, peer_reads, async_enqueue, fine_grained, enqueue_mode_, record_timeline,
-                graph_min_launches};
+                graph_min_launches, kernel_times_on()};
+  set_kernel_times(false);  // stamped launches are not captured (their events would never be recorded)
   device_spans = false;
   record_timeline = false;
   peer_reads = false;
@@ -539,6 +543,7 @@ void Cores::restore_capture_state() {
   graph_min_launches = cap_saved_.graph_min_launches;
   enqueue_mode_ = cap_saved_.enqueue_mode;
   record_timeline = cap_saved_.record_timeline;
+  set_kernel_times(cap_saved_.kernel_times);
 }
 
 int Cores::capture_end() {
@@ -633,8 +638,25 @@ void Cores::finish() {
   gather_pending_ = false;  // every gather copy (on the main streams) is done
 }
 
+// A deferred download of the array being released still targets its host
+// buffer: issue it and let it land before the device buffer goes away (the
+// host buffer is alive for the duration of the caller's __del__).
 void Cores::release_array(uint64_t uid) {
-  for (auto& w : workers_) w->release(uid);
+  std::lock_guard<std::recursive_mutex> call_guard(call_mu_);
+  for (size_t w = 0; w < workers_.size(); ++w) {
+    Worker& wk = *workers_[w];
+    if (w < pending_d2h_.size()) {
+      std::vector<hipStream_t> streams;
+      for (const auto& p : pending_d2h_[w])
+        if (p.a.uid == uid && std::find(streams.begin(), streams.end(), p.s) == streams.end()) streams.push_back(p.s);
+      if (!streams.empty()) {
+        flush_downloads(wk);
+        if (wk.gpu())
+          for (hipStream_t s : streams) CEK_HIP(hipStreamSynchronize(s));
+      }
+    }
+    wk.release(uid);
+  }
 }
 
 uint64_t Cores::device_pointer(int i, const ArraySpec& a) {
@@ -1191,14 +1213,53 @@ bool Cores::defer_downloads(const Worker& wk) const {
          !phase_ && !comm_;
 }
 
-void Cores::flush_downloads(Worker& wk) {
+// A deferred download may not be overtaken by the next compute's uploads
+// when they share an in-order stream (the download would follow the upload)
+// or touch the same array (a stale host copy going up over the result, or
+// the next upload reading host memory the download has not filled yet).
+bool Cores::must_flush_before(const Worker& wk, hipStream_t s, const ComputeCall& c) const {
+  const int w = worker_index(wk);
+  if (w < 0 || w >= static_cast<int>(pending_d2h_.size())) return false;
+  for (const auto& p : pending_d2h_[w]) {
+    if (p.s == s) return true;
+    for (const auto& a : c.arrays)
+      if (!a.zc && a.uid == p.a.uid) return true;
+  }
+  return false;
+}
+
+// Issue the pending downloads.  With `next` (the stream the next compute
+// runs on) and that compute `c`, `next` also waits for every pending
+// download on another stream whose array the compute touches.
+void Cores::flush_downloads(Worker& wk, hipStream_t next, const ComputeCall* c) {
   const int w = worker_index(wk);
   if (w < 0 || w >= static_cast<int>(pending_d2h_.size())) return;
   auto& pd = pending_d2h_[w];
   auto& ps = pending_span_end_[w];
   if (pd.empty() && ps.empty()) return;
   wk.set_device();
-  for (const auto& p : pd) wk.d2h(p.s, p.a, p.begin, p.count);
+  std::vector<hipStream_t> order;  // streams `next` must wait for
+  for (const auto& p : pd) {
+    wk.d2h(p.s, p.a, p.begin, p.count);
+    if (c && p.s != next && std::find(order.begin(), order.end(), p.s) == order.end())
+      for (const auto& a : c->arrays)
+        if (!a.zc && a.uid == p.a.uid) {
+          order.push_back(p.s);
+          break;
+        }
+  }
+  if (!order.empty() && wk.gpu()) {
+    auto& ev = order_events_[w];
+    while (ev.size() < order.size()) {
+      hipEvent_t e;
+      CEK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ev.push_back(e);
+    }
+    for (size_t i = 0; i < order.size(); ++i) {
+      CEK_HIP(hipEventRecord(ev[i], order[i]));
+      CEK_HIP(hipStreamWaitEvent(next, ev[i], 0));
+    }
+  }
   pd.clear();
   DevSpans& d = spans_[w];
   for (const auto& p : ps)
@@ -1212,7 +1273,8 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
   if (wk.gpu())
     s = (enqueue_mode_ && async_enqueue) ? wk.compute_stream(wk.next_compute_queue()) : wk.main_stream();
   const bool defer = defer_downloads(wk);
-  if (!defer) flush_downloads(wk);  // a compute that does not defer runs after every earlier download
+  if (!defer || must_flush_before(wk, s, c))
+    flush_downloads(wk, s, &c);  // this compute runs after every earlier download
   if (wk.gpu() && s != wk.main_stream()) wait_gather(wk, s);
   span_begin(wk, s);
   // across ranks: written slices all-gathered by RCCL (every written array

@@ -456,6 +456,7 @@ class Cores {
   struct CaptureSaved {
     bool device_spans, peer_reads, async_enqueue, fine_grained, enqueue_mode, record_timeline;
     int graph_min_launches;
+    bool kernel_times;
   } cap_saved_{};
   std::map<int, std::vector<hipGraphExec_t>> graphs_;  // id -> one exec per local worker (null: CPU)
   // buffers each worker handed out while capturing: (uid, pointer) — a graph
@@ -517,8 +518,10 @@ class Cores {
   };
   std::vector<std::vector<PendingD2H>> pending_d2h_;          // per local device
   std::vector<std::vector<PendingSpanEnd>> pending_span_end_;  // per local device
+  std::vector<std::vector<hipEvent_t>> order_events_;          // per local device (flush ordering)
   bool defer_downloads(const Worker& wk) const;
-  void flush_downloads(Worker& wk);
+  bool must_flush_before(const Worker& wk, hipStream_t s, const ComputeCall& c) const;
+  void flush_downloads(Worker& wk, hipStream_t next = nullptr, const ComputeCall* c = nullptr);
   ComputeRecord last_record_;
   CoresConfig cfg_;
 

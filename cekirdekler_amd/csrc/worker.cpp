@@ -625,6 +625,11 @@ void Worker::launch(hipStream_t s, const std::string& kernel, const std::vector<
       CEK_HIP(hipExtModuleLaunchKernel(f, grid * static_cast<unsigned>(local), 1, 1, static_cast<unsigned>(local),
                                        1, 1, dyn_lds_, s, params.data(), nullptr, a, b, 0));
       std::lock_guard<std::mutex> g(kstamp_mu_);
+      if (kstamps_.size() >= kMaxKernelStamps) {  // recording left on: keep the newest
+        kstamp_spare_.push_back(kstamps_.front().start);
+        kstamp_spare_.push_back(kstamps_.front().stop);
+        kstamps_.pop_front();
+      }
       kstamps_.push_back({kernel, a, b});
     } else {
       CEK_HIP(hipModuleLaunchKernel(f, grid, 1, 1, static_cast<unsigned>(local), 1, 1, dyn_lds_, s,
@@ -674,7 +679,7 @@ hipEvent_t Worker::kstamp_event() {
 }
 
 std::vector<std::pair<std::string, double>> Worker::kernel_times() {
-  std::vector<KernelStamp> st;
+  std::deque<KernelStamp> st;
   {
     std::lock_guard<std::mutex> g(kstamp_mu_);
     st.swap(kstamps_);

@@ -270,7 +270,8 @@ class Worker {
     std::string kernel;
     hipEvent_t start, stop;
   };
-  std::vector<KernelStamp> kstamps_;
+  std::deque<KernelStamp> kstamps_;  // ring: the oldest are dropped past kMaxKernelStamps
+  static constexpr size_t kMaxKernelStamps = 1 << 16;
   std::vector<hipEvent_t> kstamp_spare_;
   std::mutex kstamp_mu_;
   hipEvent_t kstamp_event();

@@ -86,6 +86,24 @@ def async_queue_count() -> int:
     return max(1, hw_queue_count() - 1)
 
 
+def mixed_cpu_policy() -> str:
+    """How a device set that mixes a CPU device with GPUs shares the host
+    (``CEK_MIXED_CPU``): the reference sizes its CPU device to every core but
+    one, the caller's (ClDevice.cs:85-95); here each GPU worker is a host
+    thread too, waiting on its streams.
+
+    * ``reserve`` — the CPU pool gives up one thread per GPU worker
+      (``usable_cpus() - 1 - #GPUs`` with the partition flag);
+    * ``sleep`` — GPU workers sleep on blocking events instead of spinning;
+    * ``both`` / ``none``.
+    """
+    v = os.environ.get("CEK_MIXED_CPU", "").strip().lower()
+    return v if v in ("reserve", "sleep", "both", "none") else MIXED_CPU_DEFAULT
+
+
+MIXED_CPU_DEFAULT = "reserve"
+
+
 class ClDevice:
     """One selectable device plus its selection flags."""
 
@@ -134,8 +152,11 @@ class ClDevice:
 
     isGddr = is_gddr
 
-    def native_info(self):
-        """DeviceInfo handed to the native runtime (CPU pool sized here)."""
+    def native_info(self, reserve_threads: int = 0):
+        """DeviceInfo handed to the native runtime (CPU pool sized here).
+        ``reserve_threads``: host threads the device set's GPU workers keep
+        busy, taken off the CPU pool (``mixed_cpu_policy``) unless the core
+        count was given explicitly (``max_cpu_cores``, ``CEK_CPU_THREADS``)."""
         if not self.is_cpu:
             if not self.cu_partition:
                 return self.info
@@ -146,6 +167,8 @@ class ClDevice:
         threads = hw - 1 if (self.partition and hw > 1) else hw
         if self.max_cpu_cores > 0:
             threads = min(threads, self.max_cpu_cores)
+        else:
+            threads -= max(0, int(reserve_threads))
         env = os.environ.get("CEK_CPU_THREADS")
         if env:
             threads = int(env)

@@ -143,3 +143,37 @@ class WaveSurface:
     def reference(self) -> np.ndarray:
         return wave_reference(self.base[:self.n], self.normals[:self.n], np.float32(self.ctr),
                               np.float32(self.t), self.base["x"][0], self.base["y"][0])
+
+
+class ReferenceCpuWave:
+    """The reference example's CPU-only strategy (Kamera.cs:208-218,
+    ``strategy = true``): no runtime, one host thread updating the vertices
+    one at a time with double-precision ``Math.Sqrt`` / ``Math.Sin`` — the
+    baseline its "CPU+GPU 3x as fast" comment (Kamera.cs:266) is measured
+    against.  The loop is native and scalar (``cek.wave_reference_scalar``,
+    csrc/refloops.cpp), as the .NET JIT runs it."""
+
+    def __init__(self, base: np.ndarray, normals: np.ndarray):
+        if base.dtype != VERTEX or normals.dtype != VERTEX or len(base) != len(normals):
+            raise ValueError("base and normals must be equal-length VERTEX arrays")
+        from .._native import cek
+
+        self._cek = cek
+        self.n = len(base)
+        self.base = np.ascontiguousarray(base)
+        self.normals = np.ascontiguousarray(normals)
+        self.vertices = self.base.copy()
+        self.t = 0.0
+        self.ctr = 0.0
+
+    def update(self) -> np.ndarray:
+        if self.ctr < 0.3:
+            self.ctr += 0.001
+        self.t += 0.001
+        self._cek.wave_reference_scalar(self.base.ctypes.data, self.normals.ctypes.data, self.vertices.ctypes.data,
+                                        self.n, float(self.ctr), float(self.t))
+        return self.vertices
+
+    def reference(self) -> np.ndarray:
+        return wave_reference(self.base, self.normals, np.float32(self.ctr), np.float32(self.t),
+                              self.base["x"][0], self.base["y"][0])

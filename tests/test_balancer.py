@@ -2,6 +2,7 @@
 HelperFunctions.loadBalance (reference HelperFunctions.cs:190-280), plus the
 properties the reference documents (sum preserved, multiples of step, 0.3
 damping, smoothing active once 10 calls of history exist)."""
+import os
 import random
 
 import pytest
@@ -56,6 +57,44 @@ def test_convergence_iters_2to1_within_budget():
     seq = B.simulate([2.0, 1.0], total, step, calls=40, smooth=False)
     shares = [r[0] / total for r in seq]
     assert B.convergence_iters(shares, 0.05) <= 10  # ≤10 computes, law-identical
+
+
+def test_convergence_iters_ignores_single_late_outlier():
+    """the steady state is the median of the last 10
+    calls, and one isolated blip late in the run does not restart the
+    count (the old definition took shares[-1] and counted from the blip)."""
+    shares = [0.5, 0.55, 0.585, 0.61, 0.628, 0.64, 0.65, 0.655] + [0.6667] * 30
+    clean = B.convergence_iters(shares, 0.05)
+    assert clean <= 10
+    blip = list(shares)
+    blip[-1] = 0.75  # the final call alone is off by 12 %
+    assert B.steady_share(blip) == pytest.approx(0.6667)
+    assert B.convergence_iters(blip, 0.05) == clean
+    blip2 = list(shares)
+    blip2[30] = 0.58
+    assert B.convergence_iters(blip2, 0.05) == clean
+    # a trajectory that never settles is not converged
+    osc = [0.5 if i % 2 else 0.7 for i in range(40)]
+    assert B.convergence_iters(osc, 0.05) > 10
+
+
+@pytest.mark.skipif(bool(os.environ.get("PYTEST_XDIST_WORKER")),
+                    reason="host-clock timing measurement: needs a host not shared with other test workers")
+@pytest.mark.parametrize("outliers", [(), (30,), (39,)])
+def test_measured_lb_iters_two_cpu_devices(outliers):
+    """The bench's measurement (measure_lb_convergence) on two CPU devices,
+    device 1 timed 2x slower: converges within the BASELINE budget of 10
+    computes, also with a single injected timing outlier (6x for one call)."""
+    import cekirdekler_amd as ck
+
+    p = ck.ClPlatforms.all()
+    # two threads per device: the measurement stays meaningful when the
+    # test runner shares the host with other workers
+    devs = p.cpus(True, max_cpu_cores=2) + p.cpus(True, max_cpu_cores=2)
+    r = B.measure_lb_convergence(devs, calls=40, n=1 << 15, inner=256, outliers=outliers)
+    assert r["iters"] <= 10, r
+    assert abs(r["steady_share_dev0"] - 2 / 3) < 0.05, r
+    assert len(r["shares"]) == 40
 
 
 def test_smoothing_uses_history_only_when_full():

@@ -863,3 +863,75 @@ def test_async_enqueue_deferred_downloads_correct(defer):
     np.testing.assert_array_equal(ys[0].array, (np.arange(n, dtype=np.float32) + 10) * 3.0 + 1.0)
     np.testing.assert_array_equal(ys[1].array, (np.arange(n, dtype=np.float32) + 11) * 3.0 + 1.0)
     cr.dispose()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("queues", [1, 2, None])
+def test_async_enqueue_dependent_chain_and_inplace(queues):
+    """a deferred download must not be overtaken by the next
+    compute's uploads of the same array, nor by anything on the same stream
+    (one compute queue: every async compute runs on the main stream).  A
+    chain x→y→z where y is written by one compute and uploaded by the next,
+    plus an in-place read+write array stepped repeatedly inside the batch,
+    must end with the sequential results."""
+    import cekirdekler_amd as ck
+
+    g = ck.ClPlatforms.all().gpus()
+    src = r"""
+    __global__ void mul3(const float* x, float* y) { long long i = get_global_id(0); y[i] = x[i] * 3.0f; }
+    __global__ void add1(float* a) { long long i = get_global_id(0); a[i] = a[i] + 1.0f; }
+    """
+    cr = ck.ClNumberCruncher(g[0], src, queue_concurrency=queues)
+    assert cr.cores.deferred_downloads
+    n = 1 << 16
+    base = np.arange(n, dtype=np.float32)
+    x = ck.ClArray(base.copy())
+    y = ck.ClArray(np.zeros(n, np.float32))
+    z = ck.ClArray(np.zeros(n, np.float32))
+    a = ck.ClArray(base.copy())  # read + write every step
+    y.read = False
+    z.read = False
+    cr.enqueue_mode = True
+    cr.enqueue_mode_async_enable = True
+    for step in range(4):
+        x.next_param(y).compute(cr, 1, "mul3", n, 256)   # y = 3x (downloaded)
+        y.next_param(z).compute(cr, 2, "mul3", n, 256)   # z = 3y (y uploaded from host)
+        a.compute(cr, 3, "add1", n, 256)                 # a += 1 (up, kernel, down)
+    cr.enqueue_mode = False
+    cr.enqueue_mode_async_enable = False
+    np.testing.assert_array_equal(y.array, base * 3.0)
+    np.testing.assert_array_equal(z.array, base * 9.0)
+    np.testing.assert_array_equal(a.array, base + 4.0)
+    cr.dispose()
+
+
+@pytest.mark.gpu
+def test_release_array_with_pending_download():
+    """an array garbage-collected inside an async batch
+    has its deferred download issued (and landed) before its device buffer is
+    freed; the batch's other results are intact."""
+    import gc
+
+    import cekirdekler_amd as ck
+
+    g = ck.ClPlatforms.all().gpus()
+    src = "__global__ void k(const float* x, float* y) { long long i = get_global_id(0); y[i] = x[i] + 2.0f; }"
+    cr = ck.ClNumberCruncher(g[0], src)
+    n = 1 << 16
+    x = ck.ClArray(np.arange(n, dtype=np.float32))
+    keep = ck.ClArray(np.zeros(n, np.float32))
+    keep.read = False
+    host = np.zeros(n, np.float32)
+    cr.enqueue_mode = True
+    cr.enqueue_mode_async_enable = True
+    tmp = ck.ClArray(host)
+    tmp.read = False
+    x.next_param(tmp).compute(cr, 1, "k", n, 256)
+    del tmp
+    gc.collect()
+    x.next_param(keep).compute(cr, 2, "k", n, 256)
+    cr.enqueue_mode = False
+    cr.enqueue_mode_async_enable = False
+    np.testing.assert_array_equal(keep.array, np.arange(n, dtype=np.float32) + 2.0)
+    np.testing.assert_array_equal(host, np.arange(n, dtype=np.float32) + 2.0)
+    cr.dispose()
