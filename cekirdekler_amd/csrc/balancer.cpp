@@ -117,7 +117,30 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
       if (static_cast<int>(v.size()) > kFitSamples) v.erase(v.begin());
     }
   }
-  if (warm && active > 0 && wall_ms > 0) {
+  // the configuration that chose the recorded call's split: the law, or
+  // the predictor (a fitted split, a single device, a probe)
+  const bool by_law = fs.decision == "law";
+  bool settled = fs.prev_ranges.size() == n;
+  for (size_t i = 0; settled && i < n; ++i)
+    settled = std::llabs(ranges[i] - fs.prev_ranges[i]) * 100 <= total;
+  fs.prev_ranges = ranges;
+  if (by_law) fs.law_ranges = ranges;
+  // hand back to the law: from its own last split when another
+  // configuration ran the recorded call
+  auto to_law = [&]() {
+    fs.decision = "law";
+    if (by_law || fs.law_ranges.size() != n) return false;
+    ranges = fs.law_ranges;
+    return true;
+  };
+  if (warm && active > 0 && wall_ms > 0 && by_law) {
+    fs.law_settled = settled ? fs.law_settled + 1 : 0;
+    if (fs.law_settled >= 3) fs.law_wall = fs.law_wall < 0 ? wall_ms : 0.5 * fs.law_wall + 0.5 * wall_ms;
+    if (active >= 2) {
+      const double ov = std::max(0.0, wall_ms - tmax);
+      fs.o_multi = fs.o_multi < 0 ? ov : 0.7 * fs.o_multi + 0.3 * ov;
+    }
+  } else if (warm && active > 0 && wall_ms > 0) {
     if (active >= 2) {
       const double ov = std::max(0.0, wall_ms - tmax);
       fs.o_multi = fs.o_multi < 0 ? ov : 0.7 * fs.o_multi + 0.3 * ov;
@@ -141,8 +164,7 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
   for (size_t i = 0; i < n; ++i) {
     const auto& v = fs.samples[i];
     if (v.size() < 2) {
-      fs.decision = "law";
-      return false;
+      return to_law();
     }
     double sx = 0, sy = 0, sxx = 0, sxy = 0;
     for (auto& p : v) {
@@ -154,8 +176,7 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
     const double k = static_cast<double>(v.size());
     const double den = k * sxx - sx * sx;
     if (den <= 0) {
-      fs.decision = "law";
-      return false;
+      return to_law();
     }
     double b = (k * sxy - sx * sy) / den;
     double a = (sy - b * sx) / k;
@@ -215,6 +236,13 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
     } else {
       single = fs.single_wall[best] <= std::max(pred_multi, fs.multi_wall);
     }
+  }
+  // the guard: defer to the law until its settled split is timed, and
+  // whenever the chosen configuration has been measured no faster than it
+  // (a probe still runs to completion: it is the measurement)
+  if (fs.probe_left == 0) {
+    const double cand = single ? fs.single_wall[best] : fs.multi_wall;
+    if (fs.law_wall < 0 || (cand > 0 && cand >= fs.law_wall)) return to_law();
   }
   std::vector<double> target(n, 0.0);
   if (single) {

@@ -27,8 +27,10 @@ namespace cek {
 // device; for the split the larger of the prediction and the measured wall
 // of recent split calls (a fit that misses a cost of co-execution — a CPU
 // pool's wake-ups, contention on shared hardware — cannot keep choosing a
-// split that is slower in fact).  Until every device has a fit it defers to
-// the law.
+// split that is slower in fact).  Until every device has a fit, and until
+// the law's own settled split has been timed, it defers to the law; and it
+// never keeps a configuration whose measured wall time is not below the
+// law's (so it can only be as slow as the law, or faster).
 struct FitState {
   std::vector<std::vector<std::pair<double, double>>> samples;  // per device: (range, ms), distinct ranges
   double o_multi = -1;                 // EWMA of wall − max device ms over multi-device calls
@@ -41,7 +43,17 @@ struct FitState {
   std::string decision = "law";        // law | multi | single | probe
   std::vector<double> a, b;            // last fits (ms, ms per work item)
   double predicted_multi_ms = 0;
-  double multi_wall = -1;              // EWMA wall ms of recent multi-device calls (−1: none yet)
+  double multi_wall = -1;              // EWMA wall ms of recent fitted-split calls (−1: none yet)
+  // Guard: the law's own split, measured once it has
+  // settled (three calls in a row in which no device's range moved more
+  // than 1 % of the total).  The predictor deviates from the law only after this is
+  // known and only to a configuration not measured slower than it.
+  double law_wall = -1;                // EWMA wall ms of settled law calls (−1: not yet)
+  int law_settled = 0;                 // consecutive settled law calls
+  std::vector<long long> prev_ranges;  // the ranges of the previous recorded call
+  // the last split the law chose: restored when the predictor hands back to
+  // the law (the law cannot bring a device back from a zero range)
+  std::vector<long long> law_ranges;
 };
 
 constexpr int kFitSamples = 8;

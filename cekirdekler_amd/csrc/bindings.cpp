@@ -231,7 +231,8 @@ PYBIND11_MODULE(_cek, m) {
       .def_readonly("o_multi", &FitState::o_multi)
       .def_readonly("single_wall", &FitState::single_wall)
       .def_readonly("predicted_multi_ms", &FitState::predicted_multi_ms)
-      .def_readonly("multi_wall", &FitState::multi_wall);
+      .def_readonly("multi_wall", &FitState::multi_wall)
+      .def_readonly("law_wall", &FitState::law_wall);
   m.def("initial_split", [](int devices, bool smooth, std::vector<std::vector<double>> history,
                             long long total, long long step) {
     std::vector<long long> ranges;
@@ -495,6 +496,7 @@ PYBIND11_MODULE(_cek, m) {
         d["single_wall_ms"] = f->single_wall;
         d["predicted_multi_ms"] = f->predicted_multi_ms;
         d["measured_multi_ms"] = f->multi_wall;
+        d["measured_law_ms"] = f->law_wall;
         return d;
       })
       .def("set_dynamic_lds", &Cores::set_dynamic_lds)
@@ -554,7 +556,7 @@ PYBIND11_MODULE(_cek, m) {
 
   py::class_<PoolTask>(m, "PoolTask")
       .def(py::init<>())
-      .def_readwrite("call", &PoolTask::call)
+      .def_property("call", &PoolTask::call, &PoolTask::set_call)
       .def_readwrite("type", &PoolTask::type)
       .def_readwrite("id", &PoolTask::id);
 
@@ -564,7 +566,8 @@ PYBIND11_MODULE(_cek, m) {
       .def_readonly("ms", &PoolCompletion::ms)
       .def_readonly("error", &PoolCompletion::error);
 
-  py::class_<DevicePool, std::shared_ptr<DevicePool>>(m, "DevicePool")
+  auto pool_cls = py::class_<DevicePool, std::shared_ptr<DevicePool>>(m, "DevicePool");
+  pool_cls
       .def(py::init<std::vector<std::shared_ptr<Cores>>, int, int>(), py::arg("devices"), py::arg("max_in_flight"),
            py::arg("policy") = 0, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("policy", &DevicePool::policy)
@@ -573,23 +576,41 @@ PYBIND11_MODULE(_cek, m) {
       // type and id (one crossing and no per-task Python objects)
       .def("enqueue_batch",
            [](DevicePool& p, const std::vector<ComputeCall>& calls, const std::vector<int>& which,
-              const std::vector<std::vector<ArraySpec>>& arrays, const std::vector<uint32_t>& types,
+              std::vector<std::vector<ArraySpec>> arrays, const std::vector<uint32_t>& types,
               const std::vector<long long>& ids) {
              const size_t n = which.size();
              if (arrays.size() != n || types.size() != n || ids.size() != n)
                throw Error("enqueue_batch: which, arrays, types and ids must have one entry per task");
+             std::vector<std::shared_ptr<const ComputeCall>> tmpl;
+             tmpl.reserve(calls.size());
+             for (const auto& c : calls) {
+               auto t = std::make_shared<ComputeCall>(c);
+               t->arrays.clear();
+               tmpl.push_back(std::move(t));
+             }
              std::vector<PoolTask> ts(n);
              for (size_t i = 0; i < n; ++i) {
                if (which[i] < 0 || static_cast<size_t>(which[i]) >= calls.size())
                  throw Error("enqueue_batch: template index out of range");
-               ts[i].call = calls[which[i]];
-               ts[i].call.arrays = arrays[i];
+               ts[i].tmpl = tmpl[which[i]];
+               ts[i].arrays = std::move(arrays[i]);
                ts[i].type = types[i];
                ts[i].id = ids[i];
              }
              py::gil_scoped_release r;
-             p.enqueue(ts);
+             p.enqueue(std::move(ts));
            })
+      .def("take_errors", &DevicePool::take_errors)
+      .def("results",
+           [](DevicePool& p, long long first, long long n) {
+             std::vector<int> dev;
+             std::vector<double> ms;
+             p.results(first, n, dev, ms);
+             return py::make_tuple(dev, ms);
+           },
+           py::arg("first"), py::arg("n"), "(devices, ms) of tasks [first, first + n); device -1: not retired")
+      .attr("NOTIFY") = static_cast<uint32_t>(kTaskNotify);
+  pool_cls
       .def("finish", &DevicePool::finish, py::call_guard<py::gil_scoped_release>())
       .def("completions", &DevicePool::completions, py::arg("timeout_ms") = 0.0,
            py::call_guard<py::gil_scoped_release>())

@@ -45,17 +45,18 @@ void DevicePool::close() {
   threads_.clear();
 }
 
-void DevicePool::enqueue(const std::vector<PoolTask>& tasks) {
+void DevicePool::enqueue(std::vector<PoolTask> tasks) {
   {
     std::lock_guard<std::mutex> g(mu_);
     if (closed_) throw Error("device pool is closed");
     bool sync_next = false;
     const int pid = static_cast<int>(pools_.size());
     pools_.push_back(PoolProgress());
-    for (const auto& t : tasks) {
+    for (auto& task : tasks) {
       Item it;
-      it.task = t;
+      it.task = std::move(task);
       it.pool = pid;
+      const PoolTask& t = it.task;
       // GLOBAL_SYNC_LAST of the previous task = a barrier before this one
       if (sync_next) it.task.type |= kTaskSyncFirst;
       sync_next = (t.type & kTaskSyncLast) != 0;
@@ -168,19 +169,54 @@ bool DevicePool::take_locked(int dev, Item& out) {
   return false;
 }
 
-void DevicePool::complete(int dev, long long id, double ms, const std::string& err) {
+// Retires one task.  Only a notify task (a callback) or a failure makes a
+// record the caller reads; the wake-ups go only to whoever can proceed now:
+// finish() when the pool drains, idle consumers when a barrier or a pinned
+// group may have been waiting for this retirement.
+void DevicePool::complete(int dev, long long id, bool notify, double ms, const std::string& err) {
+  bool wake_comp = false, wake_done = false, wake_work = false;
   {
     std::lock_guard<std::mutex> g(mu_);
-    done_.push_back({id, dev, ms, err});
+    if (id >= 0) {
+      if (static_cast<size_t>(id) >= results_.size()) results_.resize(static_cast<size_t>(id) + 1 + 1024);
+      results_[static_cast<size_t>(id)] = {dev, static_cast<float>(ms)};
+    }
+    if (!err.empty()) errors_.push_back({id, dev, ms, err});
+    if (notify) {
+      done_.push_back({id, dev, ms, err});
+      wake_comp = true;
+    }
     ++counts_[dev];
     busy_ms_[dev] += ms;
     --outstanding_;
     --running_;
     --inflight_[dev];
+    wake_done = outstanding_ == 0;
+    wake_work = running_ == 0 || owner_ >= 0 ||
+                (!queue_.empty() && (queue_.front().task.type & kTaskSyncFirst));
   }
-  comp_cv_.notify_all();
-  done_cv_.notify_all();
-  work_cv_.notify_all();
+  if (wake_comp) comp_cv_.notify_all();
+  if (wake_done) done_cv_.notify_all();
+  if (wake_work) work_cv_.notify_all();
+}
+
+std::vector<PoolCompletion> DevicePool::take_errors() {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<PoolCompletion> out;
+  out.swap(errors_);
+  return out;
+}
+
+void DevicePool::results(long long first, long long n, std::vector<int>& dev, std::vector<double>& ms) {
+  std::lock_guard<std::mutex> g(mu_);
+  dev.assign(static_cast<size_t>(std::max(0LL, n)), -1);
+  ms.assign(dev.size(), 0.0);
+  for (long long i = 0; i < n; ++i) {
+    const long long id = first + i;
+    if (id < 0 || static_cast<size_t>(id) >= results_.size()) continue;
+    dev[static_cast<size_t>(i)] = results_[static_cast<size_t>(id)].device;
+    ms[static_cast<size_t>(i)] = results_[static_cast<size_t>(id)].ms;
+  }
 }
 
 int DevicePool::retire(int dev, std::vector<Inflight>& inflight) {
@@ -188,7 +224,7 @@ int DevicePool::retire(int dev, std::vector<Inflight>& inflight) {
   int n = 0;
   for (size_t i = 0; i < inflight.size();) {
     if (cr.marker_word(0, inflight[i].slot) >= inflight[i].value) {
-      complete(dev, inflight[i].id, now_ms() - inflight[i].t0, "");
+      complete(dev, inflight[i].id, inflight[i].notify, now_ms() - inflight[i].t0, "");
       inflight[i] = inflight.back();
       inflight.pop_back();
       ++n;
@@ -211,6 +247,9 @@ void DevicePool::consumer(int dev) {
   const bool async = max_in_flight_ > 1;
   if (async) cr.fine_grained = true;  // a marker word after every compute
   std::vector<Inflight> inflight;
+  ComputeCall call;                            // scratch: the task being issued
+  const ComputeCall* call_tmpl = nullptr;      // the template `call` was copied from
+  std::shared_ptr<const ComputeCall> call_keep;  // keeps that template alive
   double last_progress = now_ms();
   for (;;) {
     if (!inflight.empty() && retire(dev, inflight) > 0) last_progress = now_ms();
@@ -253,26 +292,35 @@ void DevicePool::consumer(int dev) {
       continue;
     }
     last_progress = now_ms();
-    const double t0 = now_ms();
-    const PoolTask& t = it.task;
-    if (t.call.kernels.empty()) {  // a pure barrier / message task
-      complete(dev, t.id, 0.0, "");
+    const double t0 = last_progress;
+    PoolTask& t = it.task;
+    const bool notify = (t.type & kTaskNotify) != 0;
+    if (!t.tmpl || t.tmpl->kernels.empty()) {  // a pure barrier / message task
+      complete(dev, t.id, notify, 0.0, "");
       continue;
     }
     try {
+      // the consumer's call: the template's fields copied only when the
+      // template changes, the task's arrays moved in
+      if (t.tmpl.get() != call_tmpl) {
+        call = *t.tmpl;
+        call_tmpl = t.tmpl.get();
+        call_keep = t.tmpl;
+      }
+      call.arrays = std::move(t.arrays);
       cr.no_compute = (t.type & kTaskNoCompute) != 0;
       if (async) {
         if (!cr.enqueue_mode()) cr.set_enqueue_mode(true);
         cr.async_enqueue = !it.serial;  // serial groups stay on one in-order stream
-        cr.compute(t.call);
+        cr.compute(call);
         auto m = cr.last_marker(0);
-        inflight.push_back({t.id, m.first, m.second, t0});
+        inflight.push_back({t.id, notify, m.first, m.second, t0});
       } else {
-        cr.compute(t.call);
-        complete(dev, t.id, now_ms() - t0, "");
+        cr.compute(call);
+        complete(dev, t.id, notify, now_ms() - t0, "");
       }
     } catch (const std::exception& e) {
-      complete(dev, t.id, now_ms() - t0, e.what());
+      complete(dev, t.id, notify, now_ms() - t0, e.what());
     }
   }
   try {

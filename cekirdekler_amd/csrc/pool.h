@@ -65,10 +65,29 @@ enum PoolTaskFlags : uint32_t {
   kTaskSerialEnd = 128,
 };
 
+// Not a ClTaskType bit: the caller wants a completion record for the task
+// (it has a callback).  Other tasks retire natively without a record; their
+// device and time are kept in the pool's result table (results()).
+constexpr uint32_t kTaskNotify = 1u << 30;
+
 struct PoolTask {
-  ComputeCall call;
+  // the compute without its arrays, shared by every task of one shape (a
+  // batch of 4096 tasks holds one template, not 4096 copies of it)
+  std::shared_ptr<const ComputeCall> tmpl;
+  std::vector<ArraySpec> arrays;  // this task's frozen arrays
   uint32_t type = 0;
   long long id = 0;  // caller's handle, reported back on completion
+  ComputeCall call() const {
+    ComputeCall c = tmpl ? *tmpl : ComputeCall();
+    c.arrays = arrays;
+    return c;
+  }
+  void set_call(const ComputeCall& c) {
+    auto t = std::make_shared<ComputeCall>(c);
+    arrays = std::move(t->arrays);
+    t->arrays.clear();
+    tmpl = std::move(t);
+  }
 };
 
 struct PoolCompletion {
@@ -88,11 +107,17 @@ class DevicePool {
 
   // Appends one task pool (FIFO order kept); broadcast tasks are duplicated
   // per device, SYNC_LAST turns into SYNC_FIRST of the next task.
-  void enqueue(const std::vector<PoolTask>& tasks);
+  void enqueue(std::vector<PoolTask> tasks);
   // Blocks until every enqueued task has retired.
   void finish();
-  // Completions since the last call; waits up to timeout_ms for one (0: poll).
+  // Completions of kTaskNotify tasks since the last call; waits up to
+  // timeout_ms for one (0: poll).
   std::vector<PoolCompletion> completions(double timeout_ms);
+  // Failed tasks since the last call (every task, notified or not).
+  std::vector<PoolCompletion> take_errors();
+  // Device and issue→retirement ms of tasks [first, first + n) (device -1:
+  // not retired yet, or never enqueued).
+  void results(long long first, long long n, std::vector<int>& dev, std::vector<double>& ms);
   long long outstanding();
   std::vector<long long> device_task_counts();
   std::vector<double> device_busy_ms();
@@ -119,13 +144,14 @@ class DevicePool {
   int least_loaded_locked() const;
   struct Inflight {
     long long id;
+    bool notify;
     int slot;
     uint64_t value;
     double t0;
   };
   bool take_locked(int dev, Item& out);
   void consumer(int dev);
-  void complete(int dev, long long id, double ms, const std::string& err);
+  void complete(int dev, long long id, bool notify, double ms, const std::string& err);
   int retire(int dev, std::vector<Inflight>& inflight);
 
   std::vector<std::shared_ptr<Cores>> devs_;
@@ -136,7 +162,13 @@ class DevicePool {
   std::mutex mu_;
   std::condition_variable work_cv_, done_cv_, comp_cv_;
   std::deque<Item> queue_;
-  std::deque<PoolCompletion> done_;
+  std::deque<PoolCompletion> done_;     // notify tasks
+  std::vector<PoolCompletion> errors_;  // failed tasks
+  struct Result {
+    int device = -1;
+    float ms = 0;
+  };
+  std::vector<Result> results_;  // by task id
   long long outstanding_ = 0;
   int running_ = 0;  // taken and not yet retired
   int owner_ = -1;   // device holding a select/serial group

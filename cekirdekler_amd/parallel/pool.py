@@ -215,7 +215,9 @@ class ClDevicePool:
         self._native = None
         self._counts_base: List[int] = []
         self._cv = threading.Condition()
-        self._tasks = {}  # id -> [task, completions still expected]; keeps arrays alive
+        self._notify = {}  # id -> [task, completions still expected]: tasks with a callback
+        self._live = []  # (first id, tasks) per enqueued batch: keeps the arrays alive until finish()
+        self._templates = {}  # template key -> validated ComputeCall (per device pool)
         self._next_id = 0
         self._expected = 0
         self._handled = 0
@@ -250,6 +252,9 @@ class ClDevicePool:
             self._dispatcher.start()
 
     # ---- completions / callbacks -------------------------------------------
+    # Only tasks with a callback come back to Python one by one (the native
+    # pool records them as notify tasks); every other task retires natively,
+    # and its device and time are read for the whole batch in finish().
     def _dispatch_loop(self) -> None:
         while not self._closed:
             nat = self._native
@@ -262,7 +267,7 @@ class ClDevicePool:
             return
         for c in comps:
             with self._cv:
-                entry = self._tasks.get(c.id)
+                entry = self._notify.get(c.id)
             err = c.error
             if entry is not None:
                 t = entry[0]
@@ -274,14 +279,12 @@ class ClDevicePool:
                     try:
                         t.callback()
                     except Exception as e:  # reported by finish()
-                        err = f"callback: {e!r}"
+                        self._errors.append(f"task {c.id} on device {c.device}: callback: {e!r}")
             with self._cv:
-                if err:
-                    self._errors.append(f"task {c.id} on device {c.device}: {err}")
                 if entry is not None:
                     entry[1] -= 1
                     if entry[1] <= 0:
-                        self._tasks.pop(c.id, None)
+                        self._notify.pop(c.id, None)
                 self._handled += 1
                 self._cv.notify_all()
 
@@ -289,60 +292,69 @@ class ClDevicePool:
     def enqueue_task_pool(self, pool: ClTaskPool) -> None:
         """Hand every task of ``pool`` to the native device pool, in FIFO
         order.  Tasks that share a compute shape (compute id, kernels,
-        ranges, pipeline, repeats) share one validated template call; the
-        native side gets one batch (``DevicePool.enqueue_batch``) instead of
-        one Python-built call per task."""
+        ranges, pipeline, repeats) share one validated template call, built
+        once per device pool (``_templates``); the native side gets one batch
+        (``DevicePool.enqueue_batch``) holding one copy of each template."""
         if self._native is None:
             raise RuntimeError("device pool has no devices (add_device first)")
         cr0 = self.crunchers[0]
         ndev = len(self.crunchers)
-        templates, index = [], {}
-        empty = cek.ComputeCall()  # barrier / message tasks: no kernels
-        which, arrays, types, ids, entries = [], [], [], [], []
+        cache = self._templates
+        local = {}  # template key -> index into this batch's template list
+        templates = []
+        which, arrays, types = [], [], []
+        notify = []  # (id, [task, copies]) of tasks with a callback
         expected = 0
         tasks = list(pool.tasks)
         pool.tasks.clear()
         with self._cv:
             first_id = self._next_id
             self._next_id += len(tasks)
+        NO_COMPUTE, BROADCAST = int(ClTaskType.TASK_MESSAGE_NO_COMPUTE), int(ClTaskType.TASK_MESSAGE_BROADCAST)
+        NOTIFY = int(cek.DevicePool.NOTIFY)
         for k, t in enumerate(tasks):
-            tid = first_id + k
-            if t.group is not None and t.kernels and not (t.type & ClTaskType.TASK_MESSAGE_NO_COMPUTE
-                                                          and not t.kernels):
-                bl = t.pipeline_blobs if isinstance(t.pipeline_blobs, int) else tuple(t.pipeline_blobs)
-                kn = t.kernels if isinstance(t.kernels, str) else tuple(t.kernels)
-                key = (t.compute_id, kn, t.global_range, t.local_range, t.global_offset, bool(t.pipeline),
-                       bool(t.pipeline_type), bl, int(t.kernel_repeats), t.kernel_repeat_name)
-                j = index.get(key)
+            ty = int(t.type)
+            kn = t.kernels
+            if t.group is not None and kn and not (ty & NO_COMPUTE and not kn):
+                bl = t.pipeline_blobs
+                key = (t.compute_id, kn if isinstance(kn, str) else tuple(kn), t.global_range, t.local_range,
+                       t.global_offset, bool(t.pipeline), bool(t.pipeline_type),
+                       bl if isinstance(bl, int) else tuple(bl), int(t.kernel_repeats), t.kernel_repeat_name)
+                j = local.get(key)
                 if j is None:
-                    try:
-                        call = cr0._build_call(ClParameterGroup(), t.compute_id, t.kernels, t.global_range,
-                                               t.local_range, t.global_offset, t.pipeline, t.pipeline_type,
-                                               t.pipeline_blobs, specs=[])
-                        t._apply_repeats(call)
-                    except ClComputeError as e:
-                        raise ClComputeError(f"task {tid}: {e}") from None
-                    j = index[key] = len(templates)
+                    call = cache.get(key)
+                    if call is None:
+                        try:
+                            call = cr0._build_call(ClParameterGroup(), t.compute_id, t.kernels, t.global_range,
+                                                   t.local_range, t.global_offset, t.pipeline, t.pipeline_type,
+                                                   t.pipeline_blobs, specs=[])
+                            t._apply_repeats(call)
+                        except ClComputeError as e:
+                            raise ClComputeError(f"task {first_id + k}: {e}") from None
+                        cache[key] = call
+                    j = local[key] = len(templates)
                     templates.append(call)
                 which.append(j)
                 arrays.append(t.specs)
             else:
-                if not templates or templates[0] is not empty:
-                    templates.insert(0, empty)
-                    which = [w + 1 for w in which]
-                    index = {kk: v + 1 for kk, v in index.items()}
-                which.append(0)
+                j = local.get(None)
+                if j is None:
+                    j = local[None] = len(templates)
+                    templates.append(cek.ComputeCall())  # barrier / message tasks: no kernels
+                which.append(j)
                 arrays.append([])
-            types.append(int(t.type))
-            ids.append(tid)
-            copies = ndev if t.type & ClTaskType.TASK_MESSAGE_BROADCAST else 1
-            entries.append((tid, [t, copies]))
-            expected += copies
+            if t.callback is not None:
+                copies = ndev if ty & BROADCAST else 1
+                notify.append((first_id + k, [t, copies]))
+                expected += copies
+                ty |= NOTIFY
+            types.append(ty)
         with self._cv:
-            self._tasks.update(entries)
+            self._notify.update(notify)
             self._expected += expected
-        if ids:
-            self._native.enqueue_batch(templates, which, arrays, types, ids)
+            self._live.append((first_id, tasks))
+        if tasks:
+            self._native.enqueue_batch(templates, which, arrays, types, list(range(first_id, first_id + len(tasks))))
 
     enqueueTaskPool = enqueue_task_pool
 
@@ -359,7 +371,20 @@ class ClDevicePool:
                     break
                 self._cv.wait(0.005)
         with self._cv:
-            errs, self._errors = self._errors, []
+            live, self._live = self._live, []
+        for first, tasks in live:  # where and how long every task ran
+            devs, mss = self._native.results(first, len(tasks))
+            for t, d, m in zip(tasks, devs, mss):
+                if d >= 0:
+                    t.device_index = d
+                    t.elapsed_ms = m
+                    o = t.__dict__.get("_origin")
+                    if o is not None:
+                        o.device_index = d
+                        o.elapsed_ms = m
+        errs = [f"task {e.id} on device {e.device}: {e.error}" for e in self._native.take_errors()]
+        with self._cv:
+            errs, self._errors = self._errors + errs, []
         if errs:
             raise ClComputeError("device pool: " + "; ".join(errs))
         return 0

@@ -129,6 +129,33 @@ def test_task_error_is_reported_by_finish():
     pool.dispose()
 
 
+def test_tasks_without_callback_retire_natively_and_report_device():
+    """only tasks with a callback cross back into Python
+    one by one; every other task's device and time are read for the whole
+    batch at finish() (and reach the caller's object, not only the pool's
+    copy).  A raising callback is reported by finish()."""
+    cpu = ck.ClPlatforms.all().cpus(True, max_cpu_cores=1)
+    pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, True, 2)
+    pool.add_device(cpu + cpu)
+    tp = ClTaskPool()
+    plain = []
+    for i in range(40):
+        _, t = _task("fill", 256, float(i))
+        plain.append(t)
+        tp.feed(t)
+    _, bad = _task("fill", 256, 1.0)
+    bad.set_callback(lambda: 1 / 0)
+    tp.feed(bad)
+    pool.enqueue_task_pool(tp)
+    with pytest.raises(ck.ClComputeError, match="ZeroDivisionError"):
+        pool.finish()
+    assert all(t.device_index in (0, 1) for t in plain)
+    assert all(t.elapsed_ms >= 0 for t in plain)
+    assert not pool._notify and not pool._live  # nothing held after finish
+    assert len(pool._templates) == 1  # one shape, one template for the pool's lifetime
+    pool.dispose()
+
+
 SPIN = """
 __global__ void spin(float* x, int* it) {
   long long i = get_global_id(0);
