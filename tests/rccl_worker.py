@@ -41,12 +41,16 @@ def ref_k(a):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--cpu", action="store_true", help="control-plane rehearsal on CPU devices (gloo)")
+    ap.add_argument("--torchcomm", action="store_true",
+                    help="data-plane rehearsal: every GPU-mode check on CPU devices, collectives over gloo "
+                         "(TorchComm; the host array is each rank's replica)")
     ap.add_argument("--elems", type=int, default=256 * 1024)
     a = ap.parse_args()
     import cekirdekler_amd as ck
     from cekirdekler_amd.parallel.distributed import DistributedCruncher, init_distributed
 
-    ctx = init_distributed("gloo" if a.cpu else None)
+    tc = a.torchcomm
+    ctx = init_distributed("gloo" if (a.cpu or tc) else None)
     import torch.distributed as dist
 
     rank, world, n = ctx.rank, ctx.world, a.elems
@@ -55,6 +59,9 @@ def main() -> int:
     try:
         if a.cpu:
             cr = DistributedCruncher(SRC, ctx=ctx, devices=ck.ClPlatforms.all().cpus(True))
+        elif tc:
+            cr = DistributedCruncher(SRC, ctx=ctx, devices=ck.ClPlatforms.all().cpus(True), comm=True)
+            info["comm"] = type(cr._comm).__name__
         else:
             cr = DistributedCruncher(SRC, ctx=ctx, comm=True)
             info["gpu_ordinal"] = cr.devices.device(0).info.ordinal
@@ -64,6 +71,7 @@ def main() -> int:
         splits = []
         # 1) broadcast_reads + gather_writes, uneven splits
         x = ck.ClArray(data.copy() if rank == 0 or a.cpu else np.zeros(n, np.float32))
+        replica = (lambda arr: None) if tc else (lambda arr: (arr.array.fill(0), cr.download(arr, 0)))
         x.write = False
         y = ck.ClArray(np.zeros(n, np.float32))
         y.read = False
@@ -81,8 +89,7 @@ def main() -> int:
             checks["own_slice"] = bool(np.array_equal(y.array[lo:hi], want[lo:hi]))
         else:
             checks["host_replica_all"] = bool(np.array_equal(y.array, want))
-            y.array[:] = 0
-            cr.download(y, 0)
+            replica(y)
             checks["device_replica_all"] = bool(np.array_equal(y.array, want))
             rec = cr.last_record()
             info["broadcast_h2d_bytes"] = rec["h2d_bytes"]
@@ -116,11 +123,11 @@ def main() -> int:
                 r = cr.last_record()
                 moved.append(r["h2d_bytes"] + r["d2h_bytes"])
                 src, dst = dst, src
-            src.array[:] = 0
-            cr.download(src, 0)
+            replica(src)
             # float chains: compare with a tolerance (kernel fma vs numpy)
             checks["gather_flag_replica"] = bool(np.allclose(src.array, ref, rtol=1e-4, atol=1e-4))
             checks["gather_flag_no_host_traffic"] = all(m == 0 for m in moved[1:])
+
         cr.dispose()
     except Exception as e:  # report, never hang the other ranks
         checks["exception"] = False

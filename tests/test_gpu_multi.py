@@ -3,6 +3,16 @@ MI355X.  Every test skips unless this process sees enough GPUs, so the tier
 is inert on the one-GPU box and on the CPU tier; on an 8-GPU node it runs
 before any benchmark does.
 
+With ONE GPU the tier runs in rehearsal mode: the
+"GPUs" are REHEARSAL_DEVICES logical devices on disjoint CU partitions of
+GPU 0 (``ClDevices.cu_partitions``), every byte count, output and spread
+assertion stands, and only the path assertions change — peer copies
+between partitions of one GPU are ``local`` instead of ``xgmi``, the
+topology has one ordinal.  The torchrun data-plane test then runs the same
+worker logic over gloo with CPU devices (``TorchComm``) at world 2 and 4,
+since RCCL refuses two ranks on one GPU.  With two or more GPUs nothing
+changes.
+
 Covered: the peer topology (hipDeviceCanAccessPeer + access enabled by
 Cores), the single-process read fan-out over xGMI (reference: every device
 uploads every ``read`` array, Worker.cs:833-860), the keep-resident gather
@@ -27,6 +37,11 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+PHYSICAL = visible_gpus() >= 2
+REHEARSAL_DEVICES = 4
+PATH = "xgmi" if PHYSICAL else "local"  # device-to-device path between the test's "GPUs"
+
+
 def _need(n):
     why = multi_gpu_skip_reason(n)
     if why:
@@ -35,8 +50,12 @@ def _need(n):
 
 @pytest.fixture
 def gpus():
-    _need(2)
-    return ck.ClPlatforms.all().gpus()
+    g = ck.ClPlatforms.all().gpus()
+    if PHYSICAL:
+        return g
+    if len(g) == 0:
+        pytest.skip("no GPU visible")
+    return g[0].cu_partitions(REHEARSAL_DEVICES)  # rehearsal: logical devices on disjoint CUs
 
 
 def _all(gpus):
@@ -63,9 +82,13 @@ __global__ void hop(const float* x, float* y) {
 def test_peer_topology(gpus):
     cr = ck.ClNumberCruncher(_all(gpus), GATHER)
     topo = cr.peer_topology()
-    n = len(gpus)
+    n = len(gpus) if PHYSICAL else 1  # rehearsal: every logical device is GPU 0
     assert topo["ordinals"] == list(range(n))
     assert len(topo["matrix"]) == n and all(topo["matrix"][i][i] == 1 for i in range(n))
+    if not PHYSICAL:
+        assert topo["path"] == "none", topo
+        cr.dispose()
+        return
     assert topo["path"] in ("xgmi", "staged")
     # MI355X nodes: every GPU pair has a direct xGMI link
     assert topo["path"] == "xgmi", topo
@@ -75,7 +98,7 @@ def test_peer_topology(gpus):
 def test_read_fanout_across_gpus(gpus):
     n_dev = len(gpus)
     cr = ck.ClNumberCruncher(_all(gpus), GATHER)
-    path = cr.peer_topology()["path"]
+    path = cr.peer_topology()["path"] if PHYSICAL else "local"
     nb = (3 << 20) // 4 * n_dev
     b = ck.ClArray(np.random.default_rng(0).standard_normal(nb).astype(np.float32))
     b.write = False
@@ -90,10 +113,10 @@ def test_read_fanout_across_gpus(gpus):
         b.next_param(nbv, y).compute(cr, 1, "gather", n_out, 64)
         np.testing.assert_array_equal(y.array, b.array[(i * 7919) % nb] + np.float32(2) * b.array[nb - 1 - (i % nb)])
         rec = cr.last_record()
-        if path == "xgmi":
+        if path in ("xgmi", "local"):
             assert rec["h2d_bytes"] == b.array.nbytes + n_dev * 4, rec
             assert rec["p2p_bytes"] == (n_dev - 1) * b.array.nbytes, rec
-            assert rec["p2p_path"] == "xgmi" and rec["staged_bytes"] == 0, rec
+            assert rec["p2p_path"] == path and rec["staged_bytes"] == 0, rec
         else:  # explicit PCIe fallback: one whole upload per device
             assert rec["p2p_path"] == "pcie" and rec["h2d_bytes"] == n_dev * (b.array.nbytes + 4), rec
     cr.dispose()
@@ -120,7 +143,7 @@ def test_gather_flag_across_gpus(gpus):
         if it:
             assert rec["h2d_bytes"] == 0 and rec["d2h_bytes"] == 0, rec
         assert rec["gather_bytes"] == (n_dev - 1) * n * 4, rec
-        assert rec["p2p_path"] == "xgmi", rec  # MI355X: never host-staged
+        assert rec["p2p_path"] == PATH, rec  # MI355X: never host-staged
         src, dst = dst, src
     for d in range(n_dev):
         src.array[:] = 0
@@ -218,6 +241,23 @@ def test_rccl_data_plane_torchrun(nproc):
     """torch.distributed.run child job, one rank per GPU (nproc 0: all of
     them): broadcast_reads, split_reads, gather_writes with uneven splits,
     and the keep-resident gather flag; every rank checks its replicas."""
+    if not PHYSICAL:
+        if visible_gpus() == 0:
+            pytest.skip("no GPU visible (the CPU tier runs this rehearsal: test_multi_gating.py)")
+        # rehearsal: the same worker checks over gloo on CPU devices
+        # (TorchComm), ranks 2 and 4 (RCCL refuses two ranks on one GPU)
+        n = nproc or REHEARSAL_DEVICES
+        cmd = torchrun_cmd(os.path.join(HERE, "rccl_worker.py"), n, ["--torchcomm"])
+        env = child_env()
+        env["CEK_CPU_THREADS"] = "2"
+        r = subprocess.run(cmd, cwd=HERE, env=env, capture_output=True, text=True, timeout=240)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert r.returncode == 0 and lines, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+        out = json.loads(lines[-1])
+        assert out["ok"] and out["ranks"] == n, json.dumps(out)[:3000]
+        assert out["per_rank"][0]["uneven"], out["per_rank"][0]
+        assert all(o["backend"] == "gloo" for o in out["per_rank"])
+        return
     n = nproc or visible_gpus()
     _need(max(2, n))
     cmd = torchrun_cmd(os.path.join(HERE, "rccl_worker.py"), n)
@@ -237,6 +277,11 @@ def test_xgmi_link_bandwidth_floor(gpus):
     pair at once must beat one pair alone (the links are point to point)."""
     from cekirdekler_amd.utils.multigpu import peer_bandwidth_report
 
+    if not PHYSICAL:  # rehearsal: the same measurement inside GPU 0 (no link to be bound by)
+        rep = peer_bandwidth_report([0, 0], reps=3)
+        assert rep["all_verified"], rep
+        assert rep["min_pair_gbps"] >= 50.0, rep
+        return
     rep = peer_bandwidth_report(list(range(len(gpus))), reps=3)
     assert rep["all_verified"], rep
     assert rep["min_pair_gbps"] >= 50.0, rep

@@ -72,6 +72,28 @@ def test_rank_worker_control_plane_two_gloo_ranks():
     assert out["per_rank"][0]["uneven"], out
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_rank_worker_data_plane_torchcomm(world):
+    """the RCCL worker's data-plane checks (broadcast of
+    reads from rank 0, split reads, all-gather of written slices with uneven
+    splits, keep-resident gather ping-pong with no host traffic) over
+    TorchComm / gloo on CPU devices, at world 2 and 4."""
+    cmd = torchrun_cmd(os.path.join(HERE, "rccl_worker.py"), world, ["--torchcomm", "--elems", str(256 * 256)])
+    env = child_env()
+    env["CEK_CPU_THREADS"] = "1"
+    r = subprocess.run(cmd, cwd=HERE, env=env, capture_output=True, text=True, timeout=240)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and lines, (r.stdout[-2000:], r.stderr[-2000:])
+    out = json.loads(lines[-1])
+    assert out["ok"] and out["splits_identical"] and out["ranks"] == world, json.dumps(out)[:3000]
+    per = out["per_rank"]
+    assert per[0]["uneven"] and all(o["comm"] == "TorchComm" for o in per), per[0]
+    assert all(set(o["checks"]) >= {"host_replica_all", "split_reads_slice", "gather_flag_replica",
+                                    "gather_flag_no_host_traffic"} for o in per)
+    # rank 0 alone uploads for the broadcast of reads
+    assert per[0]["broadcast_h2d_bytes"] > 0 and all(o["broadcast_h2d_bytes"] == 0 for o in per[1:])
+
+
 def test_peer_pairs_and_report_shape(monkeypatch):
     """The xGMI bandwidth report's structure, on a fake measurement backend
     (the real one needs GPUs): pairs chosen, both engines per pair, the
