@@ -706,8 +706,10 @@ def compact_extra(full: dict, detail: str) -> dict:
                                    for k, v in hs.items() if k.startswith("iters_") and isinstance(v, dict)}
     wv = full.get("wave_cpu_gpu")
     if isinstance(wv, dict):
-        w = _pick(wv, ["cpu_ms_per_frame", "gpu_ms_per_frame", "gpu+cpu_ms_per_frame", "gpu+cpu_fit_ms_per_frame",
-                       "speedup_gpu+cpu_over_cpu", "speedup_gpu_over_cpu", "speedup_gpu+cpu_fit_over_cpu"], 4)
+        w = _pick(wv, ["reference_cpu_ms_per_frame", "cpu_ms_per_frame", "gpu_ms_per_frame", "gpu+cpu_ms_per_frame",
+                       "gpu+cpu_fit_ms_per_frame", "speedup_gpu+cpu_over_reference_cpu",
+                       "speedup_gpu_over_reference_cpu", "speedup_gpu+cpu_over_cpu", "speedup_gpu_over_cpu",
+                       "speedup_gpu+cpu_fit_over_cpu"], 4)
         pred = wv.get("gpu+cpu_fit_predictor")
         if isinstance(pred, dict):
             w["fit_decision"] = pred.get("decision")
@@ -717,7 +719,8 @@ def compact_extra(full: dict, detail: str) -> dict:
     po = full.get("pipeline_overlap")
     if isinstance(po, dict):
         p = _pick(po, ["read_compute_write_ms", "ideal_speedup_sum_over_max", "pipeline_speedup_event",
-                       "pipeline_speedup_driver", "best_event", "best_event_4streams", "default_compute_streams",
+                       "pipeline_speedup_driver", "pipeline_speedup_driver_in_queue",
+                       "pipeline_speedup_driver_reads_main", "best_event", "best_event_4streams", "default_compute_streams",
                        "best_driver_default", "best_driver_q4", "best_driver_q16", "event_5_vs_4_streams",
                        "driver_default_q4_q16", "outputs_exact", "lcg_iters"])
         if isinstance(po.get("ms"), dict):
@@ -744,6 +747,11 @@ def compact_extra(full: dict, detail: str) -> dict:
             t["makespan_over_concurrent_ideal"] = _r(cs.get("makespan_over_ideal"))
             t["contention_factor"] = _r(cs.get("contention_factor"))
         t["makespan_over_greedy_sim"] = _r(tp.get("makespan_over_greedy_sim"))
+        pj = tp.get("projected_8gpu")
+        if isinstance(pj, dict):
+            t["projected_8gpu_makespan_over_ideal"] = _r(pj.get("makespan_over_ideal"))
+            t["projected_8gpu_serial_host_over_ideal"] = _r(pj.get("makespan_serial_host_over_ideal"))
+            t["dispatch_tasks_per_s_one_device"] = pj.get("dispatch_tasks_per_s_one_device")
         ex["task_pool"] = t
     nb = full.get("nbody_pipeline")
     if isinstance(nb, dict):
@@ -756,7 +764,7 @@ def compact_extra(full: dict, detail: str) -> dict:
         ex["nbody_pipeline"] = n
     # ---- the headline metric's components, last ----
     lb = full.get("load_balance_iters") or {}
-    ex["load_balance_iters"] = _pick(lb, ["iters", "steady_share_dev0"], 4) if lb else None
+    ex["load_balance_iters"] = _pick(lb, ["iters", "steady_share_dev0", "calls"], 4) if lb else None
     mb = full.get("mandelbrot_4k") or {}
     if mb:
         m = _pick(mb, ["ms", "gflops", "kernel"], 4)

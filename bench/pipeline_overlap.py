@@ -152,12 +152,30 @@ def main():
         configs.append((f"driver_b{b}_qd", lambda c, i, b=b: call(crs["qd"], i, True, ck.PIPELINE_DRIVER, b), None))
         configs.append((f"driver_b{b}_q4", lambda c, i, b=b: call(crs["q4"], i, True, ck.PIPELINE_DRIVER, b), None))
         configs.append((f"driver_b{b}_q16", lambda c, i, b=b: call(crs["q16"], i, True, ck.PIPELINE_DRIVER, b), None))
+        # the reference's layout: each blob's download in its compute queue
+        # (driver_downloads_own_stream off)
+        configs.append((f"driver_b{b}_inqueue", lambda c, i, b=b: call(crs["qd"], i, True, ck.PIPELINE_DRIVER, b),
+                        "downloads_in_queue"))
+        configs.append((f"driver_b{b}_readsmain", lambda c, i, b=b: call(crs["qd"], i, True, ck.PIPELINE_DRIVER, b),
+                        "reads_main"))
     ids = {name: next(cid) for name, _, _ in configs}
     times = {name: [] for name, _, _ in configs}
     exact = {name: True for name, _, _ in configs}
     piped, moved = {}, {}
 
     def run(name, fn, layout):
+        if layout == "reads_main":
+            crs["qd"].cores.driver_reads_on_main_stream = True
+            try:
+                return fn(None, ids[name])
+            finally:
+                crs["qd"].cores.driver_reads_on_main_stream = False
+        if layout == "downloads_in_queue":
+            crs["qd"].cores.driver_downloads_own_stream = False
+            try:
+                return fn(None, ids[name])
+            finally:
+                crs["qd"].cores.driver_downloads_own_stream = True
         c = crs["q16"] if layout else None
         if c is not None:
             c.cores.pipeline_writes_one_stream = True
@@ -171,7 +189,8 @@ def main():
         y.array[:] = 0
         run(name, fn, layout)
         exact[name] &= bool(np.array_equal(y.array, want))
-        c = crs["q16"] if ("q16" in name or layout) else (crs["q4"] if name.endswith("_q4") else crs["qd"])
+        c = crs["q16"] if ("q16" in name or layout == "writes_one_stream") else (
+            crs["q4"] if name.endswith("_q4") else crs["qd"])
         rec = c.last_record()
         piped[name] = bool(rec["pipelined"])
         moved[name] = [int(rec["h2d_bytes"]), int(rec["d2h_bytes"])]
@@ -187,6 +206,8 @@ def main():
     dqd = min((k for k in res if k.startswith("driver_") and k.endswith("_qd")), key=res.get)
     dq4 = min((k for k in res if k.startswith("driver_") and k.endswith("_q4")), key=res.get)
     dq16 = min((k for k in res if k.endswith("q16")), key=res.get)
+    dinq = min((k for k in res if k.endswith("_inqueue")), key=res.get)
+    drm = min((k for k in res if k.endswith("_readsmain")), key=res.get)
     parts = [up_ms, kernel_ms, down_ms]
     out = {
         "config": "pipeline_overlap_balanced",
@@ -204,8 +225,13 @@ def main():
         "best_driver_q16": dq16,
         "pipeline_speedup_event": round(base / min(res[ev], res[ev4]), 3),
         "pipeline_speedup_driver": round(base / min(res[dqd], res[dq4], res[dq16]), 3),
+        "pipeline_speedup_driver_in_queue": round(base / res[dinq], 3),
         "event_5_vs_4_streams": [res[ev], res[ev4]],
         "driver_default_q4_q16": [res[dqd], res[dq4], res[dq16]],
+        "best_driver_downloads_in_queue": dinq,
+        "driver_own_download_stream_vs_in_queue": [res[dqd], res[dinq]],
+        "best_driver_reads_main": drm,
+        "pipeline_speedup_driver_reads_main": round(base / res[drm], 3),
         "timing": f"median of {a.rounds} interleaved rounds of {a.calls} calls per config",
     }
     for c in crs.values():

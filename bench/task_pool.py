@@ -178,6 +178,33 @@ for _, grp, kern, G, L, _ in work:
         x.read, x.write, x.partial_read = r, w, p
 single = [sp["end_ms"] - sp["begin_ms"] for sp in ref_cr.timeline()]
 assert len(single) == len(work), (len(single), len(work))
+ref_cr.record_timeline = False
+
+
+def time_alone(cr):
+    """hipEvent device time of every task alone on ``cr`` (device-resident)."""
+    for _, grp, kern, G, L, _ in work:
+        grp.compute(cr, 1, kern, G, L)
+    sync()
+    cr.record_timeline = True
+    for _, grp, kern, G, L, _ in work:
+        flags = [(x.read, x.write, x.partial_read) for x in grp.arrays]
+        dev_only(*grp.arrays)
+        grp.compute(cr, 1, kern, G, L)
+        for x, (r, w, p) in zip(grp.arrays, flags):
+            x.read, x.write, x.partial_read = r, w, p
+    out = [sp["end_ms"] - sp["begin_ms"] for sp in cr.timeline()]
+    cr.record_timeline = False
+    return out
+
+
+# the same tasks alone on a WHOLE GPU: the basis of the 8-GPU projection
+if partitioned:
+    whole_cr = ck.ClNumberCruncher(g[0], SRC, prebuilt=prebuilt)
+    single_whole = time_alone(whole_cr)
+    whole_cr.dispose()
+else:
+    single_whole = list(single)
 per_kind = collections.defaultdict(list)
 for (kind, *_), ms in zip(work, single):
     per_kind[kind].append(ms)
@@ -288,6 +315,36 @@ def run_policy(policy, spans=False):
     return n, ms, counts, dispatch, concurrent
 
 
+def dispatch_one_device(dev, tasks=4096):
+    """Tasks per second through a pool of ONE whole-GPU device: the host cost
+    per task of one consumer thread that has its GPU to itself (on an 8-GPU
+    node every consumer does)."""
+    pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, True, a.queues, prebuilt=prebuilt)
+    pool.add_device(dev)
+    xs = [ck.ClArray(np.zeros(256, np.float32)) for _ in range(64)]
+    for x in xs:
+        x.read = x.write = False
+        pool.crunchers[0].upload(x)
+    pool.crunchers[0].upload(serial_v)
+
+    def tiny(k):
+        t = ClTaskPool()
+        for i in range(k):
+            t.feed(xs[i % 64].next_param(serial_v).task(3, "add", 256, 256))
+        return t
+    pool.enqueue_task_pool(tiny(512))
+    pool.finish()
+    tp = tiny(tasks)
+    sync()
+    t0 = time.perf_counter()
+    pool.enqueue_task_pool(tp)
+    pool.finish()
+    sync()
+    rate = tasks / (time.perf_counter() - t0)
+    pool.dispose()
+    return rate
+
+
 ntasks, makespan, counts, dispatch, concurrent = run_policy(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, spans=True)
 ideal = sum(single) / (len(devs) if partitioned else max(1, ng))
 
@@ -312,6 +369,23 @@ greedy_ms = greedy_fifo_ms(single, len(devs) if partitioned else max(1, ng), len
 greedy_ms_contended = greedy_fifo_ms([t * contention for t in single], len(devs) if partitioned else max(1, ng),
                                      len(work) // 2)
 _, makespan_rr, counts_rr, dispatch_rr, _ = run_policy(ClDevicePoolType.DEVICE_ROUND_ROBIN)
+
+# Projection to 8 GPUs: the reference's FIFO-greedy
+# policy over 8 devices on the tasks' WHOLE-GPU alone times, each task
+# costing its device max(device time, h) — h = one consumer's host cost per
+# task with its GPU to itself, hidden behind the device while the pool keeps
+# two or more tasks in flight — and, as an upper bound, device time + h
+# (no overlap at all); ideal = Σ whole-GPU times / 8.
+one_dev_rate = dispatch_one_device(g[0])
+h_ms = 1e3 / one_dev_rate
+proj_ideal = sum(single_whole) / 8
+proj = greedy_fifo_ms([max(t, h_ms) for t in single_whole], 8, len(work) // 2)
+proj_serial = greedy_fifo_ms([t + h_ms for t in single_whole], 8, len(work) // 2)
+projection = {"devices": 8, "basis": "whole-GPU alone device times, FIFO greedy with the mid-pool barrier",
+              "host_us_per_task_one_consumer": round(1e3 * h_ms, 2), "dispatch_tasks_per_s_one_device": round(one_dev_rate),
+              "ideal_ms": proj_ideal, "makespan_ms": proj, "makespan_over_ideal": proj / proj_ideal,
+              "makespan_serial_host_ms": proj_serial, "makespan_serial_host_over_ideal": proj_serial / proj_ideal,
+              "median_task_whole_gpu_us": round(1e3 * float(np.median(single_whole)), 2)}
 
 # checks: serial group order (x ← 2x + 1, eight times from 0 = 255), one GEMM, one reduction
 serial_ok = bool(np.all(serial_x.array == 255.0))
@@ -351,6 +425,7 @@ emit({"config": "task_pool_256", "tasks": ntasks, "gpus": ng, "logical_devices":
       "round_robin": {"makespan_ms": makespan_rr, "makespan_over_ideal": makespan_rr / ideal,
                       "per_device_tasks": counts_rr, "dispatch_tasks_per_s": round(dispatch_rr)},
       "dispatch_tasks_per_s": round(dispatch), "pool_devices": len(devs),
+      "projected_8gpu": projection,
       "gemm_task_max_rel_err": gemm_err, "reduce_task_rel_err": red_err})
 ref_cr.dispose()
 if not (serial_ok and gemm_err < 5e-3 and red_err < 1e-4):

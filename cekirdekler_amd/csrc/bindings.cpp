@@ -462,6 +462,8 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("pipeline_reads_two_streams", &Cores::pipeline_reads_two_streams)
       .def_readwrite("sleep_waits", &Cores::sleep_waits)
       .def_readwrite("pipeline_writes_one_stream", &Cores::pipeline_writes_one_stream)
+      .def_readwrite("driver_downloads_own_stream", &Cores::driver_downloads_own_stream)
+      .def_readwrite("driver_reads_on_main_stream", &Cores::driver_reads_on_main_stream)
       .def_readwrite("peer_read_min_bytes", &Cores::peer_read_min_bytes)
       .def_readwrite("graph_min_launches", &Cores::graph_min_launches)
       .def_readwrite("auto_failover", &Cores::auto_failover)

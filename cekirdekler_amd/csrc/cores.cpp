@@ -1560,6 +1560,12 @@ void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long
   const int full_slot = slot++;
   const int nq = wk.queue_concurrency();
   std::vector<char> used(16, 0);
+  // the download stream (the event pipeline's first write stream, id 19 in
+  // the schedule log)
+  const bool own_dl = driver_downloads_own_stream;
+  hipStream_t ds = own_dl && wk.gpu() ? wk.pipe_stream(0, 2) : nullptr;
+  const int dsid = 19;
+  bool ds_used = false;
   for (long long k = 0; k < B; ++k) {
     int qi = static_cast<int>(k % nq);
     hipStream_t s = wk.compute_stream(qi);
@@ -1569,24 +1575,63 @@ void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long
     }
     used[qi] = 1;
     long long off = ref + k * chunk;
+    // reads_main: the blob's upload goes into the main stream's one in-order
+    // chain of copies and its queue waits for it, so no upload waits behind
+    // an earlier blob's kernel in a compute queue
+    const bool reads_main = driver_reads_on_main_stream && wk.gpu();
+    hipStream_t rs = reads_main ? m : s;
+    bool reads = false;
     for (auto& a : c.arrays) {
       if (a.zc || !a.partial) continue;
       uint64_t b, n;
       a.slice(off, chunk, c.local_range, b, n);
-      wk.h2d(s, a, b, n);
+      wk.h2d(rs, a, b, n);
       *h2d += n * a.elem_size;
+      reads = true;
     }
-    log_op(gidx, "h2d", 1 + qi, off, chunk);
+    log_op(gidx, "h2d", reads_main ? 0 : 1 + qi, off, chunk);
+    if (reads_main && reads) {
+      hipEvent_t er = wk.event(slot);
+      CEK_HIP(hipEventRecord(er, m));
+      CEK_HIP(hipStreamWaitEvent(s, er, 0));
+      log_op(gidx, "rec", 0, off, chunk, slot);
+      log_op(gidx, "wait", 1 + qi, off, chunk, slot);
+      ++slot;
+    }
     launch_kernels(wk, s, c, off, chunk);
     log_op(gidx, "kernel", 1 + qi, off, chunk);
+    bool writes = false;
+    for (auto& a : c.arrays) writes |= !a.zc && a.write && !a.write_all;
+    hipStream_t w = s;
+    const bool to_ds = own_dl && writes && wk.gpu();
+    if (to_ds) {
+      hipEvent_t ek = wk.event(slot);
+      CEK_HIP(hipEventRecord(ek, s));
+      CEK_HIP(hipStreamWaitEvent(ds, ek, 0));
+      w = ds;
+      log_op(gidx, "rec", 1 + qi, off, chunk, slot);
+      log_op(gidx, "wait", dsid, off, chunk, slot);
+      ++slot;
+      ds_used = true;
+    }
     for (auto& a : c.arrays) {
       if (a.zc || !a.write || a.write_all) continue;
       uint64_t b, n;
       a.slice(off, chunk, c.local_range, b, n);
-      wk.d2h(s, a, b, n);
+      wk.d2h(w, a, b, n);
       *d2h += n * a.elem_size;
     }
-    log_op(gidx, "d2h", 1 + qi, off, chunk);
+    log_op(gidx, "d2h", to_ds ? dsid : 1 + qi, off, chunk);
+  }
+  if (ds_used) {  // the call ends after the last download
+    if (wk.gpu()) {
+      hipEvent_t e = wk.event(slot);
+      CEK_HIP(hipEventRecord(e, ds));
+      CEK_HIP(hipStreamWaitEvent(m, e, 0));
+    }
+    log_op(gidx, "rec", dsid, 0, 0, slot);
+    log_op(gidx, "wait", 0, 0, 0, slot);
+    ++slot;
   }
   for (int q = 0; q < 16; ++q) {
     if (!used[q]) continue;
@@ -1628,7 +1673,8 @@ void Cores::run_device_body(int w, const ComputeCall& c, long long ref, long lon
                        double* out_ms, uint64_t* h2d, uint64_t* d2h) {
   Worker& wk = *workers_[w];
   const int gidx = global_base_ + w;
-  TraceRange tr("cek.device" + std::to_string(gidx) + ".id" + std::to_string(c.compute_id));
+  TraceRange tr(trace_enabled() ? "cek.device" + std::to_string(gidx) + ".id" + std::to_string(c.compute_id)
+                                : std::string());
   t_phase_wait = 0;
   if (range > 0 && inject_[w] > 0) {
     --inject_[w];
@@ -1749,7 +1795,7 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
   const long long U = c.granularity > 0 ? c.granularity : L;  // balancer unit
   if (U % L != 0) throw Error("granularity must be a multiple of the local range");
   if (G % U != 0) throw Error("global range must be a multiple of the granularity");
-  TraceRange tr("cek.compute.id" + std::to_string(c.compute_id));
+  TraceRange tr(trace_enabled() ? "cek.compute.id" + std::to_string(c.compute_id) : std::string());
   double wall0 = now_ms();
 
   auto it = state_.find(c.compute_id);

@@ -355,6 +355,15 @@ class Cores {
   // (profiles/hostres_streaming.md, tools/hostres_stall_probe.py)
   bool pipeline_reads_on_main_stream = true;
   bool pipeline_reads_two_streams = false;
+  // driver pipeline (Cores.cs:1368-1858): blob k's upload and kernels stay on
+  // queue k mod Q, its download goes to one download stream gated by the
+  // blob's kernel event, so no blob's D2H waits in a compute queue ahead of a
+  // later blob's upload.  Off: the reference's
+  // read→compute→write on the one queue.
+  bool driver_downloads_own_stream = true;
+  // driver pipeline: blob uploads on the main stream (one in-order chain of
+  // copies, as the event pipeline's), each blob's queue waiting for its own
+  bool driver_reads_on_main_stream = false;
   // GPU workers wait for their streams by sleeping on a blocking-sync event
   // (off by default; CEK_SLEEP_WAITS=1)
   bool sleep_waits = false;  // explicit blobs: partial arrays alternate over two upload streams (slower: 12.7 vs 7.1 ms for the shells, the extra stream shares a hardware queue)

@@ -222,8 +222,24 @@ void DevicePool::results(long long first, long long n, std::vector<int>& dev, st
 int DevicePool::retire(int dev, std::vector<Inflight>& inflight) {
   Cores& cr = *devs_[dev];
   int n = 0;
+  // one marker query per stream slot per poll (a slot's markers retire in
+  // order), not one per task in flight: every query takes the HIP runtime's
+  // lock that the other consumers' launches need
+  int slots[16];
+  uint64_t words[16];
+  int nslots = 0;
+  auto word = [&](int slot) {
+    for (int j = 0; j < nslots; ++j)
+      if (slots[j] == slot) return words[j];
+    const uint64_t w = cr.marker_word(0, slot);
+    if (nslots < 16) {
+      slots[nslots] = slot;
+      words[nslots++] = w;
+    }
+    return w;
+  };
   for (size_t i = 0; i < inflight.size();) {
-    if (cr.marker_word(0, inflight[i].slot) >= inflight[i].value) {
+    if (word(inflight[i].slot) >= inflight[i].value) {
       complete(dev, inflight[i].id, inflight[i].notify, now_ms() - inflight[i].t0, "");
       inflight[i] = inflight.back();
       inflight.pop_back();

@@ -653,13 +653,28 @@ void Worker::launch(hipStream_t s, const std::string& kernel, const std::vector<
     long long groups = count / local;
     // chunk groups so every pool thread gets several (amortise dispatch)
     long long nthreads = pool_->size();
-    long long per = std::max<long long>(1, groups / (nthreads * 8));
-    long long tasks = (groups + per - 1) / per;
+    long long tasks_max = std::max<long long>(1, std::min(groups, (nthreads + 1) * 8));
+    // ...but no task shorter than kCpuMinTaskNs by this kernel's measured
+    // cost per work item: a small range (the CPU's share of a GPU+CPU wave
+    // frame is ~1,400 vertices) runs on the calling thread alone instead of
+    // paying every pool thread's wake-up
+    double& est = cpu_item_ns_[kernel];
+    if (est > 0) {
+      const double by_work = est * static_cast<double>(count) / kCpuMinTaskNs;
+      tasks_max = std::max<long long>(1, std::min<long long>(tasks_max, static_cast<long long>(by_work)));
+    }
+    const long long per = (groups + tasks_max - 1) / tasks_max;
+    const long long tasks = (groups + per - 1) / per;
     void** argv = ptrs.data();
+    const double t0 = now_ms();
     pool_->parallel_for(tasks, [&](long long t) {
       long long g0 = t * per, g1 = std::min(groups, g0 + per);
       fn(argv, offset, gsize, offset + g0 * local, (g1 - g0) * local, local);
     });
+    // per-item cost on one thread: wall time × the threads that ran
+    const double used = static_cast<double>(std::min<long long>(tasks, nthreads + 1));
+    const double ns = (now_ms() - t0) * 1e6 * used / static_cast<double>(std::max<long long>(1, count));
+    est = est > 0 ? 0.7 * est + 0.3 * ns : ns;
   }
 }
 

@@ -270,6 +270,10 @@ class Worker {
     std::string kernel;
     hipEvent_t start, stop;
   };
+  // CPU device: measured ns per work item per kernel (one thread), and the
+  // shortest task worth handing to a pool thread
+  std::unordered_map<std::string, double> cpu_item_ns_;
+  static constexpr double kCpuMinTaskNs = 20000.0;
   std::deque<KernelStamp> kstamps_;  // ring: the oldest are dropped past kMaxKernelStamps
   static constexpr size_t kMaxKernelStamps = 1 << 16;
   std::vector<hipEvent_t> kstamp_spare_;
