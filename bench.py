@@ -720,7 +720,7 @@ def compact_extra(full: dict, detail: str) -> dict:
     if isinstance(po, dict):
         p = _pick(po, ["read_compute_write_ms", "ideal_speedup_sum_over_max", "pipeline_speedup_event",
                        "pipeline_speedup_driver", "pipeline_speedup_driver_in_queue",
-                       "pipeline_speedup_driver_reads_main", "best_event", "best_event_4streams", "default_compute_streams",
+                       "pipeline_speedup_driver_reads_in_queue", "best_event", "best_event_4streams", "default_compute_streams",
                        "best_driver_default", "best_driver_q4", "best_driver_q16", "event_5_vs_4_streams",
                        "driver_default_q4_q16", "outputs_exact", "lcg_iters"])
         if isinstance(po.get("ms"), dict):

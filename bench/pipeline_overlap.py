@@ -10,8 +10,12 @@ exactly that case and runs it through ``compute()`` three ways:
 * ``event``   — the event-driven pipeline (Cores.cs:1197-1367): two
   interleaved half-pipelines of {upload, kernel, download} streams with
   event edges, at 4 / 8 / 16 blobs;
-* ``driver``  — the driver-driven pipeline (Cores.cs:1368-1958): blob k does
-  upload, kernel and download in order on queue k mod Q, at 4 / 8 / 16 blobs.
+* ``driver``  — the driver-driven pipeline (Cores.cs:1368-1958): blob k's
+  kernels on queue k mod Q, at 4 / 8 / 16 blobs.  Default layout: the
+  uploads in the main stream's one chain of copies, the downloads on one
+  download stream, each gated by events (``_inqueue``: the reference's
+  upload→kernel→download in order on the queue; ``_readsq``: uploads in the
+  queue, downloads on their own stream).
 
 The kernel is a user kernel string (hiprtc), one uint32 in and one out per
 work item, with ``iters`` LCG steps per element.  ``iters`` is calibrated at
@@ -152,30 +156,29 @@ def main():
         configs.append((f"driver_b{b}_qd", lambda c, i, b=b: call(crs["qd"], i, True, ck.PIPELINE_DRIVER, b), None))
         configs.append((f"driver_b{b}_q4", lambda c, i, b=b: call(crs["q4"], i, True, ck.PIPELINE_DRIVER, b), None))
         configs.append((f"driver_b{b}_q16", lambda c, i, b=b: call(crs["q16"], i, True, ck.PIPELINE_DRIVER, b), None))
-        # the reference's layout: each blob's download in its compute queue
-        # (driver_downloads_own_stream off)
+        # the reference's layout: each blob's upload, kernels and download in
+        # order on its queue (driver_reads_on_main_stream and
+        # driver_downloads_own_stream off); and uploads in the queue with the
+        # downloads on their own stream
         configs.append((f"driver_b{b}_inqueue", lambda c, i, b=b: call(crs["qd"], i, True, ck.PIPELINE_DRIVER, b),
                         "downloads_in_queue"))
-        configs.append((f"driver_b{b}_readsmain", lambda c, i, b=b: call(crs["qd"], i, True, ck.PIPELINE_DRIVER, b),
-                        "reads_main"))
+        configs.append((f"driver_b{b}_readsq", lambda c, i, b=b: call(crs["qd"], i, True, ck.PIPELINE_DRIVER, b),
+                        "reads_in_queue"))
     ids = {name: next(cid) for name, _, _ in configs}
     times = {name: [] for name, _, _ in configs}
     exact = {name: True for name, _, _ in configs}
     piped, moved = {}, {}
 
     def run(name, fn, layout):
-        if layout == "reads_main":
-            crs["qd"].cores.driver_reads_on_main_stream = True
+        if layout in ("reads_in_queue", "downloads_in_queue"):
+            cc = crs["qd"].cores
+            cc.driver_reads_on_main_stream = False
+            cc.driver_downloads_own_stream = layout == "reads_in_queue"
             try:
                 return fn(None, ids[name])
             finally:
-                crs["qd"].cores.driver_reads_on_main_stream = False
-        if layout == "downloads_in_queue":
-            crs["qd"].cores.driver_downloads_own_stream = False
-            try:
-                return fn(None, ids[name])
-            finally:
-                crs["qd"].cores.driver_downloads_own_stream = True
+                cc.driver_reads_on_main_stream = True
+                cc.driver_downloads_own_stream = True
         c = crs["q16"] if layout else None
         if c is not None:
             c.cores.pipeline_writes_one_stream = True
@@ -207,7 +210,7 @@ def main():
     dq4 = min((k for k in res if k.startswith("driver_") and k.endswith("_q4")), key=res.get)
     dq16 = min((k for k in res if k.endswith("q16")), key=res.get)
     dinq = min((k for k in res if k.endswith("_inqueue")), key=res.get)
-    drm = min((k for k in res if k.endswith("_readsmain")), key=res.get)
+    drq = min((k for k in res if k.endswith("_readsq")), key=res.get)
     parts = [up_ms, kernel_ms, down_ms]
     out = {
         "config": "pipeline_overlap_balanced",
@@ -230,8 +233,8 @@ def main():
         "driver_default_q4_q16": [res[dqd], res[dq4], res[dq16]],
         "best_driver_downloads_in_queue": dinq,
         "driver_own_download_stream_vs_in_queue": [res[dqd], res[dinq]],
-        "best_driver_reads_main": drm,
-        "pipeline_speedup_driver_reads_main": round(base / res[drm], 3),
+        "best_driver_reads_in_queue": drq,
+        "pipeline_speedup_driver_reads_in_queue": round(base / res[drq], 3),
         "timing": f"median of {a.rounds} interleaved rounds of {a.calls} calls per config",
     }
     for c in crs.values():

@@ -464,6 +464,7 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("pipeline_writes_one_stream", &Cores::pipeline_writes_one_stream)
       .def_readwrite("driver_downloads_own_stream", &Cores::driver_downloads_own_stream)
       .def_readwrite("driver_reads_on_main_stream", &Cores::driver_reads_on_main_stream)
+      .def_readwrite("inline_largest_share", &Cores::inline_largest_share)
       .def_readwrite("peer_read_min_bytes", &Cores::peer_read_min_bytes)
       .def_readwrite("graph_min_launches", &Cores::graph_min_launches)
       .def_readwrite("auto_failover", &Cores::auto_failover)
@@ -573,13 +574,14 @@ PYBIND11_MODULE(_cek, m) {
       .def(py::init<std::vector<std::shared_ptr<Cores>>, int, int>(), py::arg("devices"), py::arg("max_in_flight"),
            py::arg("policy") = 0, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("policy", &DevicePool::policy)
-      .def("enqueue", &DevicePool::enqueue, py::call_guard<py::gil_scoped_release>())
+      .def("enqueue", &DevicePool::enqueue, py::arg("tasks"), py::arg("pool_total") = -1, py::arg("append") = false,
+           py::call_guard<py::gil_scoped_release>())
       // the batch form: task i = template calls[which[i]] with its own arrays,
       // type and id (one crossing and no per-task Python objects)
       .def("enqueue_batch",
            [](DevicePool& p, const std::vector<ComputeCall>& calls, const std::vector<int>& which,
               std::vector<std::vector<ArraySpec>> arrays, const std::vector<uint32_t>& types,
-              const std::vector<long long>& ids) {
+              const std::vector<long long>& ids, long long pool_total, bool append) {
              const size_t n = which.size();
              if (arrays.size() != n || types.size() != n || ids.size() != n)
                throw Error("enqueue_batch: which, arrays, types and ids must have one entry per task");
@@ -600,8 +602,10 @@ PYBIND11_MODULE(_cek, m) {
                ts[i].id = ids[i];
              }
              py::gil_scoped_release r;
-             p.enqueue(std::move(ts));
-           })
+             p.enqueue(std::move(ts), pool_total, append);
+           },
+           py::arg("calls"), py::arg("which"), py::arg("arrays"), py::arg("types"), py::arg("ids"),
+           py::arg("pool_total") = -1, py::arg("append") = false)
       .def("take_errors", &DevicePool::take_errors)
       .def("results",
            [](DevicePool& p, long long first, long long n) {

@@ -51,6 +51,7 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
   if (const char* e = std::getenv("CEK_DEVICE_SPANS")) device_spans = std::string(e) != "0";
   if (const char* e = std::getenv("CEK_SINGLE_DEVICE_SPANS")) single_device_spans = std::string(e) == "1";
   if (const char* e = std::getenv("CEK_DEFER_DOWNLOADS")) deferred_downloads = std::string(e) != "0";
+  if (const char* e = std::getenv("CEK_INLINE_LARGEST")) inline_largest_share = std::string(e) != "0";
   if (const char* e = std::getenv("CEK_KERNEL_D2H")) set_kernel_d2h(std::string(e) != "0");
   if (const char* e = std::getenv("CEK_ZC_RELEASE")) zc_release = std::string(e) != "0";
   // CEK_SLEEP_WAITS=1: GPU workers wait for their streams by sleeping on a
@@ -1920,9 +1921,21 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
     // CPU device is preferred there — its work is the calling thread plus
     // the CPU pool either way, and the GPU workers are posted first so
     // their launches go out while the CPU computes.
+    // With CPU + GPU, the participant holding the
+    // largest share runs here: a GPU that takes 99 % of a wave frame keeps
+    // the GPU-alone path (launch and wait on this thread) and the CPU's
+    // sliver goes to its worker, whose hand-off hides behind the GPU's
+    // frame; a CPU holding most of a host-resident stream stays inline.
     int inline_w = -1;
-    for (int w = 0; w < nloc; ++w)
-      if (part[w] && (inline_w < 0 || !workers_[w]->gpu())) inline_w = w;
+    if (inline_largest_share && !all_gpu_) {
+      for (int w = 0; w < nloc; ++w)
+        if (part[w] && (inline_w < 0 || st.ranges[global_base_ + w] > st.ranges[global_base_ + inline_w] ||
+                        (st.ranges[global_base_ + w] == st.ranges[global_base_ + inline_w] && !workers_[w]->gpu())))
+          inline_w = w;
+    } else {
+      for (int w = 0; w < nloc; ++w)
+        if (part[w] && (inline_w < 0 || !workers_[w]->gpu())) inline_w = w;
+    }
     for (int w = 0; w < nloc; ++w) {
       if (!part[w] || w == inline_w) continue;
       int g = global_base_ + w;

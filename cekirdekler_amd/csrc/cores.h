@@ -363,7 +363,10 @@ class Cores {
   bool driver_downloads_own_stream = true;
   // driver pipeline: blob uploads on the main stream (one in-order chain of
   // copies, as the event pipeline's), each blob's queue waiting for its own
-  bool driver_reads_on_main_stream = false;
+  bool driver_reads_on_main_stream = true;
+  // a mixed CPU + GPU call runs the participant with the largest share on
+  // the calling thread (off: the CPU device, as before)
+  bool inline_largest_share = true;
   // GPU workers wait for their streams by sleeping on a blocking-sync event
   // (off by default; CEK_SLEEP_WAITS=1)
   bool sleep_waits = false;  // explicit blobs: partial arrays alternate over two upload streams (slower: 12.7 vs 7.1 ms for the shells, the extra stream shares a hardware queue)

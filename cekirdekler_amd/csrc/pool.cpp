@@ -45,13 +45,21 @@ void DevicePool::close() {
   threads_.clear();
 }
 
-void DevicePool::enqueue(std::vector<PoolTask> tasks) {
+void DevicePool::enqueue(std::vector<PoolTask> tasks, long long pool_total, bool append) {
   {
     std::lock_guard<std::mutex> g(mu_);
     if (closed_) throw Error("device pool is closed");
-    bool sync_next = false;
-    const int pid = static_cast<int>(pools_.size());
-    pools_.push_back(PoolProgress());
+    // append: the tasks continue the last enqueued pool (a pool handed over
+    // in chunks, so the consumers start on the first chunk while the caller
+    // prepares the next); pool_total pre-sizes a new pool's task count for
+    // the queue-depth policy
+    if (!append || pools_.empty()) {
+      pools_.push_back(PoolProgress());
+      if (pool_total > 0) pools_.back().preset = pool_total;
+      sync_carry_ = false;
+    }
+    bool sync_next = sync_carry_;
+    const int pid = static_cast<int>(pools_.size()) - 1;
     for (auto& task : tasks) {
       Item it;
       it.task = std::move(task);
@@ -90,6 +98,7 @@ void DevicePool::enqueue(std::vector<PoolTask> tasks) {
         ++pools_[pid].total;
       }
     }
+    sync_carry_ = sync_next;
   }
   work_cv_.notify_all();
 }
@@ -104,7 +113,7 @@ int DevicePool::least_loaded_locked() const {
 int DevicePool::limit_locked() {
   if (queue_.empty()) return max_in_flight_;
   const PoolProgress& p = pools_[queue_.front().pool];
-  const long long n = p.total, sub = p.taken, rem = n - sub;
+  const long long n = std::max(p.total, p.preset), sub = p.taken, rem = n - sub;
   long long q;
   if (rem < 3)
     q = 1;
@@ -267,8 +276,14 @@ void DevicePool::consumer(int dev) {
   const ComputeCall* call_tmpl = nullptr;      // the template `call` was copied from
   std::shared_ptr<const ComputeCall> call_keep;  // keeps that template alive
   double last_progress = now_ms();
+  bool issued = false;  // the previous iteration issued a task
   for (;;) {
-    if (!inflight.empty() && retire(dev, inflight) > 0) last_progress = now_ms();
+    // while tasks keep flowing, poll the markers only once a few are in
+    // flight: each poll is a HIP call that costs about as much as a launch
+    if (!inflight.empty() && !(issued && static_cast<int>(inflight.size()) < kPollBatch) &&
+        retire(dev, inflight) > 0)
+      last_progress = now_ms();
+    issued = false;
     Item it;
     bool got = false, idle = false, stop = false;
     {
@@ -331,6 +346,7 @@ void DevicePool::consumer(int dev) {
         cr.compute(call);
         auto m = cr.last_marker(0);
         inflight.push_back({t.id, notify, m.first, m.second, t0});
+        issued = true;
       } else {
         cr.compute(call);
         complete(dev, t.id, notify, now_ms() - t0, "");

@@ -69,6 +69,9 @@ enum PoolTaskFlags : uint32_t {
 // (it has a callback).  Other tasks retire natively without a record; their
 // device and time are kept in the pool's result table (results()).
 constexpr uint32_t kTaskNotify = 1u << 30;
+// a consumer issuing back to back polls its markers once this many tasks are
+// in flight (and whenever it cannot issue)
+constexpr int kPollBatch = 3;
 
 struct PoolTask {
   // the compute without its arrays, shared by every task of one shape (a
@@ -107,7 +110,7 @@ class DevicePool {
 
   // Appends one task pool (FIFO order kept); broadcast tasks are duplicated
   // per device, SYNC_LAST turns into SYNC_FIRST of the next task.
-  void enqueue(std::vector<PoolTask> tasks);
+  void enqueue(std::vector<PoolTask> tasks, long long pool_total = -1, bool append = false);
   // Blocks until every enqueued task has retired.
   void finish();
   // Completions of kTaskNotify tasks since the last call; waits up to
@@ -139,7 +142,9 @@ class DevicePool {
   };
   struct PoolProgress {
     long long total = 0, taken = 0;
+    long long preset = 0;  // the whole pool's size when it arrives in chunks
   };
+  bool sync_carry_ = false;  // a SYNC_LAST at the end of the last chunk
   int limit_locked();
   int least_loaded_locked() const;
   struct Inflight {

@@ -300,19 +300,29 @@ class ClDevicePool:
         cr0 = self.crunchers[0]
         ndev = len(self.crunchers)
         cache = self._templates
-        local = {}  # template key -> index into this batch's template list
-        templates = []
-        which, arrays, types = [], [], []
-        notify = []  # (id, [task, copies]) of tasks with a callback
-        expected = 0
         tasks = list(pool.tasks)
         pool.tasks.clear()
         with self._cv:
             first_id = self._next_id
             self._next_id += len(tasks)
+            self._live.append((first_id, tasks))
+        # handed over in chunks: the consumers start on the first chunk while
+        # this thread prepares the next (one pool for the queue-depth policy)
+        for c0 in range(0, max(1, len(tasks)), self.ENQUEUE_CHUNK):
+            self._enqueue_chunk(tasks, c0, min(len(tasks), c0 + self.ENQUEUE_CHUNK), first_id, cr0, ndev, cache)
+
+    ENQUEUE_CHUNK = 256
+
+    def _enqueue_chunk(self, tasks, c0, c1, first_id, cr0, ndev, cache) -> None:
+        local = {}  # template key -> index into this chunk's template list
+        templates = []
+        which, arrays, types = [], [], []
+        notify = []  # (id, [task, copies]) of tasks with a callback
+        expected = 0
         NO_COMPUTE, BROADCAST = int(ClTaskType.TASK_MESSAGE_NO_COMPUTE), int(ClTaskType.TASK_MESSAGE_BROADCAST)
         NOTIFY = int(cek.DevicePool.NOTIFY)
-        for k, t in enumerate(tasks):
+        for k in range(c0, c1):
+            t = tasks[k]
             ty = int(t.type)
             kn = t.kernels
             if t.group is not None and kn and not (ty & NO_COMPUTE and not kn):
@@ -352,9 +362,9 @@ class ClDevicePool:
         with self._cv:
             self._notify.update(notify)
             self._expected += expected
-            self._live.append((first_id, tasks))
-        if tasks:
-            self._native.enqueue_batch(templates, which, arrays, types, list(range(first_id, first_id + len(tasks))))
+        if c1 > c0:
+            self._native.enqueue_batch(templates, which, arrays, types, list(range(first_id + c0, first_id + c1)),
+                                       len(tasks), c0 > 0)
 
     enqueueTaskPool = enqueue_task_pool
 

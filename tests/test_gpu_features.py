@@ -935,3 +935,53 @@ def test_release_array_with_pending_download():
     np.testing.assert_array_equal(keep.array, np.arange(n, dtype=np.float32) + 2.0)
     np.testing.assert_array_equal(host, np.arange(n, dtype=np.float32) + 2.0)
     cr.dispose()
+
+
+@pytest.mark.gpu
+def test_cpu_device_inside_gpu_cpu_cruncher_keeps_its_speed():
+    """a CPU device that shares a cruncher with a GPU
+    runs its share as fast as a CPU-only cruncher with the same thread count
+    runs the same range (the mixed set reserves a host thread per GPU worker,
+    hardware.mixed_cpu_policy, so the two do not oversubscribe the host)."""
+    import statistics
+
+    import cekirdekler_amd as ck
+
+    src = r"""
+    __global__ void poly(const float* x, float* y) {
+        long long i = get_global_id(0);
+        float v = x[i], acc = 1.0f;
+        for (int k = 0; k < 96; ++k) acc = fmaf(acc, v, 0.25f);
+        y[i] = acc;
+    }"""
+    p = ck.ClPlatforms.all()
+    mixed = ck.ClNumberCruncher(p.gpus()[0] + p.cpus(True), src)
+    cpu_threads = mixed.cores.device(1).cpu_threads
+    n = 1 << 22
+    x = ck.ClArray(np.random.default_rng(0).uniform(0.1, 0.9, n).astype(np.float32))
+    y = ck.ClArray(np.zeros(n, np.float32))
+    x.write = False
+    y.read = False
+    for _ in range(25):  # the law converges
+        x.next_param(y).compute(mixed, 1, "poly", n, 256)
+    r_cpu = mixed.ranges(1)[1]
+    assert r_cpu >= 256 * 64, mixed.ranges(1)
+    alone = ck.ClNumberCruncher(p.cpus(True, max_cpu_cores=cpu_threads), src)
+    assert alone.cores.device(0).cpu_threads == cpu_threads
+    xs = ck.ClArray(x.array[:r_cpu].copy())
+    ys = ck.ClArray(np.zeros(r_cpu, np.float32))
+    xs.write = False
+    ys.read = False
+    m_ms, a_ms = [], []
+    for _ in range(12):  # interleaved: host-load drift hits both alike
+        x.next_param(y).compute(mixed, 1, "poly", n, 256)
+        rec = mixed.last_record()
+        if rec["ranges"][1] == r_cpu:
+            m_ms.append(rec["device_ms"][1])
+        xs.next_param(ys).compute(alone, 1, "poly", r_cpu, 256)
+        a_ms.append(alone.last_record()["device_ms"][0])
+    assert len(m_ms) >= 4, "the split kept moving"
+    mixed_ms, alone_ms = statistics.median(m_ms), statistics.median(a_ms)
+    assert mixed_ms <= 1.05 * alone_ms, (mixed_ms, alone_ms, cpu_threads, r_cpu)
+    mixed.dispose()
+    alone.dispose()
