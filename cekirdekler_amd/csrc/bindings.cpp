@@ -465,6 +465,7 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("driver_downloads_own_stream", &Cores::driver_downloads_own_stream)
       .def_readwrite("driver_reads_on_main_stream", &Cores::driver_reads_on_main_stream)
       .def_readwrite("inline_largest_share", &Cores::inline_largest_share)
+      .def_readwrite("attached_markers", &Cores::attached_markers)
       .def_readwrite("peer_read_min_bytes", &Cores::peer_read_min_bytes)
       .def_readwrite("graph_min_launches", &Cores::graph_min_launches)
       .def_readwrite("auto_failover", &Cores::auto_failover)

@@ -367,6 +367,9 @@ class Cores {
   // a mixed CPU + GPU call runs the participant with the largest share on
   // the calling thread (off: the CPU device, as before)
   bool inline_largest_share = true;
+  // fine-grained markers carried by the kernel launch when nothing follows
+  // it in the compute (CEK_ATTACHED_MARKERS=0: a separate event record)
+  bool attached_markers = true;
   // GPU workers wait for their streams by sleeping on a blocking-sync event
   // (off by default; CEK_SLEEP_WAITS=1)
   bool sleep_waits = false;  // explicit blobs: partial arrays alternate over two upload streams (slower: 12.7 vs 7.1 ms for the shells, the extra stream shares a hardware queue)
@@ -532,6 +535,7 @@ class Cores {
   std::vector<std::vector<PendingSpanEnd>> pending_span_end_;  // per local device
   std::vector<std::vector<hipEvent_t>> order_events_;          // per local device (flush ordering)
   bool defer_downloads(const Worker& wk) const;
+  bool attachable_marker(const ComputeCall& c) const;
   bool must_flush_before(const Worker& wk, hipStream_t s, const ComputeCall& c) const;
   void flush_downloads(Worker& wk, hipStream_t next = nullptr, const ComputeCall* c = nullptr);
   ComputeRecord last_record_;

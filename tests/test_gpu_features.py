@@ -985,3 +985,30 @@ def test_cpu_device_inside_gpu_cpu_cruncher_keeps_its_speed():
     assert mixed_ms <= 1.05 * alone_ms, (mixed_ms, alone_ms, cpu_threads, r_cpu)
     mixed.dispose()
     alone.dispose()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("attached", [True, False])
+def test_markers_attached_to_kernel_launch(gpu, attached):
+    """Fine-grained markers of device-resident computes ride on the kernel
+    launch (its completion event) instead of a separate event record: every
+    marker is reached, in order, and the result is that of every compute."""
+    c = ck.ClNumberCruncher(gpu[0], SRC)
+    c.cores.attached_markers = attached
+    n = 1 << 16
+    x = ck.ClArray(np.zeros(n, np.float32))
+    x.compute(c, 21, "inc", n, 256)  # up once
+    x.read = x.write = False
+    c.fine_grained_queue_control = True
+    c.enqueue_mode_async_enable = True
+    c.enqueue_mode = True
+    for _ in range(64):
+        x.compute(c, 21, "inc", n, 256)
+    issued = c.count_markers_remaining() + c.count_markers_reached()
+    c.enqueue_mode = False
+    c.enqueue_mode_async_enable = False
+    c.fine_grained_queue_control = False
+    assert c.count_markers_remaining() == 0 and c.count_markers_reached() >= 64, issued
+    c.download(x, 0)
+    np.testing.assert_array_equal(x.array, 65.0)
+    c.dispose()
