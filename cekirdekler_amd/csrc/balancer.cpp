@@ -135,7 +135,10 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
   };
   if (warm && active > 0 && wall_ms > 0 && by_law) {
     fs.law_settled = settled ? fs.law_settled + 1 : 0;
-    if (fs.law_settled >= 3) fs.law_wall = fs.law_wall < 0 ? wall_ms : 0.5 * fs.law_wall + 0.5 * wall_ms;
+    // the best settled law call: the guard compares against what the law
+    // has been seen to do (an average would keep the slow first settled
+    // calls — a host-resident stream's first calls are several times slower)
+    if (fs.law_settled >= 3) fs.law_wall = fs.law_wall < 0 ? wall_ms : std::min(fs.law_wall, wall_ms);
     if (active >= 2) {
       const double ov = std::max(0.0, wall_ms - tmax);
       fs.o_multi = fs.o_multi < 0 ? ov : 0.7 * fs.o_multi + 0.3 * ov;
@@ -242,7 +245,7 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
   // (a probe still runs to completion: it is the measurement)
   if (fs.probe_left == 0) {
     const double cand = single ? fs.single_wall[best] : fs.multi_wall;
-    if (fs.law_wall < 0 || (cand > 0 && cand >= fs.law_wall)) return to_law();
+    if (fs.law_wall < 0 || (cand > 0 && cand >= kGuardMargin * fs.law_wall)) return to_law();
   }
   std::vector<double> target(n, 0.0);
   if (single) {

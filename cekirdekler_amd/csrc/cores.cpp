@@ -1938,11 +1938,8 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
     // CPU device is preferred there — its work is the calling thread plus
     // the CPU pool either way, and the GPU workers are posted first so
     // their launches go out while the CPU computes.
-    // With CPU + GPU, the participant holding the
-    // largest share runs here: a GPU that takes 99 % of a wave frame keeps
-    // the GPU-alone path (launch and wait on this thread) and the CPU's
-    // sliver goes to its worker, whose hand-off hides behind the GPU's
-    // frame; a CPU holding most of a host-resident stream stays inline.
+    // Option (inline_largest_share): the participant holding the largest
+    // share runs here instead (measured slower on the wave frame, off).
     int inline_w = -1;
     if (inline_largest_share && !all_gpu_) {
       for (int w = 0; w < nloc; ++w)

@@ -37,7 +37,7 @@
 
 namespace {
 
-template <int WM, int WN, int FM, int FN, int MODE, bool SK = false, int XCH = 0, bool ROWC = false, bool XS = false>
+template <int WM, int WN, int FM, int FN, int MODE, bool SK = false, int XCH = 0, bool ROWC = false>
 __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
                                           const uint16_t* __restrict__ A,
                                           const uint16_t* __restrict__ Bt, float* __restrict__ C,
@@ -66,23 +66,8 @@ __device__ __forceinline__ void gemm_tile(const int* __restrict__ dims,
   // Split-K (SK): work-group u computes K-tiles [ks, ks + nk) of tile u / S;
   // the S work-groups of a tile are consecutive ids, so the XCD remap keeps
   // them on one XCD and the load balancer (granularity S·local) on one device.
+  const long long u = (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
   const int S = SK ? max(dims[4], 1) : 1;
-  // XS (two-way split-K with a hand-over, XCH >= 3): the launch's first
-  // half of work-groups (XCDs 0-3 after the remap) are the owners of its
-  // tiles, the second half (XCDs 4-7) the helpers, so an XCD's 32
-  // work-groups are 32 different tiles on the same K half — the K-slices
-  // they share through the XCD's L2 are those of a 4 × 8 tile block, as in
-  // the unsplit full problem, instead of 16 tiles × both halves.  The pair
-  // (2t, 2t+1) and a device's contiguous tile range are unchanged; the
-  // hand-over crosses XCDs (the partial goes through memory, fenced).
-  const long long u = [&]() -> long long {
-    if constexpr (XS) {
-      const long long v = cek_xcd_remap(blockIdx.x, gridDim.x), ntl = gridDim.x / 2;
-      return 2 * (off / NT / 2 + v % ntl) + v / ntl;
-    } else {
-      return (long long)cek_xcd_remap(blockIdx.x, gridDim.x) + off / NT;
-    }
-  }();
   const long long t = u / S;
   // XCH 3: the K-split of u odd (the helper) takes K/64/2 − dims[5] K-tiles
   // from the start, u even (the owner) the rest
@@ -792,14 +777,6 @@ extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sw(
     const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
   __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
   gemm_tile<2, 4, 8, 4, 4, true, 3>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
-}
-
-// the same with owners and helpers on different XCDs (XS): each XCD's
-// work-groups multiply one K half of 32 distinct tiles
-extern "C" __global__ __launch_bounds__(512) void cek_sgemm_bf16_256x256pb_sx(
-    const int* dims, const uint16_t* A, const uint16_t* Bt, float* C, float* W, int* tile_cnt, CEK_HIDDEN) {
-  __shared__ __attribute__((aligned(16))) char smem[(2 * 256 + 3 * 256) * 64 * 2];
-  gemm_tile<2, 4, 8, 4, 4, true, 3, false, true>(dims, A, Bt, C, smem, __cek_off, W, tile_cnt);
 }
 
 // the same with the row halves exchanged at the end (XCH 4): the owner's

@@ -38,10 +38,6 @@ TILES = {
     # hand-over is co-residency-safe: an owner whose helper is late claims
     # the hand-over and multiplies the helper's K-range itself.
     "256x256pbw": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sw"),
-    # the same with the owners on XCDs 0-3 and the helpers on XCDs 4-7: an
-    # XCD's work-groups share the K-slices of 32 distinct tiles (the hand-over
-    # crosses XCDs)
-    "256x256pbx": (256, 256, 512, "cek_sgemm_bf16_256x256pb_sx"),
     # the same, row halves exchanged at the end: the helper hands over its
     # partial of the owner's half, the owner hands back its partial of the
     # helper's half, each stores one half of C (384 KiB of tail traffic on
@@ -68,7 +64,7 @@ GEMM_LIBS = ("sgemm_bf16",)
 # each): the kernels store a C tile in fragment order (one dwordx4 per lane
 # per fragment), which tile_to_rows / rows_to_tile convert.
 TILE_WAVES = {
-    "256x256pb": (2, 4, 8, 4), "256x256pbr": (2, 4, 8, 4), "256x256pbw": (2, 4, 8, 4), "256x256pbx": (2, 4, 8, 4), "256x256pbh": (2, 4, 8, 4), "256x256pbs": (2, 4, 8, 4), "256x256": (2, 4, 8, 4), "256x256pp": (2, 4, 8, 4),
+    "256x256pb": (2, 4, 8, 4), "256x256pbr": (2, 4, 8, 4), "256x256pbw": (2, 4, 8, 4), "256x256pbh": (2, 4, 8, 4), "256x256pbs": (2, 4, 8, 4), "256x256": (2, 4, 8, 4), "256x256pp": (2, 4, 8, 4),
     "256x128pe": (4, 2, 4, 4), "256x128pb": (4, 2, 4, 4), "128x128": (2, 2, 4, 4),
 }
 
@@ -135,10 +131,10 @@ ROW_MAJOR_TILES = {"256x256pbr"}
 # tiles with a split-K kernel variant ("<kernel>_sk", arrays + W + counters)
 SPLIT_K_TILES = {"256x256pp", "256x256pb"}
 # tiles whose kernel always runs two K-splits with a hand-over (flag words per tile)
-EXCHANGE_TILES = {"256x256pbw": 4, "256x256pbx": 4, "256x256pbh": 4, "256x256pbs": 4}
+EXCHANGE_TILES = {"256x256pbw": 4, "256x256pbh": 4, "256x256pbs": 4}
 # K-tile deficit of the helper split (dims[5]): it hands its whole partial
 # over and leaves while the owner still multiplies
-EXCHANGE_SHIFT = {"256x256pbw": 4, "256x256pbx": 4, "256x256pbh": 4, "256x256pbs": 0}
+EXCHANGE_SHIFT = {"256x256pbw": 4, "256x256pbh": 4, "256x256pbs": 0}
 
 
 def to_bf16_bits(x: np.ndarray) -> np.ndarray:

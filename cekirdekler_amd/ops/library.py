@@ -20,8 +20,7 @@ LIBRARY = {
                    "cek_sgemm_bf16_256x256pbr",
                    "cek_sgemm_bf16_256x128pb", "cek_sgemm_bf16_256x128pe", "cek_sgemm_bf16_128x128",
                    "cek_sgemm_bf16_256x256pp_sk", "cek_sgemm_bf16_256x256pb_sk",
-                   "cek_sgemm_bf16_256x256pb_sw", "cek_sgemm_bf16_256x256pb_sx", "cek_sgemm_bf16_256x256pb_sh",
-                   "cek_sgemm_bf16_256x256pb_ss"],
+                   "cek_sgemm_bf16_256x256pb_sw", "cek_sgemm_bf16_256x256pb_sh", "cek_sgemm_bf16_256x256pb_ss"],
     "sgemm_f32": ["cek_sgemm_f32_128x128", "cek_sgemm_f32_256x128", "cek_sgemm_f32_256x256",
                   "cek_sgemm_f32_256x256ir", "cek_sgemm_f32_256x256ib7", "cek_sgemm_f32_256x128ie",
                   "cek_sgemm_f32_256x256w", "cek_sgemm_f32_256x256g", "cek_sgemm_f32_256x256gt", "cek_sgemm_f32_256x256gh",
@@ -42,7 +41,7 @@ LIBRARY = {
 # "name:arity" so a compute() whose array list does not match the kernel's
 # signature is rejected on the host instead of faulting on the device.
 ARITY = {
-    **{k: (6 if k.endswith(("_sk", "_sw", "_sx", "_sh", "_ss")) else 4) for k in LIBRARY["sgemm_bf16"]},
+    **{k: (6 if k.endswith(("_sk", "_sw", "_sh", "_ss")) else 4) for k in LIBRARY["sgemm_bf16"]},
     **{k: 4 for k in LIBRARY["sgemm_f32"]},
     **{k: 3 for k in LIBRARY["mandelbrot"]},
     **{k: 4 for k in LIBRARY["nbody"] if "energy" not in k},
