@@ -528,6 +528,44 @@ def _mandelbrot_kernel_only(kernel: str = "blk8y", reps: int = 40) -> dict:
     return out
 
 
+def bench_sgemm_slices(steps: int, rows=(4096, 2048, 1024), size: int = 8192) -> dict:
+    """The per-GPU share of the strongly scaled headline, measured on this
+    GPU: at N = 2 / 4 / 8 GPUs a rank computes 4096 /
+    2048 / 1024 rows of the 8192³ GEMM.  Each slice runs as bench_sgemm
+    times it (one GEMM in flight, enqueue mode, the tile bench_sgemm picks
+    at that N) and its whole output is checked against a float64 product."""
+    import torch
+
+    from cekirdekler_amd.ops.gemm import GEMM_LIBS, GemmBf16
+    from cekirdekler_amd.ops.library import library
+    import cekirdekler_amd as ck
+
+    gpu = ck.ClPlatforms.all().gpus()[0]
+    out = {}
+    for m in rows:
+        tile = "256x256pb" if (m // 256) * (size // 256) >= 256 else "256x256pbw"
+        cr = ck.ClNumberCruncher(gpu, "", prebuilt=library(*GEMM_LIBS))
+        g = GemmBf16(m, size, size, cruncher=cr, tile=tile)
+        for _ in range(3):
+            g.run(compute_id=1, resident=True)
+        torch.cuda.synchronize()
+        cr.enqueue_mode = True
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.run(compute_id=1, resident=True)
+        cr.enqueue_mode = False
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3 / steps
+        err, tiles = g.verify_full(compute_id=1)
+        out[str(m)] = {"tflops": round(g.flops / ms / 1e9, 1), "ms": round(ms, 4), "tile": tile,
+                       "max_rel_err": err, "tiles_checked": tiles, "tiles_total": g.tiles,
+                       "handover_fallbacks": g.handover_fallbacks()}
+        cr.dispose()
+        for a in (g.A, g.B, g.C, g.dims, *g.extra):
+            a.dispose()
+    return out
+
+
 def bench_lb_iters():
     """Computes until device 0's share stays within 5% of its steady state
     (the median of the last 10 of 40 calls), on two logical devices of this
@@ -781,6 +819,16 @@ def compact_extra(full: dict, detail: str) -> dict:
         ex["mandelbrot_4k"] = m
     else:
         ex["mandelbrot_4k"] = None
+    sl = full.get("sgemm_slices") or {}
+    if isinstance(sl, dict) and sl:
+        if "error" in sl:
+            ex["sgemm_slices"] = _pick(sl, [])
+        else:  # TF/s per slice (rows), the worst error over all of them
+            ex["sgemm_slices"] = {k: v.get("tflops") for k, v in sl.items() if isinstance(v, dict)}
+            ex["sgemm_slices"]["max_rel_err"] = _r(max((v.get("max_rel_err", 0) for v in sl.values()
+                                                        if isinstance(v, dict)), default=None), 9)
+            ex["sgemm_slices"]["all_tiles_checked"] = all(v.get("tiles_checked") == v.get("tiles_total")
+                                                          for v in sl.values() if isinstance(v, dict))
     sg = full.get("sgemm") or {}
     rc = full.get("sgemm_row_major_c") or {}
     all_ranges = full.get("sgemm_ranges_all_ranks") or [sg.get("ranges")]
@@ -877,6 +925,12 @@ def main(argv=None) -> int:
         dist.barrier()
         dist.destroy_process_group()  # the other ranks exit here; rank 0 goes on alone
     lb = bench_lb_iters() if (ctx.rank == 0 and use_gpu) else {}
+    slices = {}
+    if ctx.rank == 0 and use_gpu and args.size == 8192:
+        try:  # an extra: a failure is reported in its field
+            slices = bench_sgemm_slices(args.steps)
+        except Exception as e:  # pragma: no cover
+            slices = {"error": repr(e)[:300]}
     node = {} if (ctx.rank != 0 or args.skip_node_configs or not use_gpu) else bench_node_configs(ctx.world)
     peers = _peer_topology(ctx.world) if (ctx.rank == 0 and use_gpu) else {}
     ok = sg["max_rel_err"] <= MAX_REL_ERR
@@ -884,7 +938,8 @@ def main(argv=None) -> int:
         size = args.size if use_gpu else min(args.size, 512)
         full = {
             "sgemm": sg, "sgemm_ranges_all_ranks": all_ranges,
-            "sgemm_row_major_c": rowc, "mandelbrot_4k": mb, "load_balance_iters": lb, **node,
+            "sgemm_row_major_c": rowc, "sgemm_slices": slices, "mandelbrot_4k": mb, "load_balance_iters": lb,
+            **node,
             "peer_topology": peers,
         }
         detail = write_detail(full, ctx.world, args.detail, gpu=use_gpu)

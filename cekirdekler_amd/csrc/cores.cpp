@@ -53,6 +53,7 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
   if (const char* e = std::getenv("CEK_DEFER_DOWNLOADS")) deferred_downloads = std::string(e) != "0";
   if (const char* e = std::getenv("CEK_INLINE_LARGEST")) inline_largest_share = std::string(e) != "0";
   if (const char* e = std::getenv("CEK_ATTACHED_MARKERS")) attached_markers = std::string(e) != "0";
+  if (const char* e = std::getenv("CEK_ADAPTIVE_SLEEP")) adaptive_sleep_waits = std::string(e) != "0";
   if (const char* e = std::getenv("CEK_KERNEL_D2H")) set_kernel_d2h(std::string(e) != "0");
   if (const char* e = std::getenv("CEK_ZC_RELEASE")) zc_release = std::string(e) != "0";
   // CEK_SLEEP_WAITS=1: GPU workers wait for their streams by sleeping on a
@@ -1344,7 +1345,7 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
       }
       CEK_HIP(hipEventRecord(ds->gap_a, s));
     }
-    if (wk.gpu()) wk.wait_stream(s, sleep_waits);
+    if (wk.gpu()) wk.wait_stream(s, sleep_waits || sleep_this_call_);
     t_phase_arrived = true;
     const double w0 = now_ms();
     phase_->arrive_and_wait();
@@ -1391,7 +1392,7 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
   }
   if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(s);
   if (fine_grained && !(attach && wk.take_attached_marker(s))) wk.add_marker(s, marker_needs_release(c));
-  if (!enqueue_mode_ && wk.gpu()) wk.wait_stream(s, sleep_waits);
+  if (!enqueue_mode_ && wk.gpu()) wk.wait_stream(s, sleep_waits || sleep_this_call_);
 }
 
 // The compute's last command on its stream is its one kernel launch: no
@@ -1557,7 +1558,7 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
   span_end(wk, m);
   if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(m);
   if (fine_grained) wk.add_marker(m, marker_needs_release(c));
-  if (wk.gpu()) wk.wait_stream(m, sleep_waits);
+  if (wk.gpu()) wk.wait_stream(m, sleep_waits || sleep_this_call_);
 }
 
 void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long long ref,
@@ -1672,7 +1673,7 @@ void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long
   span_end(wk, m);
   if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(m);
   if (fine_grained) wk.add_marker(m, marker_needs_release(c));
-  if (wk.gpu()) wk.wait_stream(m, sleep_waits);
+  if (wk.gpu()) wk.wait_stream(m, sleep_waits || sleep_this_call_);
 }
 
 void Cores::run_device(int w, const ComputeCall& c, long long ref, long long range, bool pipelined,
@@ -1893,6 +1894,15 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
   }
   if (collective(c)) pipelined = false;
 
+  // A GPU that shares the call with a CPU device sleeps on its stream when
+  // its last time for this compute id was long: a spinning wait would take
+  // a core (an SMT sibling) from the CPU device's threads for milliseconds.
+  // Short GPU waits (a 0.03 ms wave frame) keep spinning, where a wake-up
+  // would cost more than the core.
+  sleep_this_call_ = false;
+  if (!all_gpu_ && adaptive_sleep_waits)
+    for (int w = 0; w < nloc; ++w)
+      if (workers_[w]->gpu() && st.bench[global_base_ + w] > sleep_wait_min_ms) sleep_this_call_ = true;
   std::vector<double> ms(nloc, 0.0);
   std::vector<uint64_t> h2d(nloc, 0), d2h(nloc, 0);
   // xGMI fan-out of full reads, enqueued before the per-device work (its

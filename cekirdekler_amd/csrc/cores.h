@@ -372,6 +372,10 @@ class Cores {
   // fine-grained markers carried by the kernel launch when nothing follows
   // it in the compute (CEK_ATTACHED_MARKERS=0: a separate event record)
   bool attached_markers = true;
+  // CPU + GPU sets: GPU workers sleep-wait in calls whose previous GPU time
+  // for the compute id exceeded sleep_wait_min_ms (CEK_ADAPTIVE_SLEEP=0: off)
+  bool adaptive_sleep_waits = true;
+  double sleep_wait_min_ms = 0.25;
   // GPU workers wait for their streams by sleeping on a blocking-sync event
   // (off by default; CEK_SLEEP_WAITS=1)
   bool sleep_waits = false;  // explicit blobs: partial arrays alternate over two upload streams (slower: 12.7 vs 7.1 ms for the shells, the extra stream shares a hardware queue)
@@ -465,6 +469,7 @@ class Cores {
   double build_ms_ = 0;
   bool enqueue_mode_ = false;
   bool capturing_ = false;
+  bool sleep_this_call_ = false;  // compute_once: GPU waits of this call sleep
   std::vector<void*> shell_dims_;         // gemm_host_shells: per-kernel dims, per worker
   std::vector<size_t> shell_dims_cap_;
   std::vector<std::vector<int>> shell_dims_host_;  // what shell_dims_ holds (re-uploaded only on change)
