@@ -465,7 +465,6 @@ PYBIND11_MODULE(_cek, m) {
       .def_readwrite("driver_downloads_own_stream", &Cores::driver_downloads_own_stream)
       .def_readwrite("driver_reads_on_main_stream", &Cores::driver_reads_on_main_stream)
       .def_readwrite("inline_largest_share", &Cores::inline_largest_share)
-      .def_readwrite("attached_markers", &Cores::attached_markers)
       .def_readwrite("adaptive_sleep_waits", &Cores::adaptive_sleep_waits)
       .def_readwrite("sleep_wait_min_ms", &Cores::sleep_wait_min_ms)
       .def_readwrite("peer_read_min_bytes", &Cores::peer_read_min_bytes)

@@ -52,7 +52,6 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
   if (const char* e = std::getenv("CEK_SINGLE_DEVICE_SPANS")) single_device_spans = std::string(e) == "1";
   if (const char* e = std::getenv("CEK_DEFER_DOWNLOADS")) deferred_downloads = std::string(e) != "0";
   if (const char* e = std::getenv("CEK_INLINE_LARGEST")) inline_largest_share = std::string(e) != "0";
-  if (const char* e = std::getenv("CEK_ATTACHED_MARKERS")) attached_markers = std::string(e) != "0";
   if (const char* e = std::getenv("CEK_ADAPTIVE_SLEEP")) adaptive_sleep_waits = std::string(e) != "0";
   if (const char* e = std::getenv("CEK_KERNEL_D2H")) set_kernel_d2h(std::string(e) != "0");
   if (const char* e = std::getenv("CEK_ZC_RELEASE")) zc_release = std::string(e) != "0";
@@ -1307,11 +1306,7 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
   // the earlier computes' downloads go into the copy queues after this
   // compute's uploads
   if (defer) flush_downloads(wk);
-  // phase 2: kernels.  A fine-grained marker rides on the one kernel launch
-  // when nothing else follows it in this compute (device-resident task-pool
-  // tasks): one HIP command per task fewer
-  const bool attach = fine_grained && attached_markers && wk.gpu() && attachable_marker(c);
-  if (attach) wk.arm_attached_marker();
+  // phase 2: kernels
   launch_kernels(wk, s, c, ref, range);
   if (call_gathers_ && wk.gpu()) {  // in-process gather: this device's kernels are enqueued
     const int w = worker_index(wk);
@@ -1391,20 +1386,8 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
     span_end(wk, s);
   }
   if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(s);
-  if (fine_grained && !(attach && wk.take_attached_marker(s))) wk.add_marker(s, marker_needs_release(c));
+  if (fine_grained) wk.add_marker(s, marker_needs_release(c));
   if (!enqueue_mode_ && wk.gpu()) wk.wait_stream(s, sleep_waits || sleep_this_call_);
-}
-
-// The compute's last command on its stream is its one kernel launch: no
-// downloads, gathers, phase barrier, span or release event after it, and a
-// marker that needs no system-scope release.
-bool Cores::attachable_marker(const ComputeCall& c) const {
-  if (c.kernels.size() != 1 || c.repeats > 1 || !c.repeat_kernel.empty() || no_compute || record_timeline ||
-      call_gathers_ || phase_ || comm_ || capturing_ || spans_on() || marker_needs_release(c))
-    return false;
-  for (const auto& a : c.arrays)
-    if ((a.write && !a.zc) || a.gather) return false;
-  return !(zc_release && !enqueue_mode_ && writes_host_memory(c));
 }
 
 void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long long ref,

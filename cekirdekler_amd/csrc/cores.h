@@ -369,9 +369,6 @@ class Cores {
   // wave frame: the GPU inline left the CPU a 1 % share and 0.044 ms per
   // frame, the CPU inline an 11 % share and 0.033 ms (GPU alone 0.030)
   bool inline_largest_share = false;
-  // fine-grained markers carried by the kernel launch when nothing follows
-  // it in the compute (CEK_ATTACHED_MARKERS=0: a separate event record)
-  bool attached_markers = true;
   // CPU + GPU sets: GPU workers sleep-wait in calls whose previous GPU time
   // for the compute id exceeded sleep_wait_min_ms (CEK_ADAPTIVE_SLEEP=0: off)
   bool adaptive_sleep_waits = true;
@@ -542,7 +539,6 @@ class Cores {
   std::vector<std::vector<PendingSpanEnd>> pending_span_end_;  // per local device
   std::vector<std::vector<hipEvent_t>> order_events_;          // per local device (flush ordering)
   bool defer_downloads(const Worker& wk) const;
-  bool attachable_marker(const ComputeCall& c) const;
   bool must_flush_before(const Worker& wk, hipStream_t s, const ComputeCall& c) const;
   void flush_downloads(Worker& wk, hipStream_t next = nullptr, const ComputeCall* c = nullptr);
   ComputeRecord last_record_;

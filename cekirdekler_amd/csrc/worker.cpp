@@ -620,23 +620,7 @@ void Worker::launch(hipStream_t s, const std::string& kernel, const std::vector<
       CEK_HIP(hipMemsetAsync(q, 0, 8 * sizeof(int), s));
     }
     unsigned grid = static_cast<unsigned>(count / local);
-    if (attach_armed_ && !dyn && !kernel_times_on.load(std::memory_order_relaxed)) {
-      attach_armed_ = false;
-      hipEvent_t e = nullptr;
-      {
-        std::lock_guard<std::mutex> g(marker_mu_);
-        auto& spare = rings_[stream_slot(s)].spare;
-        if (!spare.empty()) {
-          e = spare.front();
-          spare.pop_front();
-        }
-      }
-      if (!e) CEK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
-      CEK_HIP(hipExtModuleLaunchKernel(f, grid * static_cast<unsigned>(local), 1, 1, static_cast<unsigned>(local),
-                                       1, 1, dyn_lds_, s, params.data(), nullptr, nullptr, e, 0));
-      attached_ev_ = e;
-      attached_s_ = s;
-    } else if (kernel_times_on.load(std::memory_order_relaxed)) {
+    if (kernel_times_on.load(std::memory_order_relaxed)) {
       hipEvent_t a = kstamp_event(), b = kstamp_event();
       CEK_HIP(hipExtModuleLaunchKernel(f, grid * static_cast<unsigned>(local), 1, 1, static_cast<unsigned>(local),
                                        1, 1, dyn_lds_, s, params.data(), nullptr, a, b, 0));
@@ -821,27 +805,6 @@ void Worker::add_marker(hipStream_t s, bool release) {
   }
   CEK_HIP(hipEventRecord(e, s));
   r.pending.emplace_back(e, release);
-}
-
-bool Worker::take_attached_marker(hipStream_t s) {
-  attach_armed_ = false;
-  hipEvent_t e = attached_ev_;
-  attached_ev_ = nullptr;
-  if (!e || attached_s_ != s || !gpu() || write_value_markers_) {
-    if (e) {  // not used as a marker: a spare again (re-using an event re-arms it)
-      std::lock_guard<std::mutex> g(marker_mu_);
-      rings_[stream_slot(attached_s_)].spare.push_back(e);
-    }
-    return false;
-  }
-  ++markers_issued_;
-  const int slot = stream_slot(s);
-  const uint64_t v = ++marker_issued_per_slot_[slot];
-  last_slot_ = slot;
-  last_value_ = v;
-  std::lock_guard<std::mutex> g(marker_mu_);
-  rings_[slot].pending.emplace_back(e, false);
-  return true;
 }
 
 uint64_t Worker::marker_word(int slot) {

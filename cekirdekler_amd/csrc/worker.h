@@ -179,16 +179,6 @@ class Worker {
   // release: the marker also makes earlier writes to HOST memory visible
   // (a system-scope release; set when the compute downloaded results)
   void add_marker(hipStream_t s, bool release = false);
-  // A fine-grained marker carried by the next kernel launch itself — the
-  // launch's completion event (hipExtModuleLaunchKernel's stop event)
-  // instead of a separate event record after it: one command per task
-  // fewer.  take_attached_marker() books it like add_marker(); false when no
-  // launch carried one (then add_marker as usual).
-  void arm_attached_marker() {
-    attach_armed_ = true;
-    attached_ev_ = nullptr;
-  }
-  bool take_attached_marker(hipStream_t s);
   long long markers_reached();
   // (slot, value) of the newest marker; a marker is reached once
   // marker_word(slot) >= value.  CPU device: slot -1 (always reached).
@@ -280,9 +270,6 @@ class Worker {
     std::string kernel;
     hipEvent_t start, stop;
   };
-  bool attach_armed_ = false;      // the next launch carries the marker (arm_attached_marker)
-  hipEvent_t attached_ev_ = nullptr;
-  hipStream_t attached_s_ = nullptr;
   // CPU device: measured ns per work item per kernel (one thread), and the
   // shortest task worth handing to a pool thread
   std::unordered_map<std::string, double> cpu_item_ns_;

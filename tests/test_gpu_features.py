@@ -988,13 +988,14 @@ def test_cpu_device_inside_gpu_cpu_cruncher_keeps_its_speed():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("attached", [True, False])
-def test_markers_attached_to_kernel_launch(gpu, attached):
-    """Fine-grained markers of device-resident computes ride on the kernel
-    launch (its completion event) instead of a separate event record: every
-    marker is reached, in order, and the result is that of every compute."""
+def test_device_resident_async_markers_all_reached(gpu):
+    """Fine-grained markers of device-resident computes on the async queues
+    (the device pool's task shape): every marker is reached once the mode is
+    left, and the array holds every compute's result.  (Markers attached to
+    the kernel launch as its hipExtModuleLaunchKernel stop event failed this
+    check — the last kernel was still running when its marker fired — and
+    were dropped.)"""
     c = ck.ClNumberCruncher(gpu[0], SRC)
-    c.cores.attached_markers = attached
     n = 1 << 16
     x = ck.ClArray(np.zeros(n, np.float32))
     x.compute(c, 21, "inc", n, 256)  # up once
@@ -1004,11 +1005,10 @@ def test_markers_attached_to_kernel_launch(gpu, attached):
     c.enqueue_mode = True
     for _ in range(64):
         x.compute(c, 21, "inc", n, 256)
-    issued = c.count_markers_remaining() + c.count_markers_reached()
     c.enqueue_mode = False
     c.enqueue_mode_async_enable = False
     c.fine_grained_queue_control = False
-    assert c.count_markers_remaining() == 0 and c.count_markers_reached() >= 64, issued
+    assert c.count_markers_remaining() == 0 and c.count_markers_reached() >= 64
     c.download(x, 0)
     np.testing.assert_array_equal(x.array, 65.0)
     c.dispose()
