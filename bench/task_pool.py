@@ -345,6 +345,9 @@ def dispatch_one_device(dev, tasks=4096):
     return rate
 
 
+# one consumer with its GPU to itself, measured before the pools below
+# create their (CU-masked) streams in this process
+one_dev_rate = dispatch_one_device(g[0])
 ntasks, makespan, counts, dispatch, concurrent = run_policy(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, spans=True)
 ideal = sum(single) / (len(devs) if partitioned else max(1, ng))
 
@@ -376,7 +379,6 @@ _, makespan_rr, counts_rr, dispatch_rr, _ = run_policy(ClDevicePoolType.DEVICE_R
 # task with its GPU to itself, hidden behind the device while the pool keeps
 # two or more tasks in flight — and, as an upper bound, device time + h
 # (no overlap at all); ideal = Σ whole-GPU times / 8.
-one_dev_rate = dispatch_one_device(g[0])
 h_ms = 1e3 / one_dev_rate
 proj_ideal = sum(single_whole) / 8
 proj = greedy_fifo_ms([max(t, h_ms) for t in single_whole], 8, len(work) // 2)
@@ -385,7 +387,8 @@ projection = {"devices": 8, "basis": "whole-GPU alone device times, FIFO greedy 
               "host_us_per_task_one_consumer": round(1e3 * h_ms, 2), "dispatch_tasks_per_s_one_device": round(one_dev_rate),
               "ideal_ms": proj_ideal, "makespan_ms": proj, "makespan_over_ideal": proj / proj_ideal,
               "makespan_serial_host_ms": proj_serial, "makespan_serial_host_over_ideal": proj_serial / proj_ideal,
-              "median_task_whole_gpu_us": round(1e3 * float(np.median(single_whole)), 2)}
+              "median_task_whole_gpu_us": round(1e3 * float(np.median(single_whole)), 2),
+              "task_whole_gpu_ms": [round(t, 5) for t in single_whole]}
 
 # checks: serial group order (x ← 2x + 1, eight times from 0 = 255), one GEMM, one reduction
 serial_ok = bool(np.all(serial_x.array == 255.0))

@@ -629,6 +629,8 @@ PYBIND11_MODULE(_cek, m) {
       .def("queue_limit_history", &DevicePool::queue_limit_history)
       .def("marker_speeds", &DevicePool::marker_speeds)
       .def("device_in_flight", &DevicePool::device_in_flight)
+      .def("host_profile", &DevicePool::host_profile,
+           "[issue ms, marker-poll ms, tasks issued, polls] summed over the consumer threads")
       .def_property_readonly("num_devices", &DevicePool::num_devices)
       .def_property_readonly("max_in_flight", &DevicePool::max_in_flight)
       .def("close", &DevicePool::close, py::call_guard<py::gil_scoped_release>());

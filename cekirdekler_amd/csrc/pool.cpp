@@ -6,6 +6,17 @@
 
 namespace cek {
 
+static void add_ms(std::atomic<double>& a, double v) {
+  double cur = a.load(std::memory_order_relaxed);
+  while (!a.compare_exchange_weak(cur, cur + v, std::memory_order_relaxed)) {
+  }
+}
+
+std::vector<double> DevicePool::host_profile() {
+  return {prof_issue_ms_.load(), prof_retire_ms_.load(), static_cast<double>(prof_tasks_.load()),
+          static_cast<double>(prof_polls_.load())};
+}
+
 DevicePool::DevicePool(std::vector<std::shared_ptr<Cores>> devices, int max_in_flight, int policy)
     : devs_(std::move(devices)), max_in_flight_(std::max(1, std::min(16, max_in_flight))), policy_(policy) {
   if (devs_.empty()) throw Error("device pool needs at least one device");
@@ -280,9 +291,14 @@ void DevicePool::consumer(int dev) {
   for (;;) {
     // while tasks keep flowing, poll the markers only once a few are in
     // flight: each poll is a HIP call that costs about as much as a launch
-    if (!inflight.empty() && !(issued && static_cast<int>(inflight.size()) < kPollBatch) &&
-        retire(dev, inflight) > 0)
-      last_progress = now_ms();
+    if (!inflight.empty() && !(issued && static_cast<int>(inflight.size()) < kPollBatch)) {
+      const double r0 = now_ms();
+      const int done = retire(dev, inflight);
+      const double r1 = now_ms();
+      add_ms(prof_retire_ms_, r1 - r0);
+      prof_polls_.fetch_add(1, std::memory_order_relaxed);
+      if (done > 0) last_progress = r1;
+    }
     issued = false;
     Item it;
     bool got = false, idle = false, stop = false;
@@ -343,7 +359,10 @@ void DevicePool::consumer(int dev) {
       if (async) {
         if (!cr.enqueue_mode()) cr.set_enqueue_mode(true);
         cr.async_enqueue = !it.serial;  // serial groups stay on one in-order stream
+        const double i0 = now_ms();
         cr.compute(call);
+        add_ms(prof_issue_ms_, now_ms() - i0);
+        prof_tasks_.fetch_add(1, std::memory_order_relaxed);
         auto m = cr.last_marker(0);
         inflight.push_back({t.id, notify, m.first, m.second, t0});
         issued = true;

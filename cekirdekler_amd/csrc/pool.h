@@ -44,6 +44,7 @@
 // device k mod D in strict rotation (a select/serial group as a whole takes
 // one rotation slot; barriers stay untargeted so every device stops at them).
 #pragma once
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <memory>
@@ -129,6 +130,9 @@ class DevicePool {
   std::vector<int> queue_limit_history();
   std::vector<double> marker_speeds();  // smoothed markers per ms, per device
   std::vector<int> device_in_flight();
+  // consumer host time by part, summed over devices (ms): issuing computes,
+  // polling markers, everything else (queue lock, bookkeeping, idle waits)
+  std::vector<double> host_profile();
   int num_devices() const { return static_cast<int>(devs_.size()); }
   int max_in_flight() const { return max_in_flight_; }
   void close();  // drain, stop and join the consumer threads
@@ -191,6 +195,8 @@ class DevicePool {
   };
   std::vector<Speed> speed_;
   std::vector<std::thread> threads_;
+  std::atomic<double> prof_issue_ms_{0}, prof_retire_ms_{0};
+  std::atomic<long long> prof_tasks_{0}, prof_polls_{0};
 };
 
 }  // namespace cek
