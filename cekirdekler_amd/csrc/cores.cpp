@@ -1778,10 +1778,10 @@ void Cores::compute_once(const ComputeCall& c, DeviceFailure* failed) {
   {
     const int nargs = static_cast<int>(c.arrays.size());
     auto check = [&](const std::string& k) {
-      for (auto& sig : workers_[0]->program().kernels())
-        if (sig.name == k && sig.arity >= 0 && sig.arity != nargs)
-          throw Error("kernel " + k + " takes " + std::to_string(sig.arity) + " array parameter(s) but compute passes " +
-                      std::to_string(nargs));
+      const int ar = workers_[0]->program().arity(k);
+      if (ar >= 0 && ar != nargs)
+        throw Error("kernel " + k + " takes " + std::to_string(ar) + " array parameter(s) but compute passes " +
+                    std::to_string(nargs));
     };
     for (auto& k : c.kernels) check(k);
     if (!c.repeat_kernel.empty()) check(c.repeat_kernel);

@@ -820,6 +820,16 @@ Program::~Program() {
   // object may still be registered on pool threads.
 }
 
+int Program::arity(const std::string& name) const {
+  std::lock_guard<std::mutex> g(arity_mu_);
+  if (arity_.size() != kernels_.size()) {
+    arity_.clear();
+    for (const auto& k : kernels_) arity_.emplace(k.name, k.arity);
+  }
+  auto it = arity_.find(name);
+  return it == arity_.end() ? -1 : it->second;
+}
+
 bool Program::has(const std::string& name) const {
   return type_ == kGPU ? gpu_fns_.count(name) > 0 : cpu_fns_.count(name) > 0;
 }

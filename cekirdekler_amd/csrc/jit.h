@@ -19,6 +19,8 @@
 #include "device.h"
 
 #include <map>
+#include <unordered_map>
+#include <mutex>
 #include <set>
 
 namespace cek {
@@ -55,6 +57,9 @@ class Program {
   bool ok() const { return ok_; }
   const std::string& log() const { return log_; }
   const std::vector<KernelSig>& kernels() const { return kernels_; }
+  // user-parameter count of a kernel (-1: unknown name or unparsed), by a
+  // hash lookup (compute() checks it on every call)
+  int arity(const std::string& name) const;
   bool has(const std::string& name) const;
   hipFunction_t gpu_fn(const std::string& name) const;
   CpuRunner cpu_fn(const std::string& name) const;
@@ -76,6 +81,8 @@ class Program {
   std::vector<KernelSig> kernels_;
   std::vector<hipModule_t> modules_;
   std::map<std::string, hipFunction_t> gpu_fns_;
+  mutable std::mutex arity_mu_;
+  mutable std::unordered_map<std::string, int> arity_;  // built from kernels_ on first use
   void* dl_ = nullptr;
   std::map<std::string, CpuRunner> cpu_fns_;
 };
