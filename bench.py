@@ -559,8 +559,9 @@ def bench_sgemm_slices(steps: int, rows=(4096, 2048, 1024), size: int = 8192) ->
             torch.cuda.synchronize()
             rounds.append((time.perf_counter() - t0) * 1e3 / steps)
         ms = sorted(rounds)[len(rounds) // 2]
+        rounds_tf = [round(g.flops / r / 1e9, 1) for r in rounds]
         err, tiles = g.verify_full(compute_id=1)
-        out[str(m)] = {"tflops": round(g.flops / ms / 1e9, 1), "ms": round(ms, 4), "tile": tile,
+        out[str(m)] = {"tflops": round(g.flops / ms / 1e9, 1), "ms": round(ms, 4), "tile": tile, "rounds_tflops": rounds_tf,
                        "max_rel_err": err, "tiles_checked": tiles, "tiles_total": g.tiles,
                        "handover_fallbacks": g.handover_fallbacks()}
         cr.dispose()

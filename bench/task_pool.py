@@ -315,11 +315,14 @@ def run_policy(policy, spans=False):
     return n, ms, counts, dispatch, concurrent
 
 
-def dispatch_one_device(dev, tasks=4096):
+def dispatch_one_device(dev, tasks=4096, queues=1):
     """Tasks per second through a pool of ONE whole-GPU device: the host cost
     per task of one consumer thread that has its GPU to itself (on an 8-GPU
-    node every consumer does)."""
-    pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, True, a.queues, prebuilt=prebuilt)
+    node every consumer does).  One queue: the FIFO-greedy projection runs
+    one task at a time per device, and a launch that alternates between
+    streams costs the HIP runtime 2-3× a launch on one stream
+    (tools/pool_cost_probe.py, profiles/r6/README.md)."""
+    pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, True, queues, prebuilt=prebuilt)
     pool.add_device(dev)
     xs = [ck.ClArray(np.zeros(256, np.float32)) for _ in range(64)]
     for x in xs:
@@ -348,6 +351,7 @@ def dispatch_one_device(dev, tasks=4096):
 # one consumer with its GPU to itself, measured before the pools below
 # create their (CU-masked) streams in this process
 one_dev_rate = dispatch_one_device(g[0])
+one_dev_rate_q3 = dispatch_one_device(g[0], queues=3)
 ntasks, makespan, counts, dispatch, concurrent = run_policy(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, spans=True)
 ideal = sum(single) / (len(devs) if partitioned else max(1, ng))
 
@@ -385,6 +389,7 @@ proj = greedy_fifo_ms([max(t, h_ms) for t in single_whole], 8, len(work) // 2)
 proj_serial = greedy_fifo_ms([t + h_ms for t in single_whole], 8, len(work) // 2)
 projection = {"devices": 8, "basis": "whole-GPU alone device times, FIFO greedy with the mid-pool barrier",
               "host_us_per_task_one_consumer": round(1e3 * h_ms, 2), "dispatch_tasks_per_s_one_device": round(one_dev_rate),
+              "dispatch_tasks_per_s_one_device_3_queues": round(one_dev_rate_q3),
               "ideal_ms": proj_ideal, "makespan_ms": proj, "makespan_over_ideal": proj / proj_ideal,
               "makespan_serial_host_ms": proj_serial, "makespan_serial_host_over_ideal": proj_serial / proj_ideal,
               "median_task_whole_gpu_us": round(1e3 * float(np.median(single_whole)), 2),

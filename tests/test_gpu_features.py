@@ -991,24 +991,26 @@ def test_cpu_device_inside_gpu_cpu_cruncher_keeps_its_speed():
 def test_device_resident_async_markers_all_reached(gpu):
     """Fine-grained markers of device-resident computes on the async queues
     (the device pool's task shape): every marker is reached once the mode is
-    left, and the array holds every compute's result.  (Markers attached to
-    the kernel launch as its hipExtModuleLaunchKernel stop event failed this
-    check — the last kernel was still running when its marker fired — and
-    were dropped.)"""
+    left, and every compute's result is there.  Each compute writes its own
+    array: computes on different async queues are unordered (the
+    reference's enqueueModeAsyncEnable), so two of them incrementing one
+    array would race."""
     c = ck.ClNumberCruncher(gpu[0], SRC)
     n = 1 << 16
-    x = ck.ClArray(np.zeros(n, np.float32))
-    x.compute(c, 21, "inc", n, 256)  # up once
-    x.read = x.write = False
+    xs = [ck.ClArray(np.full(n, float(k), np.float32)) for k in range(64)]
+    for x in xs:
+        x.compute(c, 21, "inc", n, 256)  # up once (+1)
+        x.read = x.write = False
     c.fine_grained_queue_control = True
     c.enqueue_mode_async_enable = True
     c.enqueue_mode = True
-    for _ in range(64):
+    for x in xs:
         x.compute(c, 21, "inc", n, 256)
     c.enqueue_mode = False
     c.enqueue_mode_async_enable = False
     c.fine_grained_queue_control = False
     assert c.count_markers_remaining() == 0 and c.count_markers_reached() >= 64
-    c.download(x, 0)
-    np.testing.assert_array_equal(x.array, 65.0)
+    for k, x in enumerate(xs):
+        c.download(x, 0)
+        np.testing.assert_array_equal(x.array, k + 2.0)
     c.dispose()
