@@ -546,8 +546,14 @@ def bench_sgemm_slices(steps: int, rows=(4096, 2048, 1024), size: int = 8192) ->
         tile = "256x256pb" if (m // 256) * (size // 256) >= 256 else "256x256pbw"
         cr = ck.ClNumberCruncher(gpu, "", prebuilt=library(*GEMM_LIBS))
         g = GemmBf16(m, size, size, cruncher=cr, tile=tile)
-        for _ in range(5):
-            g.run(compute_id=1, resident=True)
+        # warm-up until the clocks have settled: the first rounds after a
+        # new GEMM object run up to 12 % slow (rounds of one process:
+        # 1278 → 1469 TF/s at 4096 rows, profiles/r6/README.md)
+        t_w = time.perf_counter()
+        while time.perf_counter() - t_w < SLICE_WARMUP_S:
+            for _ in range(10):
+                g.run(compute_id=1, resident=True)
+            torch.cuda.synchronize()
         rounds = []
         for _ in range(SLICE_ROUNDS):  # the median round: one cold round cannot set the number
             torch.cuda.synchronize()
@@ -670,6 +676,7 @@ def bench_node_configs(world: int) -> dict:
 
 
 SLICE_ROUNDS = 5  # bench_sgemm_slices: timed rounds per slice (median)
+SLICE_WARMUP_S = 0.3  # bench_sgemm_slices: untimed GEMMs per slice before timing
 MAX_REL_ERR = 1e-4  # bf16 inputs, fp32 accumulation: measured ~1.5e-6 relative to max |ref| per tile
 NODE_CONFIGS_BUDGET_S = 360  # all of bench_node_configs' child processes together
 PEER_TOPOLOGY_TIMEOUT_S = 90
