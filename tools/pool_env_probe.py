@@ -56,12 +56,19 @@ def rate(prebuilt=None, queues=1):
 
 LIBS = library("sgemm_bf16", "reduce", "nbody", "mandelbrot", "stream")
 out = {"fresh": rate(), "fresh_q3": rate(queues=3), "libs": rate(LIBS)}
+def touch(cr):  # one compute: the cruncher's streams exist
+    x = ck.ClArray(np.zeros(256, np.float32))
+    v = ck.ClArray(np.ones(1, np.float32))
+    x.next_param(v).compute(cr, 1, "add", 256, 256)
+
+
 part = ck.ClNumberCruncher(g[0:1].cu_partitions(8)[0], SRC)
-x = ck.ClArray(np.zeros(256, np.float32))
-x.compute(part, 1, "add", 256, 256) if False else None
+touch(part)
 out["with_partition_cruncher"] = rate()
 out["with_partition_cruncher_libs"] = rate(LIBS)
 parts = [ck.ClNumberCruncher(d, SRC, queue_concurrency=1) for d in g[0:1].cu_partitions(8)]
+for c in parts:
+    touch(c)
 out["with_8_partition_crunchers"] = rate()
 for c in parts:
     c.dispose()
