@@ -58,7 +58,7 @@ LIBS = library("sgemm_bf16", "reduce", "nbody", "mandelbrot", "stream")
 out = {"fresh": rate(), "fresh_q3": rate(queues=3), "libs": rate(LIBS)}
 def touch(cr):  # one compute: the cruncher's streams exist
     x = ck.ClArray(np.zeros(256, np.float32))
-    v = ck.ClArray(np.ones(1, np.float32))
+    v = ck.ClArray(np.ones(256, np.float32))
     x.next_param(v).compute(cr, 1, "add", 256, 256)
 
 
