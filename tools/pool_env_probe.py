@@ -66,7 +66,8 @@ part = ck.ClNumberCruncher(g[0:1].cu_partitions(8)[0], SRC)
 touch(part)
 out["with_partition_cruncher"] = rate()
 out["with_partition_cruncher_libs"] = rate(LIBS)
-parts = [ck.ClNumberCruncher(d, SRC, queue_concurrency=1) for d in g[0:1].cu_partitions(8)]
+cp = g[0:1].cu_partitions(8)
+parts = [ck.ClNumberCruncher(cp[i], SRC, queue_concurrency=1) for i in range(len(cp))]
 for c in parts:
     touch(c)
 out["with_8_partition_crunchers"] = rate()
