@@ -356,11 +356,11 @@ PYBIND11_MODULE(_cek, m) {
       }, py::call_guard<py::gil_scoped_release>());
 
   m.def("launch_rate_probe", [](int ordinal, const std::string& co, const std::string& kernel, int threads,
-                                int launches) {
+                                int launches, int mode) {
         LaunchRate r;
         {
           py::gil_scoped_release rel;
-          r = launch_rate_probe(ordinal, co, kernel, threads, launches);
+          r = launch_rate_probe(ordinal, co, kernel, threads, launches, mode);
         }
         py::dict d;
         d["threads"] = r.threads;
@@ -370,7 +370,8 @@ PYBIND11_MODULE(_cek, m) {
         d["launches_per_s"] = r.launches_per_s;
         d["per_thread_ms"] = r.per_thread_ms;
         return d;
-      }, py::arg("ordinal"), py::arg("code_object"), py::arg("kernel"), py::arg("threads"), py::arg("launches"));
+      }, py::arg("ordinal"), py::arg("code_object"), py::arg("kernel"), py::arg("threads"), py::arg("launches"),
+      py::arg("mode") = 0);
 
   m.def("allgatherv_plan", [](int rank, int world, const std::vector<uint64_t>& offsets,
                               const std::vector<uint64_t>& sizes) {

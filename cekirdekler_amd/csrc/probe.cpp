@@ -11,8 +11,11 @@
 
 namespace cek {
 
+// mode 0: kernelParams (an array of pointers to each argument, which the
+// runtime packs by the kernel's metadata); mode 1: the arguments pre-packed
+// into one buffer (HIP_LAUNCH_PARAM_BUFFER_POINTER)
 LaunchRate launch_rate_probe(int ordinal, const std::string& code_object, const std::string& kernel, int threads,
-                             int launches) {
+                             int launches, int mode) {
   if (threads < 1 || threads > 64 || launches < 1) throw Error("launch_rate_probe: 1..64 threads, >= 1 launch");
   CEK_HIP(hipSetDevice(ordinal));
   hipModule_t mod = nullptr;
@@ -40,10 +43,23 @@ LaunchRate launch_rate_probe(int ordinal, const std::string& code_object, const 
       try {
         CEK_HIP(hipSetDevice(ordinal));
         void* a[] = {&src, &dst, &off, &gsize};
+        struct {
+          void* s;
+          void* d;
+          long long o, g;
+        } packed{src, dst, off, gsize};
+        size_t psize = sizeof(packed);
+        void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &packed, HIP_LAUNCH_PARAM_BUFFER_SIZE, &psize,
+                         HIP_LAUNCH_PARAM_END};
         ++ready;
         while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
         const double t0 = now_ms();
-        for (int k = 0; k < launches; ++k) CEK_HIP(hipModuleLaunchKernel(fn, 1, 1, 1, 64, 1, 1, 0, streams[t], a, nullptr));
+        for (int k = 0; k < launches; ++k) {
+          if (mode == 1)
+            CEK_HIP(hipModuleLaunchKernel(fn, 1, 1, 1, 64, 1, 1, 0, streams[t], nullptr, extra));
+          else
+            CEK_HIP(hipModuleLaunchKernel(fn, 1, 1, 1, 64, 1, 1, 0, streams[t], a, nullptr));
+        }
         ms[t] = now_ms() - t0;
       } catch (const std::exception& e) {
         err[t] = e.what();

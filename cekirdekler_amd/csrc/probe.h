@@ -15,6 +15,6 @@ struct LaunchRate {
 // one 64-thread work-group `launches` times; host time until every launch
 // call returned, and until the device drained.
 LaunchRate launch_rate_probe(int ordinal, const std::string& code_object, const std::string& kernel, int threads,
-                             int launches);
+                             int launches, int mode = 0);
 
 }  // namespace cek
