@@ -547,7 +547,7 @@ PYBIND11_MODULE(_cek, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("graph_destroy", &Cores::graph_destroy, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("capturing", &Cores::capturing)
-      .def("release_array", &Cores::release_array)
+      .def("release_array", &Cores::release_array, py::call_guard<py::gil_scoped_release>())
       .def("device_bytes", &Cores::device_bytes)
       .def("device_pointer", &Cores::device_pointer)
       .def("upload", &Cores::upload, py::call_guard<py::gil_scoped_release>())

@@ -198,7 +198,8 @@ void DevicePool::complete(int dev, long long id, bool notify, double ms, const s
   {
     std::lock_guard<std::mutex> g(mu_);
     if (id >= 0) {
-      if (static_cast<size_t>(id) >= results_.size()) results_.resize(static_cast<size_t>(id) + 1 + 1024);
+      if (static_cast<size_t>(id) >= results_.size())  // geometric growth: ids rise by one per task
+        results_.resize(std::max<size_t>(static_cast<size_t>(id) + 1, 2 * results_.size() + 1024));
       results_[static_cast<size_t>(id)] = {dev, static_cast<float>(ms)};
     }
     if (!err.empty()) errors_.push_back({id, dev, ms, err});
