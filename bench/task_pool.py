@@ -387,7 +387,18 @@ h_ms = 1e3 / one_dev_rate
 proj_ideal = sum(single_whole) / 8
 proj = greedy_fifo_ms([max(t, h_ms) for t in single_whole], 8, len(work) // 2)
 proj_serial = greedy_fifo_ms([t + h_ms for t in single_whole], 8, len(work) // 2)
+# context for the projection: the same FIFO greedy with no host cost at all,
+# longest-first within each barrier segment (LPT), and both without the
+# barrier — the pool's own order and its mid-pool barrier, not host cost,
+# set most of the gap (profiles/r6/README.md)
+half = len(work) // 2
+lpt = sorted(single_whole[:half], reverse=True) + sorted(single_whole[half:], reverse=True)
+schedule_bounds = {"fifo_no_host_cost": greedy_fifo_ms(single_whole, 8, half) / proj_ideal,
+                   "lpt_no_host_cost": greedy_fifo_ms(lpt, 8, half) / proj_ideal,
+                   "fifo_no_barrier": greedy_fifo_ms(single_whole, 8, -1) / proj_ideal,
+                   "lpt_no_barrier": greedy_fifo_ms(sorted(single_whole, reverse=True), 8, -1) / proj_ideal}
 projection = {"devices": 8, "basis": "whole-GPU alone device times, FIFO greedy with the mid-pool barrier",
+              "schedule_bounds": schedule_bounds,
               "host_us_per_task_one_consumer": round(1e3 * h_ms, 2), "dispatch_tasks_per_s_one_device": round(one_dev_rate),
               "dispatch_tasks_per_s_one_device_3_queues": round(one_dev_rate_q3),
               "ideal_ms": proj_ideal, "makespan_ms": proj, "makespan_over_ideal": proj / proj_ideal,
