@@ -49,6 +49,11 @@ ap.add_argument("--calls", type=int, default=6, help="timed calls per round and 
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--warm", type=int, default=25, help="balancer convergence calls")
 ap.add_argument("--blobs", type=int, default=8)
+ap.add_argument("--order", default="",
+                help="comma list of configs in run order (a name may repeat with a _N suffix: "
+                     "gpu+cpu_2 is a second law cruncher); default cpu,gpu,gpu+cpu,gpu+cpu_fit")
+ap.add_argument("--records", action="store_true",
+                help="keep each mixed cruncher's per-call record (wall, per-device ms, GPU share)")
 ap.add_argument("--cpu-threads", type=int, default=-1,
                 help="cap on the CPU device's threads (default: the process's CPU share minus one)")
 a = ap.parse_args()
@@ -68,6 +73,13 @@ y.partial_read = True
 configs = [("cpu", cpu)]
 if len(gpus):
     configs += [("gpu", gpus[0]), ("gpu+cpu", gpus[0] + cpu), ("gpu+cpu_fit", gpus[0] + cpu)]
+if a.order:
+    base = {"cpu": lambda: cpu, "gpu": lambda: gpus[0], "gpu+cpu": lambda: gpus[0] + cpu,
+            "gpu+cpu_fit": lambda: gpus[0] + cpu}
+    configs = []
+    for name in a.order.split(","):
+        key = name if name in base else name.rsplit("_", 1)[0]
+        configs.append((name, base[key]()))
 
 out = {"config": "hetero_stream", "n": n, "bytes_per_call": 12 * n, "cpu_threads": cpu.device(0).native_info().cpu_threads,
        "timing": f"median of {a.rounds} interleaved rounds of {a.calls} calls per config",
@@ -99,11 +111,17 @@ for iters in [int(s) for s in a.iters.split(",")]:
         for _ in range(a.warm):
             call(cr)
     runs = {name: [] for name in crs}
+    recs = {name: [] for name in crs if "+" in name}
     for _ in range(a.rounds):
         for name, cr in crs.items():
             t = time.perf_counter()
             for _ in range(a.calls):
                 call(cr)
+                if a.records and name in recs:
+                    r = cr.last_record()
+                    rr = r["ranges"]
+                    recs[name].append([round(r["wall_ms"], 3), [round(v, 3) for v in r["device_ms"]],
+                                       round(rr[0] / max(1, sum(rr)), 4)])
             runs[name].append((time.perf_counter() - t) * 1e3 / a.calls)
     res = {}
     probe = np.concatenate([np.arange(0, 4096), rng.integers(0, n, 4096), np.arange(n - 4096, n)])
@@ -119,11 +137,13 @@ for iters in [int(s) for s in a.iters.split(",")]:
         if "+" in name:
             rr = cr.ranges(1)
             r["shares"] = [v / sum(rr) for v in rr]
+        if a.records and name in recs:
+            r["records"] = recs[name]
         if name.endswith("_fit"):
             r["predictor"] = cr.balancer_predictor_info(1)
         res[name] = r
         cr.dispose()
-    if "gpu+cpu" in res:
+    if all(k in res for k in ("cpu", "gpu", "gpu+cpu")):
         res["speedup_over_cpu"] = res["cpu"]["ms"] / res["gpu+cpu"]["ms"]
         res["speedup_over_gpu"] = res["gpu"]["ms"] / res["gpu+cpu"]["ms"]
         res["ideal_ms"] = 1.0 / (1.0 / res["cpu"]["ms"] + 1.0 / res["gpu"]["ms"])
