@@ -508,6 +508,7 @@ PYBIND11_MODULE(_cek, m) {
       .def("set_dynamic_lds", &Cores::set_dynamic_lds)
       .def("has_state", &Cores::has_state)
       .def("ranges", &Cores::ranges)
+      .def("cpu_pool_id", &Cores::cpu_pool_id)
       .def("references", &Cores::references)
       .def("benchmarks", &Cores::benchmarks)
       .def("history", &Cores::history)

@@ -21,6 +21,7 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
   double t0 = now_ms();
   // One code object per architecture, one module per device.
   std::ostringstream errs;
+  int cpu_slot = 0;
   for (size_t i = 0; i < devices.size(); ++i) {
     const auto& d = devices[i];
     std::shared_ptr<Program> prog;
@@ -36,7 +37,8 @@ Cores::Cores(const std::vector<DeviceInfo>& devices, const std::string& source,
       error_code_ = 1;
       continue;
     }
-    workers_.emplace_back(new Worker(d, prog, cfg.queue_concurrency, cfg.no_pipelining));
+    workers_.emplace_back(new Worker(d, prog, cfg.queue_concurrency, cfg.no_pipelining,
+                                     d.type == kGPU ? 0 : cpu_slot++));
   }
   error_ = errs.str();
   if (workers_.empty() && error_code_ == 0) {

@@ -243,6 +243,11 @@ class Cores {
     for (auto& w : workers_) w->set_cu_reserve(n);
   }
   int copy_cus() const { return workers_.empty() ? 0 : workers_[0]->cu_reserve(); }
+  // identity of device w's host thread pool (0 for a GPU): equal across
+  // crunchers that share one (CpuPool::shared)
+  uintptr_t cpu_pool_id(int w) const {
+    return (w < 0 || w >= static_cast<int>(workers_.size())) ? 0 : workers_[w]->cpu_pool_id();
+  }
   uint64_t kernel_d2h_bytes() const {
     uint64_t b = 0;
     for (auto& w : workers_) b += w->kernel_d2h_bytes();

@@ -1,5 +1,6 @@
 #include "worker.h"
 
+#include <map>
 #include <set>
 
 #include <algorithm>
@@ -89,12 +90,32 @@ void CpuPool::loop() {
   }
 }
 
+std::shared_ptr<CpuPool> CpuPool::shared(int threads, int slot) {
+  static const bool on = [] {
+    const char* e = std::getenv("CEK_SHARED_CPU_POOL");
+    return !(e && std::string(e) == "0");
+  }();
+  threads = std::max(1, threads);
+  if (!on) return std::make_shared<CpuPool>(threads);
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, std::weak_ptr<CpuPool>> pools;
+  std::lock_guard<std::mutex> g(mu);
+  auto& w = pools[{threads, slot}];
+  auto p = w.lock();
+  if (!p) {
+    p = std::make_shared<CpuPool>(threads);
+    w = p;
+  }
+  return p;
+}
+
 void CpuPool::parallel_for(long long n, const std::function<void(long long)>& fn) {
   if (n <= 0) return;
   if (threads_.empty() || n == 1) {
     for (long long i = 0; i < n; ++i) fn(i);
     return;
   }
+  std::lock_guard<std::mutex> turn(call_mu_);
   {
     std::lock_guard<std::mutex> g(mu_);
     fn_ = &fn;
@@ -127,7 +148,7 @@ void CpuPool::parallel_for(long long n, const std::function<void(long long)>& fn
 // ------------------------------------------------------------------ Worker --
 
 Worker::Worker(const DeviceInfo& dev, std::shared_ptr<Program> prog, int queue_concurrency,
-               bool no_pipelining)
+               bool no_pipelining, int cpu_slot)
     : dev_(dev), prog_(std::move(prog)), qconc_(queue_concurrency < 1 ? 1 : (queue_concurrency > 16 ? 16 : queue_concurrency)),
       no_pipelining_(no_pipelining) {
   cq_.assign(16, nullptr);
@@ -143,7 +164,7 @@ Worker::Worker(const DeviceInfo& dev, std::shared_ptr<Program> prog, int queue_c
     // one lookup here instead of a runtime call (under HIP's lock) per marker
     marker_dev_ = static_cast<uint64_t*>(host_device_ptr(marker_words_));
   } else {
-    pool_.reset(new CpuPool(dev_.cpu_threads > 0 ? dev_.cpu_threads : 1));
+    pool_ = CpuPool::shared(dev_.cpu_threads > 0 ? dev_.cpu_threads : 1, cpu_slot);
   }
   th_ = std::thread([this] { thread_loop(); });
 }

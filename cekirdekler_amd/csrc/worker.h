@@ -65,12 +65,24 @@ class CpuPool {
  public:
   explicit CpuPool(int threads);
   ~CpuPool();
-  // Run fn(i) for i in [0, n) across the pool; blocks until done.
+  // Run fn(i) for i in [0, n) across the pool; blocks until done.  Callers
+  // on different threads take turns (a pool may be shared, see shared()).
   void parallel_for(long long n, const std::function<void(long long)>& fn);
   int size() const { return static_cast<int>(threads_.size()) + 1; }
+  // The process-wide pool of `threads` threads for the `slot`-th CPU device
+  // of a device set: every cruncher's first CPU device of a given size runs
+  // on the same threads, as an OpenCL CPU runtime shares one thread pool
+  // among its contexts.  Separate crunchers on one host then see the same
+  // CPU device (on a shared host a pool's speed depends on where its
+  // threads landed: 3.0-4.4 ms for the same stream in four crunchers of one
+  // process, profiles/r6/README.md) and do not oversubscribe the host when
+  // used in turn; two CPU devices of ONE set (slots 0 and 1) still run side
+  // by side.  CEK_SHARED_CPU_POOL=0: a pool per device.
+  static std::shared_ptr<CpuPool> shared(int threads, int slot);
 
  private:
   void loop();
+  std::mutex call_mu_;  // one parallel_for at a time
   std::vector<std::thread> threads_;
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
@@ -91,12 +103,15 @@ void apply_sync_mode(int ordinal);
 
 class Worker {
  public:
+  // cpu_slot: this CPU device's index among the CPU devices of its set
+  // (CpuPool::shared); ignored for a GPU
   Worker(const DeviceInfo& dev, std::shared_ptr<Program> prog, int queue_concurrency,
-         bool no_pipelining);
+         bool no_pipelining, int cpu_slot = 0);
   ~Worker();
 
   const DeviceInfo& dev() const { return dev_; }
   bool gpu() const { return dev_.type == kGPU; }
+  uintptr_t cpu_pool_id() const { return reinterpret_cast<uintptr_t>(pool_.get()); }
   Program& program() { return *prog_; }
 
   // --- buffers ---------------------------------------------------------
@@ -285,7 +300,7 @@ class Worker {
   int last_slot_ = -1;
   uint64_t last_value_ = 0;
 
-  std::unique_ptr<CpuPool> pool_;
+  std::shared_ptr<CpuPool> pool_;
   std::unordered_map<std::string, hipGraphExec_t> graphs_;
 
   std::thread th_;

@@ -422,3 +422,46 @@ def test_queue_concurrency_and_last_used_compute_id(cpu):
     x.compute(cr, 7, "k", 256, 64)
     assert cr.lastUsedComputeId == 7 and cr.numberOfDevices == cr.number_of_devices
     cr.dispose()
+
+
+def test_cpu_pool_shared_between_crunchers_and_safe_concurrently(cpu):
+    """Crunchers whose CPU device has the same thread count run on one
+    process-wide pool (CpuPool::shared); two CPU devices of one set keep two
+    pools, and two crunchers computing at once from two threads take turns
+    on the shared pool with correct results."""
+    import threading
+
+    a = ck.ClNumberCruncher(cpu, SRC)
+    b = ck.ClNumberCruncher(cpu, SRC)
+    two = ck.ClNumberCruncher(cpu + cpu, SRC)
+    try:
+        pa, pb = a._cores.cpu_pool_id(0), b._cores.cpu_pool_id(0)
+        assert pa != 0 and pa == pb
+        assert two._cores.cpu_pool_id(0) == pa
+        assert two._cores.cpu_pool_id(1) not in (0, pa)
+        n = 1 << 18
+        errs = []
+
+        def run(cr, seed):
+            try:
+                rng = np.random.default_rng(seed)
+                av = ck.ClArray(np.array([1.5], np.float32))
+                av.write = False
+                x = ck.ClArray(rng.random(n, dtype=np.float32))
+                for _ in range(20):
+                    y0 = rng.random(n, dtype=np.float32)
+                    y = ck.ClArray(y0.copy())
+                    av.next_param(x, y).compute(cr, 7, "saxpy", n, 256)
+                    np.testing.assert_array_equal(y.array, np.float32(1.5) * x.array + y0)
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+
+        ts = [threading.Thread(target=run, args=(c, s)) for s, c in enumerate((a, b, two))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errs, errs
+    finally:
+        for c in (a, b, two):
+            c.dispose()
