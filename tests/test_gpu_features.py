@@ -974,15 +974,20 @@ def test_cpu_device_inside_gpu_cpu_cruncher_keeps_its_speed():
     xs.write = False
     ys.read = False
     xs.next_param(ys).compute(alone, 1, "poly", r_cpu, 256)
-    m_rate, a_rate = [], []
-    for _ in range(12):  # interleaved: host-load drift hits both alike
-        x.next_param(y).compute(mixed, 1, "poly", n, 256)
-        rec = mixed.last_record()
-        m_rate.append(rec["ranges"][1] / rec["device_ms"][1])
-        xs.next_param(ys).compute(alone, 1, "poly", r_cpu, 256)
-        a_rate.append(r_cpu / alone.last_record()["device_ms"][0])
-    mixed_rate, alone_rate = statistics.median(m_rate), statistics.median(a_rate)
-    assert mixed_rate >= alone_rate / 1.05, (mixed_rate, alone_rate, cpu_threads, r_cpu)
+    # three rounds of interleaved pairs (host-load drift hits both alike); a
+    # slowdown of the mixed set's CPU device shows in every round, a
+    # neighbour's burst on the shared host in one
+    ratios = []
+    for _ in range(3):
+        m_rate, a_rate = [], []
+        for _ in range(20):
+            x.next_param(y).compute(mixed, 1, "poly", n, 256)
+            rec = mixed.last_record()
+            m_rate.append(rec["ranges"][1] / rec["device_ms"][1])
+            xs.next_param(ys).compute(alone, 1, "poly", r_cpu, 256)
+            a_rate.append(r_cpu / alone.last_record()["device_ms"][0])
+        ratios.append(statistics.median(m_rate) / statistics.median(a_rate))
+    assert max(ratios) >= 1 / 1.05, (ratios, cpu_threads, r_cpu)
     mixed.dispose()
     alone.dispose()
 
