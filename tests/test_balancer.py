@@ -91,7 +91,7 @@ def test_measured_lb_iters_two_cpu_devices(outliers):
     # two threads per device: the measurement stays meaningful when the
     # test runner shares the host with other workers
     devs = p.cpus(True, max_cpu_cores=2) + p.cpus(True, max_cpu_cores=2)
-    r = B.measure_lb_convergence(devs, calls=40, n=1 << 15, inner=256, outliers=outliers)
+    r = B.measure_lb_convergence(devs, calls=40, n=1 << 16, inner=256, outliers=outliers)
     assert r["iters"] <= 10, r
     assert abs(r["steady_share_dev0"] - 2 / 3) < 0.05, r
     assert len(r["shares"]) == 40
