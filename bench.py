@@ -805,6 +805,7 @@ def compact_extra(full: dict, detail: str) -> dict:
             sb = pj.get("schedule_bounds") or {}
             t["projected_8gpu_fifo_zero_host_cost"] = _r(sb.get("fifo_no_host_cost"))
             t["projected_8gpu_lpt_zero_host_cost"] = _r(sb.get("lpt_no_host_cost"))
+            t["projected_8gpu_without_barrier_task"] = _r(pj.get("makespan_no_barrier_over_ideal"))
         ex["task_pool"] = t
     nb = full.get("nbody_pipeline")
     if isinstance(nb, dict):

@@ -397,8 +397,14 @@ schedule_bounds = {"fifo_no_host_cost": greedy_fifo_ms(single_whole, 8, half) / 
                    "lpt_no_host_cost": greedy_fifo_ms(lpt, 8, half) / proj_ideal,
                    "fifo_no_barrier": greedy_fifo_ms(single_whole, 8, -1) / proj_ideal,
                    "lpt_no_barrier": greedy_fifo_ms(sorted(single_whole, reverse=True), 8, -1) / proj_ideal}
+# BASELINE config 5 is "256 mixed non-separable kernels, greedy async
+# schedule": this pool adds a global barrier task to exercise the reference's
+# TASK_MESSAGE_GLOBAL_SYNCHRONIZATION_FIRST, which drains every device half
+# way; the same projection without that task, host cost included
+proj_nb = greedy_fifo_ms([max(t, h_ms) for t in single_whole], 8, -1)
 projection = {"devices": 8, "basis": "whole-GPU alone device times, FIFO greedy with the mid-pool barrier",
               "schedule_bounds": schedule_bounds,
+              "makespan_no_barrier_ms": proj_nb, "makespan_no_barrier_over_ideal": proj_nb / proj_ideal,
               "host_us_per_task_one_consumer": round(1e3 * h_ms, 2), "dispatch_tasks_per_s_one_device": round(one_dev_rate),
               "dispatch_tasks_per_s_one_device_3_queues": round(one_dev_rate_q3),
               "ideal_ms": proj_ideal, "makespan_ms": proj, "makespan_over_ideal": proj / proj_ideal,
