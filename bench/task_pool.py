@@ -86,6 +86,50 @@ elif ng == 1 and a.logical > 1:
         devs = devs + g[0]
 rng = np.random.default_rng(3)
 prebuilt = library(*LIBS)
+
+
+def dispatch_one_device(dev, tasks=4096, queues=1):
+    """Tasks per second through a pool of ONE whole-GPU device: the host cost
+    per task of one consumer thread that has its GPU to itself (on an 8-GPU
+    node every consumer does).  One queue: the FIFO-greedy projection runs
+    one task at a time per device, and a launch that alternates between
+    streams costs the HIP runtime 2-3× a launch on one stream
+    (tools/pool_cost_probe.py, profiles/r6/README.md)."""
+    pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, True, queues, prebuilt=prebuilt)
+    pool.add_device(dev)
+    xs = [ck.ClArray(np.zeros(256, np.float32)) for _ in range(64)]
+    for x in xs:
+        x.read = x.write = False
+        pool.crunchers[0].upload(x)
+    v = ck.ClArray(np.array([1.0], np.float32))
+    v.write = False
+    pool.crunchers[0].upload(v)
+
+    def tiny(k):
+        t = ClTaskPool()
+        for i in range(k):
+            t.feed(xs[i % 64].next_param(v).task(3, "add", 256, 256))
+        return t
+    pool.enqueue_task_pool(tiny(512))
+    pool.finish()
+    tp = tiny(tasks)
+    sync()
+    t0 = time.perf_counter()
+    pool.enqueue_task_pool(tp)
+    pool.finish()
+    sync()
+    rate = tasks / (time.perf_counter() - t0)
+    pool.dispose()
+    return rate
+
+
+# one consumer with its GPU to itself, measured first: before any other
+# cruncher of this process creates its (CU-masked) streams, which raise the
+# HIP launch cost of every stream (15.5 µs per task measured after them,
+# 4 µs before)
+one_dev_rate = dispatch_one_device(g[0])
+one_dev_rate_q3 = dispatch_one_device(g[0], queues=3)
+
 # the per-task reference times: alone on ONE pool device (a partition when partitioned)
 ref_cr = ck.ClNumberCruncher(devs[0], SRC, prebuilt=prebuilt)
 NS = 1 << 22  # streaming / reduction elements
@@ -315,43 +359,6 @@ def run_policy(policy, spans=False):
     return n, ms, counts, dispatch, concurrent
 
 
-def dispatch_one_device(dev, tasks=4096, queues=1):
-    """Tasks per second through a pool of ONE whole-GPU device: the host cost
-    per task of one consumer thread that has its GPU to itself (on an 8-GPU
-    node every consumer does).  One queue: the FIFO-greedy projection runs
-    one task at a time per device, and a launch that alternates between
-    streams costs the HIP runtime 2-3× a launch on one stream
-    (tools/pool_cost_probe.py, profiles/r6/README.md)."""
-    pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, True, queues, prebuilt=prebuilt)
-    pool.add_device(dev)
-    xs = [ck.ClArray(np.zeros(256, np.float32)) for _ in range(64)]
-    for x in xs:
-        x.read = x.write = False
-        pool.crunchers[0].upload(x)
-    pool.crunchers[0].upload(serial_v)
-
-    def tiny(k):
-        t = ClTaskPool()
-        for i in range(k):
-            t.feed(xs[i % 64].next_param(serial_v).task(3, "add", 256, 256))
-        return t
-    pool.enqueue_task_pool(tiny(512))
-    pool.finish()
-    tp = tiny(tasks)
-    sync()
-    t0 = time.perf_counter()
-    pool.enqueue_task_pool(tp)
-    pool.finish()
-    sync()
-    rate = tasks / (time.perf_counter() - t0)
-    pool.dispose()
-    return rate
-
-
-# one consumer with its GPU to itself, measured before the pools below
-# create their (CU-masked) streams in this process
-one_dev_rate = dispatch_one_device(g[0])
-one_dev_rate_q3 = dispatch_one_device(g[0], queues=3)
 ntasks, makespan, counts, dispatch, concurrent = run_policy(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, spans=True)
 ideal = sum(single) / (len(devs) if partitioned else max(1, ng))
 

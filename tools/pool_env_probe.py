@@ -55,6 +55,15 @@ def rate(prebuilt=None, queues=1):
 
 
 LIBS = library("sgemm_bf16", "reduce", "nbody", "mandelbrot", "stream")
+if len(sys.argv) > 1:
+    # one case per process, for a HIP API trace of each (rocprofv3 --hip-trace --stats):
+    # "fresh" = one queue in a fresh process; "after_q3" = the same after a
+    # 3-queue pool has come and gone
+    case = sys.argv[1]
+    if case == "after_q3":
+        rate(queues=3)
+    print(json.dumps({case: rate()}), flush=True)
+    sys.exit(0)
 out = {"fresh": rate(), "fresh_q3": rate(queues=3), "libs": rate(LIBS)}
 def touch(cr):  # one compute: the cruncher's streams exist
     x = ck.ClArray(np.zeros(256, np.float32))
