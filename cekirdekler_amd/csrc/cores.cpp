@@ -1388,7 +1388,12 @@ void Cores::run_3phase(Worker& wk, int gidx, const ComputeCall& c, long long ref
     span_end(wk, s);
   }
   if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(s);
-  if (fine_grained) wk.add_marker(s, marker_needs_release(c));
+  if (fine_grained) {
+    if (defer_marker)
+      wk.defer_marker(s, marker_needs_release(c));
+    else
+      wk.add_marker(s, marker_needs_release(c));
+  }
   if (!enqueue_mode_ && wk.gpu()) wk.wait_stream(s, sleep_waits || sleep_this_call_);
 }
 
@@ -1542,7 +1547,12 @@ void Cores::run_event_pipeline(Worker& wk, int gidx, const ComputeCall& c, long 
   }
   span_end(wk, m);
   if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(m);
-  if (fine_grained) wk.add_marker(m, marker_needs_release(c));
+  if (fine_grained) {
+    if (defer_marker)
+      wk.defer_marker(m, marker_needs_release(c));
+    else
+      wk.add_marker(m, marker_needs_release(c));
+  }
   if (wk.gpu()) wk.wait_stream(m, sleep_waits || sleep_this_call_);
 }
 
@@ -1657,7 +1667,12 @@ void Cores::run_driver_pipeline(Worker& wk, int gidx, const ComputeCall& c, long
   }
   span_end(wk, m);
   if (zc_release && !enqueue_mode_ && writes_host_memory(c)) wk.system_release(m);
-  if (fine_grained) wk.add_marker(m, marker_needs_release(c));
+  if (fine_grained) {
+    if (defer_marker)
+      wk.defer_marker(m, marker_needs_release(c));
+    else
+      wk.add_marker(m, marker_needs_release(c));
+  }
   if (wk.gpu()) wk.wait_stream(m, sleep_waits || sleep_this_call_);
 }
 

@@ -165,6 +165,10 @@ class Cores {
   bool async_enqueue = false;
   bool no_compute = false;
   bool fine_grained = false;
+  // with fine_grained: this compute's marker is deferred (Worker::defer_marker)
+  // until flush_markers(); the device pool sets it per task
+  bool defer_marker = false;
+  void flush_markers(int dev) { workers_.at(dev)->flush_markers(); }
   bool smooth = true;
   bool serial = false;  // run devices one after another (isolated timings)
   // Repeat loops with at least this many launches per device are captured

@@ -279,6 +279,15 @@ int DevicePool::retire(int dev, std::vector<Inflight>& inflight) {
   return n;
 }
 
+int pool_marker_batch() {
+  static const int k = [] {
+    const char* e = std::getenv("CEK_POOL_MARKER_BATCH");
+    const int v = e ? std::atoi(e) : 8;
+    return std::max(1, std::min(64, v));
+  }();
+  return k;
+}
+
 void DevicePool::consumer(int dev) {
   Cores& cr = *devs_[dev];
   const bool async = max_in_flight_ > 1;
@@ -289,6 +298,14 @@ void DevicePool::consumer(int dev) {
   std::shared_ptr<const ComputeCall> call_keep;  // keeps that template alive
   double last_progress = now_ms();
   bool issued = false;  // the previous iteration issued a task
+  const int batch = pool_marker_batch();
+  int deferred = 0;     // tasks in flight whose marker is not recorded yet
+  auto flush = [&] {
+    if (deferred > 0) {
+      cr.flush_markers(0);
+      deferred = 0;
+    }
+  };
   for (;;) {
     // while tasks keep flowing, poll the markers only once a few are in
     // flight: each poll is a HIP call that costs about as much as a launch
@@ -302,10 +319,13 @@ void DevicePool::consumer(int dev) {
     }
     issued = false;
     Item it;
-    bool got = false, idle = false, stop = false;
+    bool got = false, idle = false, stop = false, more = false;
+    int lim = 1;
     {
       std::unique_lock<std::mutex> lk(mu_);
-      if (static_cast<int>(inflight.size()) < limit_locked()) got = take_locked(dev, it);
+      lim = limit_locked();
+      if (static_cast<int>(inflight.size()) < lim) got = take_locked(dev, it);
+      more = !queue_.empty();
       if (!got && inflight.empty()) {
         if (closed_ && queue_.empty())
           stop = true;
@@ -327,6 +347,7 @@ void DevicePool::consumer(int dev) {
       continue;
     }
     if (!got) {  // only in-flight tasks: poll their markers
+      flush();  // (a deferred marker would never be reached otherwise)
       // yield-spin while tasks keep retiring: a sleep, however short it is
       // asked to be, costs ~60 µs on Linux — longer than most tasks on a
       // partition, and a late retirement leaves the device idle (median
@@ -360,8 +381,23 @@ void DevicePool::consumer(int dev) {
       if (async) {
         if (!cr.enqueue_mode()) cr.set_enqueue_mode(true);
         cr.async_enqueue = !it.serial;  // serial groups stay on one in-order stream
+        // coalesce this task's marker with the next tasks' while more work
+        // follows at once (the batch's last task records it)
+        const bool defer = batch > 1 && !notify && !it.serial && more && deferred + 1 < batch &&
+                           static_cast<int>(inflight.size()) + 1 < lim;
+        cr.defer_marker = defer;
         const double i0 = now_ms();
-        cr.compute(call);
+        try {
+          cr.compute(call);
+        } catch (...) {
+          cr.defer_marker = false;
+          throw;
+        }
+        cr.defer_marker = false;
+        if (defer)
+          ++deferred;
+        else
+          flush();  // this task's marker covers its stream; record the others'
         add_ms(prof_issue_ms_, now_ms() - i0);
         prof_tasks_.fetch_add(1, std::memory_order_relaxed);
         auto m = cr.last_marker(0);

@@ -7,9 +7,9 @@
 // :4841-5047).  Here every consumer is a C++ thread that owns one
 // single-device `Cores`; it takes the next task under one mutex, issues it in
 // enqueue mode on the device's round-robin HIP streams, and retires it when
-// the device writes the task's marker word (hipStreamWriteValue64 into pinned
-// memory) — no host callback, no GIL, no Python per task.  Up to
-// `max_in_flight` tasks per device are outstanding at once.
+// the device reaches the task's completion marker (a fence-less hipEvent,
+// shared by a batch of consecutive tasks) — no host callback, no GIL, no
+// Python per task.  Up to `max_in_flight` tasks per device are outstanding.
 //
 // Task type flags (ClTaskType, ClPipeline.cs:3247-3321):
 //   SELECT_BEGIN/END, SERIAL_BEGIN/END  pin the group to the device that took
@@ -73,6 +73,12 @@ constexpr uint32_t kTaskNotify = 1u << 30;
 // a consumer issuing back to back polls its markers once this many tasks are
 // in flight (and whenever it cannot issue)
 constexpr int kPollBatch = 3;
+// Consecutive tasks of a consumer share one completion marker (one
+// hipEventRecord per stream per batch, recorded after the batch's last
+// task): at most this many per batch; a batch also ends when the consumer
+// runs out of tasks to take, at a callback or serial-group task, and before
+// it would wait for a retirement (CEK_POOL_MARKER_BATCH, 1 = a marker per task)
+int pool_marker_batch();
 
 struct PoolTask {
   // the compute without its arrays, shared by every task of one shape (a

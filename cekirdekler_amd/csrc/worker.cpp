@@ -795,6 +795,34 @@ int Worker::device_enqueue_errors() {
   return total;
 }
 
+hipStream_t Worker::slot_stream(int slot) const {
+  if (slot == 0) return main_;
+  if (slot >= 1 && slot <= 16) return cq_[slot - 1];
+  if (slot >= 17 && slot < 23) return pq_[(slot - 17) / 3][(slot - 17) % 3];
+  return nullptr;
+}
+
+void Worker::defer_marker(hipStream_t s, bool release) {
+  if (!gpu()) {  // a CPU device's compute is done when it returns
+    add_marker(s, release);
+    return;
+  }
+  const int slot = stream_slot(s);
+  if (slot >= 31 || !slot_stream(slot)) {  // not a slot flush_markers() can find again
+    add_marker(s, release);
+    return;
+  }
+  last_slot_ = slot;  // markers_issued_ counts the marker when it is recorded
+  last_value_ = marker_issued_per_slot_[slot] + 1;
+  deferred_slots_ |= 1u << slot;
+  if (release) deferred_release_ |= 1u << slot;
+}
+
+void Worker::flush_markers() {
+  for (int slot = 0; deferred_slots_ != 0 && slot < 31; ++slot)
+    if (deferred_slots_ & (1u << slot)) add_marker(slot_stream(slot), false);
+}
+
 void Worker::add_marker(hipStream_t s, bool release) {
   ++markers_issued_;
   if (!gpu()) {
@@ -803,6 +831,12 @@ void Worker::add_marker(hipStream_t s, bool release) {
     return;
   }
   int slot = stream_slot(s);
+  if (slot < 31 && (deferred_slots_ & (1u << slot))) {
+    // this marker also completes the computes deferred on the same stream
+    release = release || (deferred_release_ & (1u << slot));
+    deferred_slots_ &= ~(1u << slot);
+    deferred_release_ &= ~(1u << slot);
+  }
   uint64_t v = ++marker_issued_per_slot_[slot];
   last_slot_ = slot;
   last_value_ = v;

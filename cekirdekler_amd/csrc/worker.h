@@ -194,6 +194,14 @@ class Worker {
   // release: the marker also makes earlier writes to HOST memory visible
   // (a system-scope release; set when the compute downloaded results)
   void add_marker(hipStream_t s, bool release = false);
+  // A compute that takes its completion from the NEXT marker of its stream:
+  // last_marker() becomes (slot, the value that marker will carry) and no
+  // HIP call is made; flush_markers() records that marker on every stream
+  // with such computes (a device pool coalesces the markers of consecutive
+  // tasks: one hipEventRecord per batch instead of per task)
+  void defer_marker(hipStream_t s, bool release = false);
+  void flush_markers();
+  bool has_deferred_markers() const { return deferred_slots_ != 0; }
   long long markers_reached();
   // (slot, value) of the newest marker; a marker is reached once
   // marker_word(slot) >= value.  CPU device: slot -1 (always reached).
@@ -296,6 +304,9 @@ class Worker {
   hipEvent_t kstamp_event();
   std::mutex marker_mu_;
   bool write_value_markers_ = false;  // CEK_MARKERS=writevalue: the old path
+  uint32_t deferred_slots_ = 0;          // bit per stream slot with deferred markers
+  uint32_t deferred_release_ = 0;        // ... whose marker must also release host writes
+  hipStream_t slot_stream(int slot) const;
   long long markers_issued_ = 0;
   int last_slot_ = -1;
   uint64_t last_value_ = 0;

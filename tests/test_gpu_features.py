@@ -293,6 +293,49 @@ def test_task_pool_gpu(gpu):
     pool.dispose()
 
 
+def test_task_pool_coalesced_markers_gpu(gpu):
+    """Consecutive device-resident tasks of a consumer share one completion
+    marker (pool_marker_batch, default 8): every task still retires with its
+    result in place, fewer markers than tasks are recorded, and every marker
+    is reached once the pool has finished."""
+    from cekirdekler_amd.parallel.pool import ClDevicePool, ClDevicePoolType, ClTaskPool
+
+    src = "__global__ void addv(float* x, const float* v) { x[get_global_id(0)] += v[0]; }"
+    pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, src, True, 1)
+    pool.add_device(gpu[0] + gpu[0])
+    v = ck.ClArray(np.array([1.0], np.float32))
+    v.write = False
+    xs = [ck.ClArray(np.zeros(256, np.float32)) for _ in range(32)]
+    for x in xs:
+        x.read = x.write = False
+        for cr in pool.crunchers:
+            cr.upload(x)
+    for cr in pool.crunchers:
+        cr.upload(v)
+    v.read = False
+    tasks = 2048
+    tp = ClTaskPool()
+    for i in range(tasks):
+        tp.feed(xs[i % 32].next_param(v).task(1, "addv", 256, 256))
+    pool.enqueue_task_pool(tp)
+    pool.finish()
+    counts = pool.device_task_counts()
+    assert sum(counts) == tasks, counts
+    issued = [cr._cores.markers_issued() for cr in pool.crunchers]
+    reached = [cr._cores.markers_reached() for cr in pool.crunchers]
+    assert issued == reached, (issued, reached)
+    assert sum(issued) < tasks, (issued, counts)  # markers were shared
+    # every task ran: each array was incremented by 1 once per task on it,
+    # whichever device ran it (download every device's replica and add up)
+    total = np.zeros(256 * 32, np.float64)
+    for cr in pool.crunchers:
+        for k, x in enumerate(xs):
+            cr.download(x)
+            total[k * 256:(k + 1) * 256] += x.array
+    assert total.sum() == tasks * 256, total.sum()
+    pool.dispose()
+
+
 def test_checkpoint_resume_gpu(gpu, tmp_path):
     from cekirdekler_amd.utils import checkpoint
 

@@ -22,16 +22,18 @@ TASKS = 4096
 g = ck.ClPlatforms.all().gpus()
 
 
-def rate(prebuilt=None, queues=1):
+def rate(prebuilt=None, queues=1, devices=None):
     pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, True, queues, prebuilt=prebuilt)
-    pool.add_device(g[0])
+    pool.add_device(g[0] if devices is None else devices)
     v = ck.ClArray(np.array([1.0], np.float32))
     v.write = False
     xs = [ck.ClArray(np.zeros(256, np.float32)) for _ in range(64)]
     for x in xs:
         x.read = x.write = False
-        pool.crunchers[0].upload(x)
-    pool.crunchers[0].upload(v)
+        for cr in pool.crunchers:
+            cr.upload(x)
+    for cr in pool.crunchers:
+        cr.upload(v)
     v.read = False
 
     def batch(k):
@@ -62,7 +64,14 @@ if len(sys.argv) > 1:
     case = sys.argv[1]
     if case == "after_q3":
         rate(queues=3)
-    print(json.dumps({case: rate()}), flush=True)
+    devices = None
+    if case == "parts8":  # 8 CU partitions, one stream each (the bench's pool)
+        devices = g[0:1].cu_partitions(8)
+    elif case == "logical8":  # 8 whole-GPU logical devices, one stream each
+        devices = g[0]
+        for _ in range(7):
+            devices = devices + g[0]
+    print(json.dumps({case: rate(devices=devices)}), flush=True)
     sys.exit(0)
 out = {"fresh": rate(), "fresh_q3": rate(queues=3), "libs": rate(LIBS)}
 def touch(cr):  # one compute: the cruncher's streams exist
