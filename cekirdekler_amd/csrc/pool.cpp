@@ -382,9 +382,13 @@ void DevicePool::consumer(int dev) {
         if (!cr.enqueue_mode()) cr.set_enqueue_mode(true);
         cr.async_enqueue = !it.serial;  // serial groups stay on one in-order stream
         // coalesce this task's marker with the next tasks' while more work
-        // follows at once (the batch's last task records it)
-        const bool defer = batch > 1 && !notify && !it.serial && more && deferred + 1 < batch &&
-                           static_cast<int>(inflight.size()) + 1 < lim;
+        // follows at once (the batch's last task records it).  A batch
+        // retires only when its last task is done, so it is at most half the
+        // queue-depth limit: the next batch is issued while one runs (with a
+        // shallow limit in the pool's tail, every task keeps its own marker
+        // and retires as soon as it is done)
+        const int eff_batch = std::min(batch, lim / 2);
+        const bool defer = eff_batch > 1 && !notify && !it.serial && more && deferred + 1 < eff_batch;
         cr.defer_marker = defer;
         const double i0 = now_ms();
         try {
