@@ -802,6 +802,7 @@ def compact_extra(full: dict, detail: str) -> dict:
             t["projected_8gpu_makespan_over_ideal"] = _r(pj.get("makespan_over_ideal"))
             t["projected_8gpu_serial_host_over_ideal"] = _r(pj.get("makespan_serial_host_over_ideal"))
             t["dispatch_tasks_per_s_one_device"] = pj.get("dispatch_tasks_per_s_one_device")
+            t["dispatch_tasks_per_s_8_logical_whole_gpu"] = pj.get("dispatch_tasks_per_s_8_whole_gpu_logical_devices")
             sb = pj.get("schedule_bounds") or {}
             t["projected_8gpu_fifo_zero_host_cost"] = _r(sb.get("fifo_no_host_cost"))
             t["projected_8gpu_lpt_zero_host_cost"] = _r(sb.get("lpt_no_host_cost"))

@@ -98,12 +98,13 @@ def dispatch_one_device(dev, tasks=4096, queues=1):
     pool = ClDevicePool(ClDevicePoolType.DEVICE_COMPUTE_AT_WILL, SRC, True, queues, prebuilt=prebuilt)
     pool.add_device(dev)
     xs = [ck.ClArray(np.zeros(256, np.float32)) for _ in range(64)]
-    for x in xs:
-        x.read = x.write = False
-        pool.crunchers[0].upload(x)
     v = ck.ClArray(np.array([1.0], np.float32))
     v.write = False
-    pool.crunchers[0].upload(v)
+    for cr in pool.crunchers:  # every device of the pool (dev may list several)
+        for x in xs:
+            x.read = x.write = False
+            cr.upload(x)
+        cr.upload(v)
 
     def tiny(k):
         t = ClTaskPool()
@@ -127,6 +128,12 @@ def dispatch_one_device(dev, tasks=4096, queues=1):
 # cruncher of this process creates its (CU-masked) streams, which raise the
 # HIP launch cost of every stream (15.5 µs per task measured after them,
 # 4 µs before)
+# 8 consumers, each on a whole-GPU logical device of GPU 0 with one stream:
+# the pool's own host fan-out (>= 400 k tasks/s)
+_eight = g[0]
+for _ in range(7):
+    _eight = _eight + g[0]
+eight_logical_rate = dispatch_one_device(_eight, tasks=8192)
 one_dev_rate = dispatch_one_device(g[0])
 one_dev_rate_q3 = dispatch_one_device(g[0], queues=3)
 
@@ -414,6 +421,7 @@ projection = {"devices": 8, "basis": "whole-GPU alone device times, FIFO greedy 
               "makespan_no_barrier_ms": proj_nb, "makespan_no_barrier_over_ideal": proj_nb / proj_ideal,
               "host_us_per_task_one_consumer": round(1e3 * h_ms, 2), "dispatch_tasks_per_s_one_device": round(one_dev_rate),
               "dispatch_tasks_per_s_one_device_3_queues": round(one_dev_rate_q3),
+              "dispatch_tasks_per_s_8_whole_gpu_logical_devices": round(eight_logical_rate),
               "ideal_ms": proj_ideal, "makespan_ms": proj, "makespan_over_ideal": proj / proj_ideal,
               "makespan_serial_host_ms": proj_serial, "makespan_serial_host_over_ideal": proj_serial / proj_ideal,
               "median_task_whole_gpu_us": round(1e3 * float(np.median(single_whole)), 2),
