@@ -193,32 +193,41 @@ bool DevicePool::take_locked(int dev, Item& out) {
 // record the caller reads; the wake-ups go only to whoever can proceed now:
 // finish() when the pool drains, idle consumers when a barrier or a pinned
 // group may have been waiting for this retirement.
+void DevicePool::complete_locked(int dev, long long id, bool notify, double ms, const std::string& err,
+                                 Wake& w) {
+  if (id >= 0) {
+    if (static_cast<size_t>(id) >= results_.size())  // geometric growth: ids rise by one per task
+      results_.resize(std::max<size_t>(static_cast<size_t>(id) + 1, 2 * results_.size() + 1024));
+    results_[static_cast<size_t>(id)] = {dev, static_cast<float>(ms)};
+  }
+  if (!err.empty()) errors_.push_back({id, dev, ms, err});
+  if (notify) {
+    done_.push_back({id, dev, ms, err});
+    w.comp = true;
+  }
+  ++counts_[dev];
+  busy_ms_[dev] += ms;
+  --outstanding_;
+  --running_;
+  --inflight_[dev];
+  w.done = w.done || outstanding_ == 0;
+  w.work = w.work || running_ == 0 || owner_ >= 0 ||
+           (!queue_.empty() && (queue_.front().task.type & kTaskSyncFirst));
+}
+
+void DevicePool::wake(const Wake& w) {
+  if (w.comp) comp_cv_.notify_all();
+  if (w.done) done_cv_.notify_all();
+  if (w.work) work_cv_.notify_all();
+}
+
 void DevicePool::complete(int dev, long long id, bool notify, double ms, const std::string& err) {
-  bool wake_comp = false, wake_done = false, wake_work = false;
+  Wake w;
   {
     std::lock_guard<std::mutex> g(mu_);
-    if (id >= 0) {
-      if (static_cast<size_t>(id) >= results_.size())  // geometric growth: ids rise by one per task
-        results_.resize(std::max<size_t>(static_cast<size_t>(id) + 1, 2 * results_.size() + 1024));
-      results_[static_cast<size_t>(id)] = {dev, static_cast<float>(ms)};
-    }
-    if (!err.empty()) errors_.push_back({id, dev, ms, err});
-    if (notify) {
-      done_.push_back({id, dev, ms, err});
-      wake_comp = true;
-    }
-    ++counts_[dev];
-    busy_ms_[dev] += ms;
-    --outstanding_;
-    --running_;
-    --inflight_[dev];
-    wake_done = outstanding_ == 0;
-    wake_work = running_ == 0 || owner_ >= 0 ||
-                (!queue_.empty() && (queue_.front().task.type & kTaskSyncFirst));
+    complete_locked(dev, id, notify, ms, err, w);
   }
-  if (wake_comp) comp_cv_.notify_all();
-  if (wake_done) done_cv_.notify_all();
-  if (wake_work) work_cv_.notify_all();
+  wake(w);
 }
 
 std::vector<PoolCompletion> DevicePool::take_errors() {
@@ -242,7 +251,6 @@ void DevicePool::results(long long first, long long n, std::vector<int>& dev, st
 
 int DevicePool::retire(int dev, std::vector<Inflight>& inflight) {
   Cores& cr = *devs_[dev];
-  int n = 0;
   // one marker query per stream slot per poll (a slot's markers retire in
   // order), not one per task in flight: every query takes the HIP runtime's
   // lock that the other consumers' launches need
@@ -259,22 +267,25 @@ int DevicePool::retire(int dev, std::vector<Inflight>& inflight) {
     }
     return w;
   };
-  for (size_t i = 0; i < inflight.size();) {
-    if (word(inflight[i].slot) >= inflight[i].value) {
-      complete(dev, inflight[i].id, inflight[i].notify, now_ms() - inflight[i].t0, "");
-      inflight[i] = inflight.back();
-      inflight.pop_back();
-      ++n;
-    } else {
-      ++i;
+  // the reached tasks move to the end, then retire under ONE lock (a batch
+  // of tasks sharing a marker retires together)
+  size_t keep = 0;
+  for (size_t i = 0; i < inflight.size(); ++i)
+    if (word(inflight[i].slot) < inflight[i].value) std::swap(inflight[keep++], inflight[i]);
+  const int n = static_cast<int>(inflight.size() - keep);
+  if (n > 0) {
+    Wake w;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      const double t = now_ms();
+      for (size_t i = keep; i < inflight.size(); ++i)
+        complete_locked(dev, inflight[i].id, inflight[i].notify, t - inflight[i].t0, "", w);
+      Speed& sp = speed_[dev];  // marker-reach speed (ClPipeline.cs:4788-4817)
+      if (sp.last_ms >= 0) sp.hist[sp.n++ % 15] = n / (t - sp.last_ms + 0.001);
+      sp.last_ms = t;
     }
-  }
-  if (n > 0) {  // marker-reach speed (ClPipeline.cs:4788-4817)
-    std::lock_guard<std::mutex> g(mu_);
-    Speed& sp = speed_[dev];
-    const double t = now_ms();
-    if (sp.last_ms >= 0) sp.hist[sp.n++ % 15] = n / (t - sp.last_ms + 0.001);
-    sp.last_ms = t;
+    inflight.resize(keep);
+    wake(w);
   }
   return n;
 }

@@ -167,6 +167,11 @@ class DevicePool {
   bool take_locked(int dev, Item& out);
   void consumer(int dev);
   void complete(int dev, long long id, bool notify, double ms, const std::string& err);
+  struct Wake {
+    bool comp = false, done = false, work = false;
+  };
+  void complete_locked(int dev, long long id, bool notify, double ms, const std::string& err, Wake& w);
+  void wake(const Wake& w);
   int retire(int dev, std::vector<Inflight>& inflight);
 
   std::vector<std::shared_ptr<Cores>> devs_;
