@@ -6,15 +6,21 @@
 
 namespace cek {
 
+// a consumer's own counter: one writer, readers only sum
 static void add_ms(std::atomic<double>& a, double v) {
-  double cur = a.load(std::memory_order_relaxed);
-  while (!a.compare_exchange_weak(cur, cur + v, std::memory_order_relaxed)) {
-  }
+  a.store(a.load(std::memory_order_relaxed) + v, std::memory_order_relaxed);
 }
+static void add_one(std::atomic<long long>& a) { a.store(a.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed); }
 
 std::vector<double> DevicePool::host_profile() {
-  return {prof_issue_ms_.load(), prof_retire_ms_.load(), static_cast<double>(prof_tasks_.load()),
-          static_cast<double>(prof_polls_.load())};
+  std::vector<double> r(4, 0.0);
+  for (int i = 0; i < num_devices(); ++i) {
+    r[0] += prof_[i].issue_ms.load();
+    r[1] += prof_[i].retire_ms.load();
+    r[2] += static_cast<double>(prof_[i].tasks.load());
+    r[3] += static_cast<double>(prof_[i].polls.load());
+  }
+  return r;
 }
 
 DevicePool::DevicePool(std::vector<std::shared_ptr<Cores>> devices, int max_in_flight, int policy)
@@ -29,6 +35,7 @@ DevicePool::DevicePool(std::vector<std::shared_ptr<Cores>> devices, int max_in_f
   busy_ms_.assign(devs_.size(), 0.0);
   inflight_.assign(devs_.size(), 0);
   speed_.assign(devs_.size(), Speed());
+  prof_.reset(new Prof[devs_.size()]);
   for (int i = 0; i < num_devices(); ++i) threads_.emplace_back([this, i] { consumer(i); });
 }
 
@@ -324,8 +331,8 @@ void DevicePool::consumer(int dev) {
       const double r0 = now_ms();
       const int done = retire(dev, inflight);
       const double r1 = now_ms();
-      add_ms(prof_retire_ms_, r1 - r0);
-      prof_polls_.fetch_add(1, std::memory_order_relaxed);
+      add_ms(prof_[dev].retire_ms, r1 - r0);
+      add_one(prof_[dev].polls);
       if (done > 0) last_progress = r1;
     }
     issued = false;
@@ -413,8 +420,8 @@ void DevicePool::consumer(int dev) {
           ++deferred;
         else
           flush();  // this task's marker covers its stream; record the others'
-        add_ms(prof_issue_ms_, now_ms() - i0);
-        prof_tasks_.fetch_add(1, std::memory_order_relaxed);
+        add_ms(prof_[dev].issue_ms, now_ms() - i0);
+        add_one(prof_[dev].tasks);
         auto m = cr.last_marker(0);
         inflight.push_back({t.id, notify, m.first, m.second, t0});
         issued = true;

@@ -206,8 +206,13 @@ class DevicePool {
   };
   std::vector<Speed> speed_;
   std::vector<std::thread> threads_;
-  std::atomic<double> prof_issue_ms_{0}, prof_retire_ms_{0};
-  std::atomic<long long> prof_tasks_{0}, prof_polls_{0};
+  // host-time profile, one cache line per consumer (written by that consumer
+  // only: shared counters bounced one line between 8 consumer threads)
+  struct alignas(64) Prof {
+    std::atomic<double> issue_ms{0}, retire_ms{0};
+    std::atomic<long long> tasks{0}, polls{0};
+  };
+  std::unique_ptr<Prof[]> prof_;
 };
 
 }  // namespace cek
