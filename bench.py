@@ -911,6 +911,21 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+def _wait_for_exit(pids, timeout_s: float = 60.0) -> None:
+    """Until every process in ``pids`` has exited (or is a zombie waiting
+    for its parent), at most ``timeout_s``."""
+    def alive(pid: int) -> bool:
+        try:
+            with open(f"/proc/{pid}/stat") as f:
+                return f.read().rsplit(")", 1)[1].split()[0] != "Z"
+        except (OSError, IndexError):
+            return False
+
+    t_end = time.time() + timeout_s
+    while time.time() < t_end and any(alive(p) for p in pids):
+        time.sleep(0.05)
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(argv)
@@ -936,11 +951,20 @@ def main(argv=None) -> int:
             rowc = _row_major_comparison(args.steps)
         except Exception as e:  # pragma: no cover
             rowc = {"error": repr(e)[:300]}
+    others = []
     if ctx.is_distributed:
         import torch.distributed as dist
 
+        pids = [None] * ctx.world
+        dist.all_gather_object(pids, os.getpid())
+        others = [p for r, p in enumerate(pids) if r != ctx.rank]
         dist.barrier()
         dist.destroy_process_group()  # the other ranks exit here; rank 0 goes on alone
+    if ctx.rank == 0 and others:
+        # the timing measurements below start once the other ranks have gone
+        # (their teardown, 7 GPU contexts when ranks share a GPU, disturbed
+        # 10 calls of the load-balance measurement in an 8-rank rehearsal)
+        _wait_for_exit(others, timeout_s=60.0)
     lb = bench_lb_iters() if (ctx.rank == 0 and use_gpu) else {}
     slices = {}
     if ctx.rank == 0 and use_gpu and args.size == 8192:
