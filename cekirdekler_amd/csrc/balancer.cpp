@@ -230,7 +230,7 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
       best = static_cast<size_t>(fs.probe_dev);
     } else if (fs.single_wall[best] < 0) {
       const double guess = fs.a[best] + fs.b[best] * static_cast<double>(total);
-      if (!fs.probed[best] && guess <= 1.25 * pred_multi) {
+      if (!fs.probed[best] && guess <= kProbeGate * pred_multi) {
         fs.probed[best] = 1;
         fs.probe_left = kProbeCalls;
         fs.probe_dev = static_cast<int>(best);

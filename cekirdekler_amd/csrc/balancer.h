@@ -22,7 +22,7 @@ namespace cek {
 // whose best share is below one step gets none) and predicts that split's
 // wall time as T + the measured multi-device overhead (wall − slowest
 // device).  The best single device is then run alone for a few calls, once,
-// when its predicted time is within 25 % of that, and from then on the
+// when its predicted time is within 50 % of that (kProbeGate), and then the
 // configuration with the lower wall time is used: measured for the single
 // device; for the split the larger of the prediction and the measured wall
 // of recent split calls (a fit that misses a cost of co-execution — a CPU
@@ -66,6 +66,13 @@ constexpr double kGuardMargin = 0.97;
 // alone for kProbeCalls computes; its wall time is the minimum over the
 // recorded ones.
 constexpr int kProbeCalls = 3;
+// The best single device is probed (once) when its fitted time alone is
+// within this factor of the split's predicted time.  Its fit comes from
+// calls it shared with the others, and sharing can slow a device a lot: a
+// CPU device streaming host memory next to a GPU's DMA on the same memory
+// measured 4.35 ms per range by its shared-call fit and 2.4-2.6 ms alone
+// (hetero_stream, iters 1), so a tight gate never measures what it would save.
+constexpr double kProbeGate = 1.5;
 
 // Records the last compute of this id (its ranges, per-device ms and wall ms;
 // `warm` = not one of the id's first computes) and, when every device has a
