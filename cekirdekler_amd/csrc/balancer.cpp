@@ -135,10 +135,17 @@ bool predict_split(FitState& fs, const std::vector<double>& bench, double wall_m
   };
   if (warm && active > 0 && wall_ms > 0 && by_law) {
     fs.law_settled = settled ? fs.law_settled + 1 : 0;
-    // the best settled law call: the guard compares against what the law
-    // has been seen to do (an average would keep the slow first settled
-    // calls — a host-resident stream's first calls are several times slower)
-    if (fs.law_settled >= 3) fs.law_wall = fs.law_wall < 0 ? wall_ms : std::min(fs.law_wall, wall_ms);
+    // the median of the last settled law calls: what the law does now (an
+    // average over every settled call would keep the slow first ones — a
+    // host-resident stream's first calls are several times slower — and a
+    // minimum keeps one lucky call)
+    if (fs.law_settled >= 3) {
+      fs.law_walls.push_back(wall_ms);
+      if (static_cast<int>(fs.law_walls.size()) > kLawWalls) fs.law_walls.erase(fs.law_walls.begin());
+      std::vector<double> v = fs.law_walls;
+      std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+      fs.law_wall = v[v.size() / 2];
+    }
     if (active >= 2) {
       const double ov = std::max(0.0, wall_ms - tmax);
       fs.o_multi = fs.o_multi < 0 ? ov : 0.7 * fs.o_multi + 0.3 * ov;

@@ -48,7 +48,8 @@ struct FitState {
   // settled (three calls in a row in which no device's range moved more
   // than 1 % of the total).  The predictor deviates from the law only after this is
   // known and only to a configuration not measured slower than it.
-  double law_wall = -1;                // best wall ms of settled law calls (−1: not yet)
+  double law_wall = -1;                // median wall ms of the last settled law calls (−1: not yet)
+  std::vector<double> law_walls;       // the last kLawWalls settled law calls' wall ms
   int law_settled = 0;                 // consecutive settled law calls
   std::vector<long long> prev_ranges;  // the ranges of the previous recorded call
   // the last split the law chose: restored when the predictor hands back to
@@ -60,6 +61,10 @@ constexpr int kFitSamples = 8;
 // the predictor keeps a configuration only while it is measured at least
 // 3 % faster than the law's best settled call
 constexpr double kGuardMargin = 0.97;
+// settled law calls the guard's reference is the median of (a minimum kept
+// one lucky call: a 0.023 ms wave frame against a typical 0.031 made the
+// GPU alone, 0.027, look no faster than the law)
+constexpr int kLawWalls = 5;
 // The first compute after the set of devices with a share changed is not
 // recorded: it pays the move (slices going up to their new device), a cost
 // of the switch, not of the split.  A probe runs the best single device
