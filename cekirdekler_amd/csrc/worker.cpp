@@ -1,6 +1,7 @@
 #include "worker.h"
 
 #include <map>
+#include <unistd.h>
 #include <set>
 
 #include <algorithm>
@@ -40,7 +41,7 @@ static bool pool_may_spin() {
   return g_pool_spin_us > 0 && g_pool_threads.load(std::memory_order_relaxed) < cores;
 }
 
-CpuPool::CpuPool(int threads) {
+CpuPool::CpuPool(int threads) : pid_(static_cast<long>(getpid())) {
   for (int i = 1; i < threads; ++i) threads_.emplace_back([this] { loop(); });
   g_pool_threads += static_cast<int>(threads_.size());
 }
@@ -102,6 +103,8 @@ std::shared_ptr<CpuPool> CpuPool::shared(int threads, int slot) {
   std::lock_guard<std::mutex> g(mu);
   auto& w = pools[{threads, slot}];
   auto p = w.lock();
+  // a pool inherited through fork() has no threads in this process
+  if (p && p->pid_ != static_cast<long>(getpid())) p.reset();
   if (!p) {
     p = std::make_shared<CpuPool>(threads);
     w = p;

@@ -82,6 +82,7 @@ class CpuPool {
 
  private:
   void loop();
+  long pid_ = 0;  // the process that started the threads (a forked child has none of them)
   std::mutex call_mu_;  // one parallel_for at a time
   std::vector<std::thread> threads_;
   std::mutex mu_;

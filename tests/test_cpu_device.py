@@ -465,3 +465,39 @@ def test_cpu_pool_shared_between_crunchers_and_safe_concurrently(cpu):
     finally:
         for c in (a, b, two):
             c.dispose()
+
+
+def test_cpu_pool_not_reused_across_fork(cpu):
+    """A process forked after a CPU cruncher exists builds its own pool: the
+    parent's pool threads do not exist in the child (a shared pool reused
+    there would wait for them forever)."""
+    import os
+
+    cr = ck.ClNumberCruncher(cpu, SRC)
+    x = ck.ClArray(np.zeros(1 << 14, np.float32))
+    x.compute(cr, 1, "inc", 1 << 14, 256)
+    pid = os.fork()
+    if pid == 0:  # child: a new cruncher of the same size, one compute
+        code = 3
+        try:
+            c2 = ck.ClNumberCruncher(cpu, SRC)
+            y = ck.ClArray(np.zeros(1 << 14, np.float32))
+            y.compute(c2, 1, "inc", 1 << 14, 256)
+            code = 0 if float(y.array.sum()) == float(1 << 14) else 4
+        finally:
+            os._exit(code)
+    import time
+
+    t_end = time.time() + 60
+    while True:
+        done, status = os.waitpid(pid, os.WNOHANG)
+        if done:
+            break
+        if time.time() > t_end:
+            os.kill(pid, 9)
+            os.waitpid(pid, 0)
+            raise AssertionError("forked child hung on the CPU pool")
+        time.sleep(0.05)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status
+    assert float(x.array.sum()) == float(1 << 14)
+    cr.dispose()
