@@ -324,10 +324,21 @@ void DevicePool::consumer(int dev) {
       deferred = 0;
     }
   };
+  int last_lim = max_in_flight_;
+  int issues_since_poll = 0;
+  static const int poll_every = [] {  // CEK_POOL_POLL_EVERY: issues between polls while flowing
+    const char* e = std::getenv("CEK_POOL_POLL_EVERY");
+    return std::max(1, std::min(64, e ? std::atoi(e) : kPollBatch));
+  }();
   for (;;) {
     // while tasks keep flowing, poll the markers only once a few are in
-    // flight: each poll is a HIP call that costs about as much as a launch
-    if (!inflight.empty() && !(issued && static_cast<int>(inflight.size()) < kPollBatch)) {
+    // flight, and then every kPollBatch issues or when the queue-depth limit
+    // is about to stop the issuing: each poll is a HIP call that costs about
+    // as much as a launch, and a batch of tasks sharing a marker cannot
+    // retire before its marker is recorded anyway
+    const int nin = static_cast<int>(inflight.size());
+    if (nin > 0 && (!issued || (nin >= kPollBatch && (issues_since_poll >= poll_every || nin + 1 >= last_lim)))) {
+      issues_since_poll = 0;
       const double r0 = now_ms();
       const int done = retire(dev, inflight);
       const double r1 = now_ms();
@@ -342,6 +353,7 @@ void DevicePool::consumer(int dev) {
     {
       std::unique_lock<std::mutex> lk(mu_);
       lim = limit_locked();
+      last_lim = lim;
       if (static_cast<int>(inflight.size()) < lim) got = take_locked(dev, it);
       more = !queue_.empty();
       if (!got && inflight.empty()) {
@@ -425,6 +437,7 @@ void DevicePool::consumer(int dev) {
         auto m = cr.last_marker(0);
         inflight.push_back({t.id, notify, m.first, m.second, t0});
         issued = true;
+        ++issues_since_poll;
       } else {
         cr.compute(call);
         complete(dev, t.id, notify, now_ms() - t0, "");
