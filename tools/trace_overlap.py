@@ -25,7 +25,8 @@ def rows(pattern):
     return list(csv.DictReader(open(f[0]))) if f else []
 
 
-ks = [r for r in rows("*kernel_trace.csv") if kernel in r["Kernel_Name"]]
+allk = rows("*kernel_trace.csv")
+ks = [r for r in allk if kernel in r["Kernel_Name"]]
 ks.sort(key=lambda r: int(r["Start_Timestamp"]))
 if len(ks) < 2 * blobs:
     raise SystemExit(f"only {len(ks)} '{kernel}' dispatches")
@@ -47,7 +48,13 @@ def direction(r):
 
 ups = [r for r in cp if direction(r) == "h2d" and int(r["End_Timestamp"]) > t_prev and int(r["Start_Timestamp"]) < k_end]
 downs = [r for r in cp if direction(r) == "d2h" and int(r["Start_Timestamp"]) > t_prev]
-downs = [r for r in downs if int(r["Start_Timestamp"]) <= k_end + 5_000_000]
+# ROCclr runs device-to-host copies into pinned memory as blit kernels
+# (__amd_rocclr_copyBuffer) on a hardware queue: those count as downloads
+downs += [r for r in allk if "copyBuffer" in r["Kernel_Name"] and int(r["Start_Timestamp"]) > t_prev]
+# this call's downloads: after its first kernel ends (earlier ones finish the
+# previous call's blobs), before 5 ms past its last kernel
+k_first_end = min(int(r["End_Timestamp"]) for r in call)
+downs = [r for r in downs if k_first_end <= int(r["Start_Timestamp"]) <= k_end + 5_000_000]
 w0 = min([int(r["Start_Timestamp"]) for r in ups + call])
 w1 = max([int(r["End_Timestamp"]) for r in downs + call])
 
@@ -75,8 +82,9 @@ print(f"window {win / 1e6:.3f} ms; busy: " + ", ".join(f"{k} {v / 1e6:.3f} ms" f
 print(f"copies in the window: {len(ups)} uploads, {len(downs)} downloads; kernels {len(call)}\n")
 print("| # | what | queue / engine | start µs | end µs |")
 print("|---|---|---|---|---|")
-ev = [("H2D", r) for r in ups] + [("kernel", r) for r in call] + [("D2H", r) for r in downs]
+ev = [("H2D", r) for r in ups] + [("kernel", r) for r in call] + \
+    [("D2H" + (" (blit kernel)" if "Kernel_Name" in r else ""), r) for r in downs]
 ev.sort(key=lambda p: int(p[1]["Start_Timestamp"]))
 for i, (what, r) in enumerate(ev):
-    lane = r.get("Queue_Id") or r.get("Stream_Id") or r.get("Engine_Id") or r.get("Dst_Agent_Id") or ""
+    lane = ("queue " + r["Queue_Id"]) if r.get("Queue_Id") else ("SDMA, stream " + (r.get("Stream_Id") or "?"))
     print(f"| {i} | {what} | {lane} | {(int(r['Start_Timestamp']) - w0) / 1e3:.1f} | {(int(r['End_Timestamp']) - w0) / 1e3:.1f} |")
