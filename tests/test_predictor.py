@@ -178,3 +178,16 @@ def test_guard_hands_back_the_law_split_after_a_single_device_probe():
     ranges, walls, dec, fs = _simulate(a, b, 0.01, 0.005, calls=80)
     assert "probe" in dec
     assert all(r > 0 for r in ranges), (ranges, dec)
+
+
+def test_guard_reference_is_the_median_of_settled_law_calls():
+    """The guard compares a candidate with the MEDIAN of the law's last
+    settled calls (kLawWalls): one lucky fast call must not become the bar
+    every other configuration has to beat (a minimum kept it)."""
+    fs = cek.FitState()
+    ranges = [51_200, 51_200]
+    walls = [10.0, 10.0, 10.0, 10.0, 10.0, 4.0, 10.0, 10.0]
+    for call, w in enumerate(walls):
+        ok, new, dec = cek.predict_split([w - 0.1, w - 0.2], w, 102_400, list(ranges), 256, fs, call >= 2)
+        assert dec == "law"
+    assert fs.law_wall == pytest.approx(10.0), fs.law_wall
