@@ -137,3 +137,29 @@ def test_run_child_reports_errors_and_kills_hung_children(tmp_path):
         time.sleep(0.1)
     else:
         pytest.fail("the hung child's grandchild survived")
+
+
+def test_wait_for_exit_waits_for_live_ranks_only():
+    """Rank 0 starts its timing extras once the other ranks' processes are
+    gone (bench._wait_for_exit): it returns at once for PIDs that do not
+    exist, waits for a live one, and gives up after its time limit."""
+    import time
+
+    bench = _bench_module()
+    t = time.time()
+    bench._wait_for_exit([2 ** 22 + 12345], timeout_s=5.0)  # no such process
+    assert time.time() - t < 1.0
+    p = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(1.0)"])
+    t = time.time()
+    bench._wait_for_exit([p.pid], timeout_s=10.0)
+    waited = time.time() - t
+    p.wait()
+    assert 0.5 < waited < 8.0, waited
+    q = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(30)"])
+    try:
+        t = time.time()
+        bench._wait_for_exit([q.pid], timeout_s=0.5)
+        assert 0.4 < time.time() - t < 3.0
+    finally:
+        q.kill()
+        q.wait()
