@@ -149,7 +149,7 @@ def eight_logical_dispatch():
     for _ in range(3):
         try:
             out = subprocess.run([_sys.executable, os.path.join(root, "tools", "pool_env_probe.py"), "logical8"],
-                                 capture_output=True, text=True, timeout=120, cwd=root)
+                                 capture_output=True, text=True, timeout=40, cwd=root)
             line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
             runs.append(_json.loads(line)["logical8"]["tasks_per_s"])
         except Exception:  # noqa: BLE001  (reported as null)
